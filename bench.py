@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""Throughput of the embedding hot path on MI355X (BASELINE.json metric).
+
+Workload (N=1 default): BASELINE.json configs[1] — WavLM-base, bf16, batch 256 x 3 s @ 16 kHz
+synthetic clips -> embeddings of hidden states [12, 11, 10, 6] (REF/WavLM_embeddings.py:506).
+A "step" = one sse_embed call over the rank's batch of 256 clips (conv frontend ->
+projection -> pos-conv -> 12 encoder layers -> pooling), inputs resident in HBM; with N > 1
+each rank processes its own 256 clips (weak scaling, clip-sharded corpus, configs[3]) and
+the step ends with one RCCL all-gather of the [256, 4, 768] fp32 embeddings.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 the driver uses
+torch.distributed.run (one rank per GPU, RANK/LOCAL_RANK/WORLD_SIZE from the env).
+
+The JSON line carries:
+  roofline      dominant kernel (most device time in the timed region): algorithmic FLOPs
+                per launch / its mean launch time, both from HIP events recorded around every
+                launch on the launch stream inside the timed region (sse_profile_*).
+  cpu_baseline  the numpy oracle ("port") on this host's cores, a bounded sample of clips
+                (rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+importlib.import_module("stuttering-speech-representation_amd")
+from ssr_amd import config as C, synth  # noqa: E402
+from ssr_amd.model import SSEModel  # noqa: E402
+
+# Algorithmic FLOPs per clip: 2 x MACs of every GEMM/conv + QK^T, AV.
+FLOP_PER_CLIP = {"wavlm-base": 42.39e9, "whisper-large-v2": 2272.67e9}
+PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}          # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", default="wavlm-base", choices=["wavlm-base", "whisper-large-v2"])
+    ap.add_argument("--batch", type=int, default=None, help="clips per rank per step (default 256 / 64)")
+    ap.add_argument("--seconds", type=float, default=None, help="clip length (default 3 s / 30 s)")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--cpu-sample", type=int, default=None, help="clips for the CPU baseline (0 = skip)")
+    ap.add_argument("--no-profile", action="store_true", help="skip the per-launch event timing")
+    return ap.parse_args()
+
+
+def cpu_baseline(model_name: str, n: int, seconds: float):
+    """The oracle (numpy restatement of the reference path, batch-1 loop like the reference)
+    timed on this host's cores.  Test infrastructure used only as the reported baseline."""
+    from threadpoolctl import threadpool_info
+    if model_name == "wavlm-base":
+        from oracle.wavlm import WavLMOracle
+        spec = C.WAVLM_BASE
+        o = WavLMOracle(spec, synth.synth_wavlm_state_dict(spec, seed=7))
+        clips = synth.synth_clips(n + 1, int(16000 * seconds), seed=2024)
+        o.embed(clips[:1], spec.default_layer_indices())            # warm-up (BLAS threads, page-in)
+        t0 = time.perf_counter()
+        o.embed(clips[1:], spec.default_layer_indices())
+        dt = time.perf_counter() - t0
+    else:
+        from oracle.whisper import WhisperOracle
+        spec = C.WHISPER_LARGE_V2
+        o = WhisperOracle(spec, synth.synth_whisper_state_dict(spec, seed=11))
+        clips = synth.synth_clips(n, int(16000 * seconds), seed=2024)
+        t0 = time.perf_counter()
+        o.embed(clips, spec.default_layer_indices())
+        dt = time.perf_counter() - t0
+    threads = max([p.get("num_threads", 1) for p in threadpool_info()] + [1])
+    return {"value": round(n / dt, 4), "unit": "clips/s", "cores": int(threads), "kind": "port",
+            "sample": f"{n} synthetic {seconds:g} s clips, batch-1 loop of oracle/{model_name.split('-')[0]}.py "
+                      f"(numpy fp32, {threads} BLAS threads, host {os.cpu_count()} CPUs), {dt:.1f} s"}
+
+
+def roofline(records, dtype):
+    """Dominant kernel over the timed region: the kernel symbol (tag prefix) with most time."""
+    by_kernel = {}
+    for tag, ms, fl, by in records:
+        k = tag.split(":", 1)[0]
+        d = by_kernel.setdefault(k, [0.0, 0.0, 0.0, 0])
+        d[0] += ms
+        d[1] += fl
+        d[2] += by
+        d[3] += 1
+    total = sum(v[0] for v in by_kernel.values())
+    name, (ms, fl, by, n) = max(by_kernel.items(), key=lambda kv: kv[1][0])
+    achieved = fl / (ms * 1e-3) / 1e12
+    peak = PEAK_TFLOPS[dtype]
+    breakdown = {k: {"ms": round(v[0], 3), "launches": v[3], "share": round(v[0] / total, 4),
+                     "tflops": round(v[1] / max(v[0], 1e-9) / 1e9, 1)} for k, v in sorted(by_kernel.items())}
+    return {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": None,
+            "flop_per_launch": fl / n, "mean_launch_ms": round(ms / n, 4), "launches": n,
+            "device_ms_per_step_sum": None, "breakdown": breakdown}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("for --gpus > 1 launch with torch.distributed.run (one process per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    wavlm = a.model == "wavlm-base"
+    spec = C.WAVLM_BASE if wavlm else C.WHISPER_LARGE_V2
+    B = a.batch or (256 if wavlm else 64)
+    secs = a.seconds or (3.0 if wavlm else 30.0)
+    L = int(16000 * secs)
+    sd = synth.synth_state_dict(spec)
+    model = SSEModel(spec, sd, device=dev, dtype=a.dtype)
+    del sd
+    idx = spec.default_layer_indices()
+    clips = torch.from_numpy(synth.synth_clips(B, L, seed=1234, first_clip=rank * B)).to(dev)
+    out = torch.empty((B, len(idx), spec.hidden), dtype=torch.float32, device=dev)
+    gathered = torch.empty((world * B, len(idx), spec.hidden), dtype=torch.float32, device=dev) if world > 1 else None
+
+    def step():
+        model.embed(clips, idx, out=out)
+        if dist is not None:
+            dist.all_gather_into_tensor(gathered, out)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if not a.no_profile:
+        model.profile_start(max_launches=200 * max(a.steps, 1))
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    records = model.profile_read() if not a.no_profile else []
+    if not a.no_profile:
+        model.profile_stop()
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t_max = float(t.item())
+    clips_total = world * B * a.steps
+    value = clips_total / t_max
+
+    if rank == 0:
+        res = {
+            "metric": "clips/sec (3 s@16 kHz) embedding extraction" if wavlm else "clips/sec (30 s) embedding extraction",
+            "value": round(value, 2), "unit": "clips/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(1e3 * t_max / a.steps, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": a.dtype,
+            "data": "synthetic 16 kHz clips (splitmix64 Gaussian+tones), random-init weights of the real architecture",
+            "config": {"workload": f"{spec.name} {a.dtype} embeddings, {B} x {secs:g} s clips per GPU per step"
+                                   + (", RCCL all-gather of [B,4,H] per step" if world > 1 else ""),
+                       "model": spec.name, "global_batch": world * B, "clip_samples": L,
+                       "layers_pooled": idx, "parallelism": f"clip-sharded dp{world}"},
+        }
+        if records:
+            rf = roofline(records, a.dtype)
+            rf["device_ms_per_step_sum"] = round(sum(r[1] for r in records) / a.steps, 3)
+            res["roofline"] = rf
+        res["model_flops_frac"] = round(value / world * FLOP_PER_CLIP[a.model] / 1e12 / PEAK_TFLOPS[a.dtype], 4)
+        ncpu = a.cpu_sample if a.cpu_sample is not None else (8 if wavlm else 1)
+        if world == 1 and ncpu > 0:
+            res["cpu_baseline"] = cpu_baseline(a.model, ncpu, secs)
+        print(json.dumps(res), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

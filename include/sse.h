@@ -1,0 +1,143 @@
+/*
+ * sse.h — C-ABI of libsse.so, the MI355X (gfx950) speech-embedding extractor.
+ *
+ * The reference (warren-machy/stuttering-speech-representation) has no native FFI: its
+ * operator API for the hot path is the HF object pair handed to its glue functions
+ * (SURVEY.md §8(b)).  Each entry point below replaces one piece of that Python surface:
+ *
+ *   sse_model_create    <- WavLMModel.from_pretrained(...).to(device)      REF/WavLM_embeddings.py:482-483
+ *                          WhisperModel.from_pretrained(...).to(device)    REF/whisper_embeddings_large.py:437-438
+ *   sse_logmel          <- WhisperProcessor(audio, sampling_rate=16000)   REF/whisper_embeddings_large.py:242-246
+ *                          (HF/models/whisper/feature_extraction_whisper.py:135-168)
+ *   sse_embed           <- fe(audio) -> model(..., output_hidden_states=True) -> torch.mean(hs[idx], dim=1)
+ *                          REF/WavLM_embeddings.py:289-323, REF/whisper_embeddings_large.py:242-281
+ *   sse_hidden_states   <- model(input_values, output_hidden_states=True).hidden_states
+ *                          REF/WavLM_embeddings.py:249-265 (get_model_layer_info), :302-310
+ *   sse_model_destroy   <- del model / torch.cuda.empty_cache()            REF/WavLM_embeddings.py:630
+ *
+ * Conventions: plain pointers and sizes only.  Every d_* pointer is DEVICE memory owned by
+ * the caller; the handle owns only the weights and derived tables.  Calls other than
+ * sse_model_create / sse_model_destroy are asynchronous on `stream` (a hipStream_t, passed
+ * as void*; NULL = the legacy default stream) and perform no host synchronisation, so they
+ * may be captured into a hipGraph.  Return value 0 = success, negative = error (see
+ * sse_strerror).  A handle is bound to one device; concurrent calls are safe on distinct
+ * streams with distinct workspaces.
+ */
+#ifndef SSE_H
+#define SSE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum sse_kind { SSE_KIND_WAVLM = 0, SSE_KIND_WHISPER = 1 };
+enum sse_dtype { SSE_DTYPE_F32 = 0, SSE_DTYPE_BF16 = 1 };
+enum sse_err {
+  SSE_OK = 0,
+  SSE_ERR_INVALID = -1,      /* bad argument / null pointer / bad layer index         */
+  SSE_ERR_HIP = -2,          /* a HIP runtime call failed (launch, copy, malloc)       */
+  SSE_ERR_UNSUPPORTED = -3,  /* shape outside what the kernels implement              */
+  SSE_ERR_WORKSPACE = -4,    /* ws_bytes < sse_workspace_bytes(...)                    */
+  SSE_ERR_WEIGHTS = -5,      /* host weight blob size does not match the config        */
+  SSE_ERR_OOM = -6           /* device allocation failed (torch.OutOfMemoryError twin) */
+};
+
+/* Model shape.  Field meaning follows the HF configs (WavLMConfig / WhisperConfig). */
+typedef struct sse_cfg {
+  int32_t kind;              /* sse_kind                                              */
+  int32_t hidden;            /* hidden_size / d_model                                 */
+  int32_t layers;            /* num_hidden_layers / encoder_layers                    */
+  int32_t heads;             /* num_attention_heads / encoder_attention_heads         */
+  int32_t ffn;               /* intermediate_size / encoder_ffn_dim                   */
+  /* WavLM conv feature encoder */
+  int32_t n_conv;            /* 7                                                     */
+  int32_t conv_dim[8];
+  int32_t conv_kernel[8];
+  int32_t conv_stride[8];
+  int32_t conv_bias;         /* 0/1                                                   */
+  int32_t feat_norm_layer;   /* 0: GroupNorm on conv0 ("group"); 1: LN after each conv */
+  int32_t stable_layer_norm; /* 0: post-LN encoder (base); 1: pre-LN + final LN (large) */
+  int32_t pos_kernel;        /* 128                                                   */
+  int32_t pos_groups;        /* 16                                                    */
+  int32_t num_buckets;       /* 320                                                   */
+  int32_t max_distance;      /* 800                                                   */
+  int32_t do_normalize;      /* Wav2Vec2FeatureExtractor.do_normalize                 */
+  /* Whisper */
+  int32_t n_mels;            /* 80                                                    */
+  int32_t max_positions;     /* 1500                                                  */
+  float ln_eps;              /* 1e-5                                                  */
+} sse_cfg;
+
+typedef struct sse_model sse_model;
+
+/* Number of fp32 values the weight blob must hold for `cfg` (canonical HF-key order,
+ * mirrored by config.param_specs() on the host side). */
+size_t sse_weight_floats(const sse_cfg* cfg);
+
+/* Upload + repack weights (weight-norm folded, conv kernels reshaped to [out][k*in],
+ * QKV concatenated, bf16 cast if dtype == SSE_DTYPE_BF16, relative-position bias table
+ * precomputed).  Synchronous.  `host_weights` is fp32, `nbytes` = 4 * sse_weight_floats. */
+int sse_model_create(const sse_cfg* cfg, const float* host_weights, size_t nbytes,
+                     int device, int dtype, sse_model** out);
+void sse_model_destroy(sse_model* m);
+
+/* Frames the encoder produces for L input samples (WavLM conv stack; Whisper: 1500). */
+int sse_output_frames(const sse_model* m, int L);
+
+/* Device workspace needed by sse_embed / sse_hidden_states for B clips of L samples. */
+size_t sse_workspace_bytes(const sse_model* m, int B, int L);
+
+/* Whisper front end: d_wave [B][L] fp32 (L <= 480000, zero-padded to 30 s like
+ * WhisperFeatureExtractor) -> d_mel [B][n_mels][3000] fp32.  Needs
+ * sse_logmel_workspace_bytes(B) of workspace. */
+size_t sse_logmel_workspace_bytes(int B, int n_mels);
+int sse_logmel(const float* d_wave, int B, int L, int n_mels, float* d_mel,
+               void* d_ws, size_t ws_bytes, void* stream);
+
+/* Fused embedding path: d_in = raw 16 kHz waves [B][L] fp32 (WavLM and Whisper; Whisper
+ * computes its log-mel in-stream) -> d_out [B][n_layers][hidden] fp32, the time-mean of
+ * hidden_states[layer_ids[i]]. */
+int sse_embed(sse_model* m, const float* d_in, int B, int L, const int32_t* layer_ids,
+              int n_layers, float* d_out, void* d_ws, size_t ws_bytes, void* stream);
+
+/* Same forward, materialising every hidden state: d_hs [layers+1][B][T][hidden] fp32. */
+int sse_hidden_states(sse_model* m, const float* d_in, int B, int L, float* d_hs,
+                      void* d_ws, size_t ws_bytes, void* stream);
+
+/* Whisper encoder from an HF-layout log-mel (model.encoder(input_features) twin,
+ * REF/whisper_embeddings_large.py:250-254): d_mel [B][n_mels][3000] fp32 ->
+ * d_hs [layers+1][B][1500][hidden] fp32.  Workspace: sse_workspace_bytes(m, B, 480000). */
+int sse_whisper_hidden_states_from_mel(sse_model* m, const float* d_mel, int B, float* d_hs, void* d_ws,
+                                       size_t ws_bytes, void* stream);
+
+/* Wav2Vec2FeatureExtractor zero_mean_unit_var_norm on device (feature_extraction_wav2vec2.py:94):
+ * d_out[b] = (d_in[b] - mean_b) / sqrt(var_b + 1e-7).  Workspace: 8 * B bytes. */
+int sse_normalize(const float* d_in, int B, int L, float* d_out, void* d_ws, size_t ws_bytes, void* stream);
+
+size_t sse_normalize_workspace_bytes(int B);
+
+/* Live per-launch timing for benchmarks: after sse_profile_start every kernel launch of
+ * sse_embed / sse_hidden_states is bracketed by two hipEvents on the caller's stream
+ * (at most max_launches per read).  sse_profile_read synchronises on the last event and
+ * returns the number of launches n, filling per launch: tag (32 chars, "<kernel>:<role>"),
+ * elapsed ms, algorithmic FLOPs and algorithmic bytes; then clears the record. */
+int sse_profile_start(sse_model* m, int max_launches);
+int sse_profile_read(sse_model* m, int cap, char* tags, float* ms, double* flops, double* bytes);
+int sse_profile_stop(sse_model* m);
+
+/* Host-only helpers (no device work; usable without a GPU). */
+const char* sse_strerror(int err);
+/* WavLM relative-position bucket of distance d = key - query (HF _relative_positions_bucket). */
+int sse_rel_bucket(int d, int num_buckets, int max_distance);
+/* Whisper Slaney mel filter bank, [n_freq = 201][n_mels] fp32 as HF casts it. */
+int sse_mel_filters(int n_mels, float* out);
+/* Library version string. */
+const char* sse_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SSE_H */

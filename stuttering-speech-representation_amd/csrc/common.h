@@ -1,0 +1,85 @@
+// Internal helpers shared by the gfx950 kernels and the host orchestration.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+#define SSE_DEV __device__ __forceinline__
+
+// Address-space casts for global_load_lds.
+#define GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
+#define LPTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+SSE_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+template <typename T> SSE_DEV T from_f32(float v);
+template <> SSE_DEV float from_f32<float>(float v) { return v; }
+template <> SSE_DEV bf16 from_f32<bf16>(float v) { return (bf16)v; }
+SSE_DEV float to_f32(float v) { return v; }
+SSE_DEV float to_f32(bf16 v) { return (float)v; }
+
+SSE_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+SSE_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+SSE_DEV double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Epilogue activation codes.
+enum { ACT_NONE = 0, ACT_GELU = 1 };
+
+// ---------------------------------------------------------------------------------------
+// GEMM descriptor.  C[m][n] = sum_k A(m, k) * Bt[n][k]  (+bias[n]) (act) (+resid[m][n]).
+// A(m, k) addressing:
+//   SEG  : A + (m / rows_per_seg) * seg_stride + (m % rows_per_seg) * lda + k
+//          (plain GEMM: rows_per_seg = M, lda = K; strided conv without padding:
+//           rows_per_seg = T_out, seg_stride = T_in*C, lda = stride*C, K = k*C)
+//   CONV : padded (grouped) conv over channels-last input [seg][T_in][ld_in]:
+//          j = k / cin, c = k % cin, t_in = (m % T_out) * stride + j - pad,
+//          A + ((m / T_out) * T_in + t_in) * ld_in + group * cin + c, zero outside [0, T_in)
+// Columns beyond K (k >= K) read as zero on both operands.
+// ---------------------------------------------------------------------------------------
+struct GemmArgs {
+  const void* A;
+  const void* B;        // [groups][N][K] row-major (K contiguous)
+  int M, N, K;
+  int rows_per_seg;     // SEG / CONV (= T_out)
+  long long seg_stride; // SEG
+  long long lda;        // SEG
+  int T_in, stride, pad, cin, ld_in;   // CONV
+  const float* bias;    // [groups*N] or null
+  const float* resid;   // [M][ldc] fp32 or null (row m % resid_rows when resid_rows > 0)
+  int resid_rows;       // 0: resid row = m; >0: periodic residual (Whisper embed_positions)
+  float* Cf;            // fp32 out [M][ldc] or null
+  void* Ct;             // element-type out [M][ldc] or null
+  int ldc;
+  int act;
+  const void* zero;     // >= 64 zero bytes of device memory
+};
+
+enum { AMODE_SEG = 0, AMODE_CONV = 1 };
+
+// Launchers (kernels_gemm.hip).  groups > 1 only with AMODE_CONV (grid.z = group).
+int launch_gemm_bf16(const GemmArgs& a, int amode, int groups, hipStream_t s);
+int launch_gemm_f32(const GemmArgs& a, int amode, int groups, hipStream_t s);
+
+template <typename T> inline int launch_gemm(const GemmArgs& a, int amode, int groups, hipStream_t s);
+template <> inline int launch_gemm<bf16>(const GemmArgs& a, int amode, int groups, hipStream_t s) {
+  return launch_gemm_bf16(a, amode, groups, s);
+}
+template <> inline int launch_gemm<float>(const GemmArgs& a, int amode, int groups, hipStream_t s) {
+  return launch_gemm_f32(a, amode, groups, s);
+}

@@ -1,0 +1,236 @@
+// MFMA GEMM / implicit-GEMM conv for gfx950 (CDNA4).
+//
+// One kernel template serves every dense contraction on the hot path:
+//   K2  WavLM conv1..6           (SEG mode: overlapping rows, A row t = x[s*t : s*t+k] of a clip)
+//   K3  feature projection, K6 QKV / out-proj, K7 FFN, K11 Whisper projections   (plain SEG)
+//   K4  pos-conv (grouped, k=128, pad 64) and K10 Whisper conv1/conv2 (k=3, pad 1)  (CONV mode)
+// Tiles: rows of 128 bytes along K (64 bf16 / 32 f32 per K-step), staged HBM->LDS with
+// global_load_lds_dwordx4 (one 1-KiB wave-instruction = 8 rows), double-buffered, one
+// barrier per K-step.  The LDS image is lane-linear; bank conflicts of the ds_read_b128
+// fragment reads are removed by an XOR swizzle applied to the SOURCE chunk
+// (phys_chunk = chunk ^ ((row >> 1) & 7)), see cdna_hip_programming.md rule 21.
+// Math: v_mfma_f32_16x16x32_bf16 (bf16 path) or v_mfma_f32_16x16x4_f32 (exact-f32 path);
+// both read the same LDS image: lane group q = lane>>4 consumes 16-B chunks q and q+4.
+// Epilogue fuses bias, erf-GELU, fp32 residual add and dual fp32/bf16 stores.
+#include "common.h"
+
+namespace {
+
+template <typename T, int BM, int BN, int WAVES_M, int WAVES_N, int AMODE>
+__global__ __launch_bounds__(WAVES_M * WAVES_N * 64)
+void gemm_kernel(GemmArgs g) {
+  constexpr int NW = WAVES_M * WAVES_N;
+  constexpr int E = 16 / (int)sizeof(T);   // elements per 16-B chunk
+  constexpr int BK = 8 * E;                 // elements per 128-B row
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int A_INSTR = BM / 8, B_INSTR = BN / 8;            // 1-KiB glds pieces per tile
+  constexpr int SA = (A_INSTR + NW - 1) / NW, SB = (B_INSTR + NW - 1) / NW;
+  static_assert(WM % 16 == 0 && WN % 16 == 0, "wave tile");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int n_tiles_n = g.N / BN;
+  const int tile_n = blockIdx.x % n_tiles_n, tile_m = blockIdx.x / n_tiles_n;
+  const int grp = blockIdx.y;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int M = g.M, N = g.N, K = g.K;
+
+  // ---- per-lane source descriptors for the glds pieces this wave issues -------------
+  const char* a_src[SA];
+  int a_chunk[SA];
+  int a_tb[SA], a_to[SA];     // CONV: seg*T_in, t_out*stride - pad
+  #pragma unroll
+  for (int s = 0; s < SA; ++s) {
+    const int piece = wave + NW * s;
+    const int row = piece * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ ((row >> 1) & 7);
+    int m = m0 + row;
+    m = m < M ? m : M - 1;
+    a_chunk[s] = ch;
+    const int seg = m / g.rows_per_seg, r = m - seg * g.rows_per_seg;
+    if (AMODE == AMODE_SEG) {
+      a_src[s] = (const char*)g.A + ((long long)seg * g.seg_stride + (long long)r * g.lda + ch * E) * sizeof(T);
+      a_tb[s] = 0; a_to[s] = 0;
+    } else {
+      a_src[s] = (const char*)g.A;
+      a_tb[s] = seg * g.T_in;
+      a_to[s] = r * g.stride - g.pad;
+    }
+  }
+  const char* b_src[SB];
+  #pragma unroll
+  for (int s = 0; s < SB; ++s) {
+    const int piece = wave + NW * s;
+    const int row = piece * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ ((row >> 1) & 7);
+    const int n = n0 + (row < BN ? row : 0);
+    b_src[s] = (const char*)g.B + (((long long)grp * N + n) * K + ch * E) * sizeof(T);
+  }
+  const int b_kbase = 0;
+  (void)b_kbase;
+
+  auto issue = [&](int kt, int buf) {
+    char* st = smem + buf * STAGE;
+    const int k0 = kt * BK;
+    #pragma unroll
+    for (int s = 0; s < SA; ++s) {
+      const int piece = wave + NW * s;
+      if (piece < A_INSTR) {
+        const void* src;
+        const int k = k0 + a_chunk[s] * E;
+        if (AMODE == AMODE_SEG) {
+          src = k < K ? (const void*)(a_src[s] + (long long)k0 * sizeof(T)) : g.zero;
+        } else {
+          const int j = k / g.cin, c = k - j * g.cin;
+          const int t = a_to[s] + j;
+          src = (k < K && t >= 0 && t < g.T_in)
+                    ? (const void*)((const char*)g.A +
+                                    (((long long)(a_tb[s] + t)) * g.ld_in + grp * g.cin + c) * sizeof(T))
+                    : g.zero;
+        }
+        __builtin_amdgcn_global_load_lds(GPTR(src), LPTR(st + piece * 1024), 16, 0, 0);
+      }
+    }
+    #pragma unroll
+    for (int s = 0; s < SB; ++s) {
+      const int piece = wave + NW * s;
+      if (piece < B_INSTR) {
+        const int row = piece * 8 + (lane >> 3);
+        const int ch = (lane & 7) ^ ((row >> 1) & 7);
+        const int k = k0 + ch * E;
+        const void* src = k < K ? (const void*)(b_src[s] + (long long)k0 * sizeof(T)) : g.zero;
+        __builtin_amdgcn_global_load_lds(GPTR(src), LPTR(st + A_BYTES + piece * 1024), 16, 0, 0);
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+  #pragma unroll
+  for (int i = 0; i < TM; ++i)
+    #pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int q = lane >> 4, r16 = lane & 15;
+  const int nk = (K + BK - 1) / BK;
+  issue(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
+    const char* As = smem + (kt & 1) * STAGE;
+    const char* Bs = As + A_BYTES;
+    if constexpr (sizeof(T) == 2) {
+      #pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 af[TM], bfr[TN];
+        #pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int row = wm * WM + i * 16 + r16;
+          const int pch = (q + 4 * ks) ^ ((row >> 1) & 7);
+          af[i] = *(const bf16x8*)(As + row * 128 + pch * 16);
+        }
+        #pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int row = wn * WN + j * 16 + r16;
+          const int pch = (q + 4 * ks) ^ ((row >> 1) & 7);
+          bfr[j] = *(const bf16x8*)(Bs + row * 128 + pch * 16);
+        }
+        #pragma unroll
+        for (int i = 0; i < TM; ++i)
+          #pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+      f32x4 a0[TM], a1[TM], b0[TN], b1[TN];
+      #pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WM + i * 16 + r16;
+        const int sw = (row >> 1) & 7;
+        a0[i] = *(const f32x4*)(As + row * 128 + ((q) ^ sw) * 16);
+        a1[i] = *(const f32x4*)(As + row * 128 + ((q + 4) ^ sw) * 16);
+      }
+      #pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * WN + j * 16 + r16;
+        const int sw = (row >> 1) & 7;
+        b0[j] = *(const f32x4*)(Bs + row * 128 + ((q) ^ sw) * 16);
+        b1[j] = *(const f32x4*)(Bs + row * 128 + ((q + 4) ^ sw) * 16);
+      }
+      #pragma unroll
+      for (int e = 0; e < 4; ++e)
+        #pragma unroll
+        for (int i = 0; i < TM; ++i)
+          #pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[i][e], b0[j][e], acc[i][j], 0, 0, 0);
+      #pragma unroll
+      for (int e = 0; e < 4; ++e)
+        #pragma unroll
+        for (int i = 0; i < TM; ++i)
+          #pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][e], b1[j][e], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue: bias -> act -> +resid -> stores --------------------------------------
+  const int col0 = grp * N;
+  #pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * WN + j * 16 + r16;
+    const float bv = g.bias ? g.bias[col0 + n] : 0.f;
+    #pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      #pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * WM + i * 16 + q * 4 + r;
+        if (m < M) {
+          float v = acc[i][j][r] + bv;
+          if (g.act == ACT_GELU) v = gelu_erf(v);
+          const long long o = (long long)m * g.ldc + col0 + n;
+          if (g.resid)
+            v += g.resid[g.resid_rows ? (long long)(m % g.resid_rows) * g.ldc + col0 + n : o];
+          if (g.Cf) g.Cf[o] = v;
+          if (g.Ct) ((T*)g.Ct)[o] = from_f32<T>(v);
+        }
+      }
+    }
+  }
+}
+
+template <typename T, int BM, int BN, int WAVES_M, int WAVES_N>
+int launch_cfg(const GemmArgs& a, int amode, int groups, hipStream_t s) {
+  dim3 grid((unsigned)(((a.M + BM - 1) / BM) * (a.N / BN)), (unsigned)groups);
+  dim3 block(WAVES_M * WAVES_N * 64);
+  if (amode == AMODE_SEG)
+    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WAVES_M, WAVES_N, AMODE_SEG>), grid, block, 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WAVES_M, WAVES_N, AMODE_CONV>), grid, block, 0, s, a);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+template <typename T>
+int launch_any(const GemmArgs& a, int amode, int groups, hipStream_t s) {
+  constexpr int E = 16 / (int)sizeof(T);
+  if (a.M <= 0 || a.N <= 0 || a.K <= 0 || a.K % E) return -3;
+  if (amode == AMODE_CONV && (a.cin % E)) return -3;
+  if (a.N % 128 == 0) return launch_cfg<T, 128, 128, 2, 2>(a, amode, groups, s);
+  if (a.N % 64 == 0) return launch_cfg<T, 128, 64, 4, 1>(a, amode, groups, s);
+  if (a.N % 48 == 0) return launch_cfg<T, 128, 48, 4, 1>(a, amode, groups, s);
+  return -3;
+}
+
+}  // namespace
+
+int launch_gemm_bf16(const GemmArgs& a, int amode, int groups, hipStream_t s) {
+  return launch_any<bf16>(a, amode, groups, s);
+}
+int launch_gemm_f32(const GemmArgs& a, int amode, int groups, hipStream_t s) {
+  return launch_any<float>(a, amode, groups, s);
+}

@@ -1,0 +1,480 @@
+// Non-GEMM kernels of the hot path (gfx950):
+//   wave_stats        Wav2Vec2FeatureExtractor zero-mean/unit-var stats      (a2)
+//   conv0_stats/apply WavLM conv0 (1->C, k=10, s=5) + GroupNorm(C, C) + GELU  (K1, a3)
+//   layernorm         LN over rows (feature projection, post/pre-LN encoders) (K3, K7)
+//   pool_mean         time-mean of one hidden state into the embedding slot  (K8, K12)
+//   attention         flash-style MFMA attention; WavLM gated rel-pos bias    (K5, K6, K11)
+#include "common.h"
+#include "kernels.h"
+
+// ---------------------------------------------------------------------------------------
+// a2: per-clip mean / rstd for do_normalize (HF feature_extraction_wav2vec2.py:94).
+__global__ __launch_bounds__(256) void wave_stats_kernel(const float* __restrict__ x, int L,
+                                                         float* __restrict__ out) {
+  const float* xb = x + (long long)blockIdx.x * L;
+  double s = 0.0, q = 0.0;
+  for (int i = threadIdx.x; i < L; i += 256) {
+    const double v = xb[i];
+    s += v;
+    q += v * v;
+  }
+  s = wave_sum_d(s);
+  q = wave_sum_d(q);
+  __shared__ double sh[2][4];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sh[0][w] = s; sh[1][w] = q; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double S = sh[0][0] + sh[0][1] + sh[0][2] + sh[0][3];
+    const double Q = sh[1][0] + sh[1][1] + sh[1][2] + sh[1][3];
+    const double mean = S / L, var = Q / L - mean * mean;
+    out[2 * blockIdx.x] = (float)mean;
+    out[2 * blockIdx.x + 1] = (float)(1.0 / sqrt((var > 0 ? var : 0.0) + 1e-7));
+  }
+}
+
+int launch_wave_stats(const float* x, int B, int L, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(wave_stats_kernel, dim3(B), dim3(256), 0, s, x, L, out);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// ---------------------------------------------------------------------------------------
+// K1: conv0.  One block = (time chunk of C0_T frames, clip), one thread per channel.
+// The waveform segment the chunk needs is staged once in LDS and broadcast to all lanes.
+constexpr int C0_T = 64;
+constexpr int C0_MAXK = 16;
+
+template <bool STATS, typename TO>
+__global__ __launch_bounds__(512) void conv0_kernel(const float* __restrict__ x, int L,
+                                                    const float* __restrict__ norm,
+                                                    const float* __restrict__ w0, const float* __restrict__ b0,
+                                                    int C, int k0, int s0, int T0,
+                                                    double2* __restrict__ part,
+                                                    const float2* __restrict__ ss, TO* __restrict__ out) {
+  __shared__ float xs[(C0_T - 1) * 8 + C0_MAXK + 4];
+  const int chunk = blockIdx.x, b = blockIdx.y;
+  const int t0 = chunk * C0_T;
+  const int nt = min(C0_T, T0 - t0);
+  const int nx = (nt - 1) * s0 + k0;
+  const float* xb = x + (long long)b * L + (long long)t0 * s0;
+  float mu = 0.f, rs = 1.f;
+  if (norm) { mu = norm[2 * b]; rs = norm[2 * b + 1]; }
+  for (int i = threadIdx.x; i < nx; i += blockDim.x) xs[i] = norm ? (xb[i] - mu) * rs : xb[i];
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float w[C0_MAXK];
+    #pragma unroll
+    for (int j = 0; j < C0_MAXK; ++j) w[j] = j < k0 ? w0[c * k0 + j] : 0.f;
+    const float bias = b0 ? b0[c] : 0.f;
+    if (STATS) {
+      double s = 0.0, q = 0.0;
+      for (int t = 0; t < nt; ++t) {
+        float y = bias;
+        #pragma unroll
+        for (int j = 0; j < C0_MAXK; ++j)
+          if (j < k0) y = fmaf(w[j], xs[t * s0 + j], y);
+        s += y;
+        q += (double)y * y;
+      }
+      part[((long long)b * gridDim.x + chunk) * C + c] = make_double2(s, q);
+    } else {
+      const float2 sc = ss[(long long)b * C + c];
+      TO* ob = out + ((long long)b * T0 + t0) * C + c;
+      for (int t = 0; t < nt; ++t) {
+        float y = bias;
+        #pragma unroll
+        for (int j = 0; j < C0_MAXK; ++j)
+          if (j < k0) y = fmaf(w[j], xs[t * s0 + j], y);
+        ob[(long long)t * C] = from_f32<TO>(gelu_erf(fmaf(y, sc.x, sc.y)));
+      }
+    }
+  }
+}
+
+// GroupNorm(C, C) statistics -> per (clip, channel) affine (scale, shift) (HF :723-744).
+__global__ void gn_finalize_kernel(const double2* __restrict__ part, int nchunk, int B, int C, int T0,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+                                   float2* __restrict__ ss) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * C) return;
+  const int b = i / C, c = i - b * C;
+  double s = 0.0, q = 0.0;
+  for (int k = 0; k < nchunk; ++k) {
+    const double2 p = part[((long long)b * nchunk + k) * C + c];
+    s += p.x;
+    q += p.y;
+  }
+  const double mean = s / T0;
+  double var = q / T0 - mean * mean;
+  var = var > 0 ? var : 0;
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float sc = gamma[c] * rstd;
+  ss[i] = make_float2(sc, beta[c] - (float)mean * sc);
+}
+
+int conv0_chunks(int T0) { return (T0 + C0_T - 1) / C0_T; }
+
+template <typename TO>
+int launch_conv0_gn(const float* x, int B, int L, const float* norm, const float* w0, const float* b0,
+                    int C, int k0, int s0, int T0, const float* gamma, const float* beta, float eps,
+                    double2* part, float2* ss, TO* out, hipStream_t s) {
+  if (k0 > C0_MAXK || s0 > 8) return -3;
+  const int nch = conv0_chunks(T0);
+  dim3 grid(nch, B), block(C < 512 ? C : 512);
+  hipLaunchKernelGGL((conv0_kernel<true, TO>), grid, block, 0, s, x, L, norm, w0, b0, C, k0, s0, T0, part,
+                     (const float2*)nullptr, (TO*)nullptr);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3((B * C + 255) / 256), dim3(256), 0, s, part, nch, B, C, T0,
+                     gamma, beta, eps, ss);
+  hipLaunchKernelGGL((conv0_kernel<false, TO>), grid, block, 0, s, x, L, norm, w0, b0, C, k0, s0, T0,
+                     (double2*)nullptr, ss, out);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+template int launch_conv0_gn<float>(const float*, int, int, const float*, const float*, const float*, int, int,
+                                    int, int, const float*, const float*, float, double2*, float2*, float*,
+                                    hipStream_t);
+template int launch_conv0_gn<bf16>(const float*, int, int, const float*, const float*, const float*, int, int,
+                                   int, int, const float*, const float*, float, double2*, float2*, bf16*,
+                                   hipStream_t);
+
+// ---------------------------------------------------------------------------------------
+// LayerNorm over rows of H (H % 256 == 0, H <= 2048).  One wave per row, 4 rows per block,
+// 4 consecutive elements per lane per step (16-B fp32 / 8-B bf16 accesses).
+template <typename TI> SSE_DEV f32x4 load4(const TI* p);
+template <> SSE_DEV f32x4 load4<float>(const float* p) { return *(const f32x4*)p; }
+template <> SSE_DEV f32x4 load4<bf16>(const bf16* p) {
+  const bf16x4 v = *(const bf16x4*)p;
+  return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void layernorm_kernel(const TI* __restrict__ in, const float* __restrict__ w,
+                                                        const float* __restrict__ bta, int rows, int H,
+                                                        float eps, int act, float* __restrict__ out_f,
+                                                        TO* __restrict__ out_t) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const int nv = H >> 8;
+  const TI* x = in + (long long)row * H;
+  f32x4 v[8];
+  float s = 0.f;
+  #pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (i < nv) {
+      v[i] = load4<TI>(x + i * 256 + lane * 4);
+      s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+    }
+  const float mean = wave_sum(s) / H;
+  float q = 0.f;
+  #pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (i < nv)
+      #pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = v[i][e] - mean;
+        q = fmaf(d, d, q);
+      }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / H + eps);
+  #pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (i < nv) {
+      const int c = i * 256 + lane * 4;
+      const f32x4 wv = *(const f32x4*)(w + c), bv = *(const f32x4*)(bta + c);
+      f32x4 o;
+      #pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float y = (v[i][e] - mean) * rstd * wv[e] + bv[e];
+        o[e] = act == ACT_GELU ? gelu_erf(y) : y;
+      }
+      const long long off = (long long)row * H + c;
+      if (out_f) *(f32x4*)(out_f + off) = o;
+      if (out_t) {
+        if constexpr (sizeof(TO) == 2) {
+          bf16x4 ob = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+          *(bf16x4*)(out_t + off) = ob;
+        } else {
+          *(f32x4*)(out_t + off) = o;
+        }
+      }
+    }
+}
+
+template <typename TI, typename TO>
+int launch_layernorm(const TI* in, const float* w, const float* b, int rows, int H, float eps, int act,
+                     float* out_f, TO* out_t, hipStream_t s) {
+  if (H % 256 || H > 2048) return -3;
+  hipLaunchKernelGGL((layernorm_kernel<TI, TO>), dim3((rows + 3) / 4), dim3(256), 0, s, in, w, b, rows, H, eps,
+                     act, out_f, out_t);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+template int launch_layernorm<float, float>(const float*, const float*, const float*, int, int, float, int,
+                                            float*, float*, hipStream_t);
+template int launch_layernorm<float, bf16>(const float*, const float*, const float*, int, int, float, int,
+                                           float*, bf16*, hipStream_t);
+template int launch_layernorm<bf16, bf16>(const bf16*, const float*, const float*, int, int, float, int, float*,
+                                          bf16*, hipStream_t);
+
+// ---------------------------------------------------------------------------------------
+// K8/K12: out[b*out_stride + n] = mean_t x[b][t][n]  (torch.mean(hs, dim=1), fp64 accumulation).
+__global__ __launch_bounds__(256) void pool_mean_kernel(const float* __restrict__ x, int T, int H,
+                                                        float* __restrict__ out, long long out_stride) {
+  const int n = blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
+  if (n >= H) return;
+  const float* xb = x + (long long)b * T * H + n;
+  double s = 0.0;
+  for (int t = 0; t < T; ++t) s += xb[(long long)t * H];
+  out[b * out_stride + n] = (float)(s / T);
+}
+
+int launch_pool_mean(const float* x, int B, int T, int H, float* out, long long out_stride, hipStream_t s) {
+  hipLaunchKernelGGL(pool_mean_kernel, dim3((H + 255) / 256, B), dim3(256), 0, s, x, T, H, out, out_stride);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// ---------------------------------------------------------------------------------------
+// K5/K6/K11: attention, flash style.  Block = (64 queries, head, clip), 4 waves x 16 queries.
+// Keys stream through LDS in tiles of 64.  Per tile and wave:
+//   S^T = K_tile . Q^T      (key on the MFMA row, query on the lane: lane holds one query)
+//   s   = S^T*scale (+ gate[q] * relbias[key - q])   -- WavLM gated relative-position bias
+//   online softmax over keys (max/sum in-lane + 2 cross-lane-group shuffles)
+//   O^T += V^T_tile . P^T   (the S^T accumulators ARE the B operand, no lane movement)
+// bf16 path: v_mfma_f32_16x16x32_bf16 on K [key][d] (128-B rows, XOR swizzle) and V^T
+// [d][key]; f32 path: v_mfma_f32_16x16x4_f32 on K [key][d] (256-B rows, XOR swizzle) and
+// V [key][d] (68-float rows).  HF: modeling_wavlm.py:141-241, modeling_whisper.py:215-238.
+constexpr int AT_Q = 64, AT_K = 64, AT_HD = 64;
+constexpr int VT_STRIDE = 72;     // bf16 V^T row stride (36 dwords = 16k+4: conflict-free b64 reads)
+constexpr int VF_STRIDE = 68;     // f32 V row stride (4 mod 8: conflict-free b32 reads)
+
+
+
+template <typename TE, bool BIAS>
+__global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
+  constexpr bool BF = sizeof(TE) == 2;
+  constexpr int KS_BYTES = BF ? AT_K * 128 : AT_K * 256;
+  constexpr int VS_BYTES = BF ? AT_HD * VT_STRIDE * 2 : AT_K * VF_STRIDE * 4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Ks = smem;
+  char* Vs = smem + KS_BYTES;
+  float* gate = (float*)(Vs + VS_BYTES);           // [AT_Q]
+  float* rb = gate + AT_Q;                         // [2*Tk]  (BIAS)
+
+  const int qc = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int T = a.T, H = a.H, H3 = 3 * a.H;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  const int q0 = qc * AT_Q;
+  const int nkt = (T + AT_K - 1) / AT_K;
+  const int Tk = nkt * AT_K;
+  const TE* qkv = (const TE*)a.qkv + (long long)b * T * H3;
+
+  if (BIAS) {
+    // gate[q] for the block's queries: sigmoid((x_h . Wg^T + bg) pairwise sums) (HF :158-170)
+    if (tid < AT_Q && q0 + tid >= T) gate[tid] = 0.f;
+    if (tid < AT_Q && q0 + tid < T) {
+      const float* xr = a.gx + ((long long)b * T + q0 + tid) * H + h * AT_HD;
+      float acc[8];
+      #pragma unroll
+      for (int o = 0; o < 8; ++o) acc[o] = a.gb[o];
+      for (int d = 0; d < AT_HD; d += 4) {
+        const f32x4 xv = *(const f32x4*)(xr + d);
+        #pragma unroll
+        for (int o = 0; o < 8; ++o) {
+          const f32x4 wv = *(const f32x4*)(a.gw + o * AT_HD + d);
+          acc[o] = fmaf(xv[0], wv[0], fmaf(xv[1], wv[1], fmaf(xv[2], wv[2], fmaf(xv[3], wv[3], acc[o]))));
+        }
+      }
+      const float ra = acc[0] + acc[1] + acc[2] + acc[3];
+      const float rbv = acc[4] + acc[5] + acc[6] + acc[7];
+      const float ga = 1.f / (1.f + expf(-ra)), gbv = 1.f / (1.f + expf(-rbv));
+      gate[tid] = ga * (gbv * a.gconst[h] - 1.0f) + 2.0f;
+    }
+    // relative bias slice: rb[u] = relb[h][u - (Tk-1)], u in [0, 2*Tk-1)
+    const float* rh = a.relb + (long long)h * (2 * a.maxd + 1) + a.maxd;
+    for (int u = tid; u < 2 * Tk - 1; u += 256) {
+      int d = u - (Tk - 1);
+      d = d < -a.maxd ? -a.maxd : (d > a.maxd ? a.maxd : d);
+      rb[u] = rh[d];
+    }
+  }
+
+  // Q fragments (B operand of S^T = K.Q^T), straight from global.
+  const int qi = q0 + wave * 16 + r16;
+  const bool qv = qi < T;
+  const TE* qrow = qkv + (long long)(qv ? qi : 0) * H3 + h * AT_HD;
+  bf16x8 qb[2];
+  f32x4 qf[4];
+  if constexpr (BF) {
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      qb[ks] = *(const bf16x8*)(qrow + ks * 32 + g * 8);
+      if (!qv) qb[ks] = bf16x8{};
+    }
+  } else {
+    #pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      qf[c] = *(const f32x4*)((const float*)qrow + (g + 4 * c) * 4);
+      if (!qv) qf[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+
+  f32x4 o[4];
+  #pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+  const float LOG2E = 1.4426950408889634f;
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    __syncthreads();   // previous tile fully consumed
+    // ---- stage K (swizzled rows) and V (transposed for bf16) ----
+    const int kbase = kt * AT_K;
+    if constexpr (BF) {
+      for (int i = tid; i < AT_K * 8; i += 256) {
+        const int kr = i >> 3, ch = i & 7;
+        const int key = kbase + kr;
+        bf16x8 kv = bf16x8{}, vv = bf16x8{};
+        if (key < T) {
+          kv = *(const bf16x8*)(qkv + (long long)key * H3 + H + h * AT_HD + ch * 8);
+          vv = *(const bf16x8*)(qkv + (long long)key * H3 + 2 * H + h * AT_HD + ch * 8);
+        }
+        *(bf16x8*)(Ks + kr * 128 + ((ch ^ ((kr >> 1) & 7)) * 16)) = kv;
+        bf16* vt = (bf16*)Vs;
+        #pragma unroll
+        for (int e = 0; e < 8; ++e) vt[(ch * 8 + e) * VT_STRIDE + kr] = vv[e];
+      }
+    } else {
+      for (int i = tid; i < AT_K * 16; i += 256) {
+        const int kr = i >> 4, ch = i & 15;
+        const int key = kbase + kr;
+        f32x4 kv = f32x4{0.f, 0.f, 0.f, 0.f}, vv = kv;
+        if (key < T) {
+          kv = *(const f32x4*)((const float*)(qkv + (long long)key * H3 + H + h * AT_HD) + ch * 4);
+          vv = *(const f32x4*)((const float*)(qkv + (long long)key * H3 + 2 * H + h * AT_HD) + ch * 4);
+        }
+        *(f32x4*)(Ks + kr * 256 + ((ch ^ (kr & 15)) * 16)) = kv;
+        *(f32x4*)((float*)Vs + kr * VF_STRIDE + ch * 4) = vv;
+      }
+    }
+    __syncthreads();
+
+    // ---- S^T tiles: s[kb][r] = score(key = kbase + kb*16 + 4g + r, query = qi) ----
+    f32x4 s[4];
+    #pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int kr = kb * 16 + r16;
+      if constexpr (BF) {
+        #pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const bf16x8 kf = *(const bf16x8*)(Ks + kr * 128 + (((g + 4 * ks) ^ ((kr >> 1) & 7)) * 16));
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qb[ks], acc, 0, 0, 0);
+        }
+      } else {
+        #pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const f32x4 kf = *(const f32x4*)(Ks + kr * 256 + (((g + 4 * c) ^ (kr & 15)) * 16));
+          #pragma unroll
+          for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[e], qf[c][e], acc, 0, 0, 0);
+        }
+      }
+      s[kb] = acc;
+    }
+    // ---- scale, bias, mask; online softmax ----
+    float tmax = -INFINITY;
+    #pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+      #pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kbase + kb * 16 + 4 * g + r;
+        float v = s[kb][r] * a.scale;
+        if (BIAS) v = fmaf(gate[wave * 16 + r16], rb[key - qi + (Tk - 1)], v);
+        v = key < T ? v : -INFINITY;
+        s[kb][r] = v;
+        tmax = fmaxf(tmax, v);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float m_new = fmaxf(m_run, tmax);
+    const float alpha = exp2f((m_run - m_new) * LOG2E);
+    m_run = m_new;
+    l_run *= alpha;
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] *= alpha;
+    const float mb = m_new * LOG2E;
+    #pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+      #pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(fmaf(s[kb][r], LOG2E, -mb));
+        s[kb][r] = p;
+        l_run += p;
+      }
+    // ---- O^T += V^T . P^T ----
+    if constexpr (BF) {
+      const bf16* vt = (const bf16*)Vs;
+      #pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 pf;
+        #pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pf[r] = (bf16)s[2 * ks][r];
+          pf[4 + r] = (bf16)s[2 * ks + 1][r];
+        }
+        #pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          const bf16* vrow = vt + (db * 16 + r16) * VT_STRIDE + ks * 32 + 4 * g;
+          const bf16x4 v0 = *(const bf16x4*)(vrow);
+          const bf16x4 v1 = *(const bf16x4*)(vrow + 16);
+          const bf16x8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+          o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[db], 0, 0, 0);
+        }
+      }
+    } else {
+      const float* vs = (const float*)Vs;
+      #pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+        #pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float* vrow = vs + (kb * 16 + 4 * g + r) * VF_STRIDE + r16;
+          #pragma unroll
+          for (int db = 0; db < 4; ++db)
+            o[db] = __builtin_amdgcn_mfma_f32_16x16x4f32(vrow[db * 16], s[kb][r], o[db], 0, 0, 0);
+        }
+    }
+  }
+  // ---- normalise and store: lane holds O[query qi][dims db*16 + 4g .. +3] ----
+  l_run += __shfl_xor(l_run, 16, 64);
+  l_run += __shfl_xor(l_run, 32, 64);
+  if (!qv) return;
+  const float inv = 1.0f / l_run;
+  TE* orow = (TE*)a.out + ((long long)b * T + qi) * H + h * AT_HD;
+  #pragma unroll
+  for (int db = 0; db < 4; ++db) {
+    if constexpr (BF) {
+      bf16x4 ov = {(bf16)(o[db][0] * inv), (bf16)(o[db][1] * inv), (bf16)(o[db][2] * inv), (bf16)(o[db][3] * inv)};
+      *(bf16x4*)(orow + db * 16 + 4 * g) = ov;
+    } else {
+      *(f32x4*)((float*)orow + db * 16 + 4 * g) = o[db] * inv;
+    }
+  }
+}
+
+template <typename T>
+int launch_attention(const AttnArgs& a, int B, hipStream_t s) {
+  if (a.H != a.nh * AT_HD) return -3;
+  constexpr bool BF = sizeof(T) == 2;
+  constexpr int KS_BYTES = BF ? AT_K * 128 : AT_K * 256;
+  constexpr int VS_BYTES = BF ? AT_HD * VT_STRIDE * 2 : AT_K * VF_STRIDE * 4;
+  const int nkt = (a.T + AT_K - 1) / AT_K;
+  size_t lds = KS_BYTES + VS_BYTES + AT_Q * 4;
+  if (a.relb) lds += (size_t)(2 * nkt * AT_K) * 4;
+  if (lds > 160 * 1024) return -3;
+  dim3 grid((a.T + AT_Q - 1) / AT_Q, a.nh, B);
+  if (a.relb)
+    hipLaunchKernelGGL((attention_kernel<T, true>), grid, dim3(256), lds, s, a);
+  else
+    hipLaunchKernelGGL((attention_kernel<T, false>), grid, dim3(256), lds, s, a);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+template int launch_attention<float>(const AttnArgs&, int, hipStream_t);
+template int launch_attention<bf16>(const AttnArgs&, int, hipStream_t);

@@ -1,0 +1,841 @@
+// libsse.so host side: the C-ABI of include/sse.h, weight repacking and the forward
+// orchestration of the WavLM / Whisper embedding path on one gfx950 device.
+//
+// Forward plan (WavLM, SURVEY.md §3.1, HF/models/wavlm/modeling_wavlm.py):
+//   [a2] wave_stats (do_normalize)                 -> per-clip (mean, rstd)
+//   [K1] conv0 + GroupNorm + GELU                  -> bufA [B][T0][C]      (channels-last)
+//   [K2] conv1..6 implicit GEMM + GELU             -> ping-pong bufB/bufA  (rows overlap, no im2col)
+//   [K3] LN(C) -> projection GEMM                  -> x (fp32 residual stream) + xt (GEMM operand)
+//   [K4] grouped pos-conv GEMM + GELU + residual   -> x ; LN (post-LN base) -> hidden_states[0]
+//   per layer [K5-K7]: QKV GEMM -> gated-bias attention -> out-proj(+x) -> LN -> FFN(GELU)(+x) -> LN
+//   [K8] pool_mean of the selected hidden states   -> out [B][n_sel][H]
+// Whisper: [K9] log-mel -> [K10] conv1/conv2 implicit GEMM (+positions) ->
+//   32 pre-LN layers (q pre-scaled by 1/8 at load, k unbiased) -> final LN -> [K12] pooling.
+// All activations that feed a GEMM are stored in the path's element type (bf16 or fp32);
+// the residual stream, LayerNorm statistics and pooled sums stay fp32.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/sse.h"
+#include "common.h"
+#include "kernels.h"
+#include "kernels_logmel.h"
+
+#define SSE_VERSION "sse 0.1.0 (gfx950)"
+
+namespace {
+
+constexpr int MAXD = 4095;   // relative-position table covers |key - query| <= MAXD (saturates at 800)
+
+inline uint16_t f2bf_bits(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+int rel_bucket(int d, int num_buckets, int max_distance) {
+  // HF WavLMAttention._relative_positions_bucket (modeling_wavlm.py:246-271), float32 path
+  const int nb = num_buckets / 2;
+  int bucket = d > 0 ? nb : 0;
+  const int rel = d < 0 ? -d : d;
+  const int max_exact = nb / 2;
+  if (rel < max_exact) return bucket + rel;
+  float v = logf((float)rel / (float)max_exact);
+  v = v / (float)std::log((double)max_distance / (double)max_exact);
+  v = v * (float)(nb - max_exact);
+  int large = (int)((float)max_exact + v);
+  if (large > nb - 1) large = nb - 1;
+  return bucket + large;
+}
+
+// ---- canonical weight blob walker (mirrors config.param_specs) -------------------------
+struct Blob {
+  const float* p;
+  size_t n, off = 0;
+  bool ok = true;
+  const float* take(size_t count) {
+    if (off + count > n) { ok = false; return nullptr; }
+    const float* r = p ? p + off : nullptr;
+    off += count;
+    return r;
+  }
+};
+
+// ---- device arena for weights ----------------------------------------------------------
+struct Arena {
+  std::vector<std::pair<size_t, std::vector<char>>> pending;  // (offset, bytes)
+  size_t size = 0;
+  size_t put(const void* src, size_t bytes) {
+    const size_t off = size;
+    std::vector<char> v(bytes);
+    if (src) std::memcpy(v.data(), src, bytes);
+    pending.emplace_back(off, std::move(v));
+    size = (size + bytes + 255) & ~(size_t)255;
+    return off;
+  }
+  size_t put_f32(const float* src, size_t n) { return put(src, n * 4); }
+  size_t put_elem(const std::vector<float>& v, bool bf) {
+    if (!bf) return put(v.data(), v.size() * 4);
+    std::vector<uint16_t> h(v.size());
+    for (size_t i = 0; i < v.size(); ++i) h[i] = f2bf_bits(v[i]);
+    return put(h.data(), h.size() * 2);
+  }
+};
+
+struct LayerW {
+  size_t qkv_w, qkv_b, o_w, o_b, ln1_w, ln1_b, f1_w, f1_b, f2_w, f2_b, ln2_w, ln2_b;
+  size_t g_const, g_w, g_b;   // WavLM gate
+};
+
+}  // namespace
+
+struct sse_model {
+  sse_cfg cfg;
+  int device = 0, dtype = 0;
+  char* dmem = nullptr;
+  size_t dbytes = 0;
+  // WavLM
+  size_t conv_w[8], conv_b[8], conv_ln_w[8], conv_ln_b[8];
+  bool has_conv_b = false;
+  size_t fp_ln_w, fp_ln_b, fp_w, fp_b, pos_w, pos_b, enc_ln_w, enc_ln_b, relb, zero;
+  // Whisper
+  size_t c1_w, c1_b, c2_w, c2_b, positions;
+  std::vector<LayerW> layers;
+  // live per-launch timing (sse_profile_*): events pre-created outside any capture
+  struct Prof {
+    bool on = false;
+    int used = 0;
+    std::vector<hipEvent_t> ev;
+    std::vector<std::string> tag;
+    std::vector<double> flops, bytes;
+  } prof;
+
+  template <typename X = void> const X* ptr(size_t off) const { return (const X*)(dmem + off); }
+  bool bf() const { return dtype == SSE_DTYPE_BF16; }
+};
+
+namespace {
+
+bool cfg_valid(const sse_cfg* c) {
+  if (!c || c->hidden <= 0 || c->layers <= 0 || c->heads <= 0 || c->ffn <= 0) return false;
+  if (c->hidden % c->heads || c->hidden / c->heads != 64) return false;
+  if (c->kind == SSE_KIND_WAVLM) {
+    if (c->n_conv < 2 || c->n_conv > 8 || c->pos_groups <= 0 || c->hidden % c->pos_groups) return false;
+  } else if (c->kind == SSE_KIND_WHISPER) {
+    if (c->n_mels <= 0 || c->max_positions <= 0) return false;
+  } else {
+    return false;
+  }
+  return true;
+}
+
+// Walk the canonical order; with a null blob only counts.
+int build_wavlm(sse_model* m, Blob& bl, Arena& ar) {
+  const sse_cfg& c = m->cfg;
+  const bool BF = m->bf();
+  const int H = c.hidden, F = c.ffn, nh = c.heads;
+  int cin = 1;
+  for (int i = 0; i < c.n_conv; ++i) {
+    const int co = c.conv_dim[i], k = c.conv_kernel[i];
+    const float* w = bl.take((size_t)co * cin * k);
+    const float* b = c.conv_bias ? bl.take(co) : nullptr;
+    const float* lw = nullptr;
+    const float* lb = nullptr;
+    if (c.feat_norm_layer || i == 0) { lw = bl.take(co); lb = bl.take(co); }
+    if (!bl.ok) return SSE_ERR_WEIGHTS;
+    if (!w) { cin = co; continue; }
+    if (i == 0) {
+      m->conv_w[0] = ar.put_f32(w, (size_t)co * k);      // [C][k] fp32 (VALU conv0)
+    } else {
+      std::vector<float> t((size_t)co * k * cin);        // [out][j*cin + c]
+      for (int o = 0; o < co; ++o)
+        for (int ci = 0; ci < cin; ++ci)
+          for (int j = 0; j < k; ++j) t[((size_t)o * k + j) * cin + ci] = w[((size_t)o * cin + ci) * k + j];
+      m->conv_w[i] = ar.put_elem(t, BF);
+    }
+    m->conv_b[i] = b ? ar.put_f32(b, co) : 0;
+    m->has_conv_b = b != nullptr;
+    m->conv_ln_w[i] = lw ? ar.put_f32(lw, co) : 0;
+    m->conv_ln_b[i] = lb ? ar.put_f32(lb, co) : 0;
+    cin = co;
+  }
+  const int C = cin;
+  const float* fplw = bl.take(C);
+  const float* fplb = bl.take(C);
+  const float* fpw = bl.take((size_t)H * C);
+  const float* fpb = bl.take(H);
+  const int K = c.pos_kernel, G = c.pos_groups, cg = H / G;
+  const float* pg = bl.take(K);
+  const float* pv = bl.take((size_t)H * cg * K);
+  const float* pb = bl.take(H);
+  const float* elw = bl.take(H);
+  const float* elb = bl.take(H);
+  const float* rel = bl.take((size_t)c.num_buckets * nh);
+  if (!bl.ok) return SSE_ERR_WEIGHTS;
+  if (fplw) {
+    m->fp_ln_w = ar.put_f32(fplw, C);
+    m->fp_ln_b = ar.put_f32(fplb, C);
+    m->fp_w = ar.put_elem(std::vector<float>(fpw, fpw + (size_t)H * C), BF);
+    m->fp_b = ar.put_f32(fpb, H);
+    // weight_norm(dim=2): w[o][c][j] = g[j] * v[o][c][j] / ||v[:, :, j]||  (fp64 norm), then
+    // per group [cg_out][j*cg + c_in]
+    std::vector<double> nrm(K, 0.0);
+    for (size_t i = 0; i < (size_t)H * cg; ++i)
+      for (int j = 0; j < K; ++j) nrm[j] += (double)pv[i * K + j] * pv[i * K + j];
+    for (int j = 0; j < K; ++j) nrm[j] = std::sqrt(nrm[j]);
+    std::vector<float> t((size_t)H * K * cg);
+    for (int o = 0; o < H; ++o)
+      for (int ci = 0; ci < cg; ++ci)
+        for (int j = 0; j < K; ++j)
+          t[((size_t)o * K + j) * cg + ci] = (float)((double)pg[j] * ((double)pv[((size_t)o * cg + ci) * K + j] / nrm[j]));
+    m->pos_w = ar.put_elem(t, BF);
+    m->pos_b = ar.put_f32(pb, H);
+    m->enc_ln_w = ar.put_f32(elw, H);
+    m->enc_ln_b = ar.put_f32(elb, H);
+    std::vector<float> tab((size_t)nh * (2 * MAXD + 1));
+    for (int d = -MAXD; d <= MAXD; ++d) {
+      const int bk = rel_bucket(d, c.num_buckets, c.max_distance);
+      for (int h = 0; h < nh; ++h) tab[(size_t)h * (2 * MAXD + 1) + d + MAXD] = rel[(size_t)bk * nh + h];
+    }
+    m->relb = ar.put_f32(tab.data(), tab.size());
+  }
+  for (int l = 0; l < c.layers; ++l) {
+    const float *qw = bl.take((size_t)H * H), *qb = bl.take(H), *kw = bl.take((size_t)H * H), *kb = bl.take(H);
+    const float *vw = bl.take((size_t)H * H), *vb = bl.take(H), *ow = bl.take((size_t)H * H), *ob = bl.take(H);
+    const float *gc = bl.take(nh), *gw = bl.take((size_t)8 * 64), *gbb = bl.take(8);
+    const float *l1w = bl.take(H), *l1b = bl.take(H);
+    const float *f1w = bl.take((size_t)F * H), *f1b = bl.take(F), *f2w = bl.take((size_t)H * F), *f2b = bl.take(H);
+    const float *l2w = bl.take(H), *l2b = bl.take(H);
+    if (!bl.ok) return SSE_ERR_WEIGHTS;
+    if (!qw) continue;
+    LayerW L{};
+    std::vector<float> qkv((size_t)3 * H * H), qkvb((size_t)3 * H);
+    std::memcpy(qkv.data(), qw, (size_t)H * H * 4);
+    std::memcpy(qkv.data() + (size_t)H * H, kw, (size_t)H * H * 4);
+    std::memcpy(qkv.data() + (size_t)2 * H * H, vw, (size_t)H * H * 4);
+    std::memcpy(qkvb.data(), qb, H * 4);
+    std::memcpy(qkvb.data() + H, kb, H * 4);
+    std::memcpy(qkvb.data() + 2 * H, vb, H * 4);
+    L.qkv_w = ar.put_elem(qkv, BF);
+    L.qkv_b = ar.put_f32(qkvb.data(), 3 * H);
+    L.o_w = ar.put_elem(std::vector<float>(ow, ow + (size_t)H * H), BF);
+    L.o_b = ar.put_f32(ob, H);
+    L.g_const = ar.put_f32(gc, nh);
+    L.g_w = ar.put_f32(gw, 8 * 64);
+    L.g_b = ar.put_f32(gbb, 8);
+    L.ln1_w = ar.put_f32(l1w, H);
+    L.ln1_b = ar.put_f32(l1b, H);
+    L.f1_w = ar.put_elem(std::vector<float>(f1w, f1w + (size_t)F * H), BF);
+    L.f1_b = ar.put_f32(f1b, F);
+    L.f2_w = ar.put_elem(std::vector<float>(f2w, f2w + (size_t)H * F), BF);
+    L.f2_b = ar.put_f32(f2b, H);
+    L.ln2_w = ar.put_f32(l2w, H);
+    L.ln2_b = ar.put_f32(l2b, H);
+    m->layers.push_back(L);
+  }
+  return bl.ok ? SSE_OK : SSE_ERR_WEIGHTS;
+}
+
+int build_whisper(sse_model* m, Blob& bl, Arena& ar) {
+  const sse_cfg& c = m->cfg;
+  const bool BF = m->bf();
+  const int D = c.hidden, F = c.ffn, nm = c.n_mels;
+  const float *c1w = bl.take((size_t)D * nm * 3), *c1b = bl.take(D);
+  const float *c2w = bl.take((size_t)D * D * 3), *c2b = bl.take(D);
+  const float* pos = bl.take((size_t)c.max_positions * D);
+  if (!bl.ok) return SSE_ERR_WEIGHTS;
+  auto conv_pack = [&](const float* w, int co, int ci) {   // [out][in][3] -> [out][j*in + c]
+    std::vector<float> t((size_t)co * 3 * ci);
+    for (int o = 0; o < co; ++o)
+      for (int x = 0; x < ci; ++x)
+        for (int j = 0; j < 3; ++j) t[((size_t)o * 3 + j) * ci + x] = w[((size_t)o * ci + x) * 3 + j];
+    return t;
+  };
+  if (c1w) {
+    m->c1_w = ar.put_elem(conv_pack(c1w, D, nm), BF);
+    m->c1_b = ar.put_f32(c1b, D);
+    m->c2_w = ar.put_elem(conv_pack(c2w, D, D), BF);
+    m->c2_b = ar.put_f32(c2b, D);
+    m->positions = ar.put_f32(pos, (size_t)c.max_positions * D);
+  }
+  const float scale = 0.125f;   // head_dim ** -0.5 for head_dim 64: exact power of two
+  for (int l = 0; l < c.layers; ++l) {
+    const float *qw = bl.take((size_t)D * D), *qb = bl.take(D), *kw = bl.take((size_t)D * D);
+    const float *vw = bl.take((size_t)D * D), *vb = bl.take(D), *ow = bl.take((size_t)D * D), *ob = bl.take(D);
+    const float *l1w = bl.take(D), *l1b = bl.take(D);
+    const float *f1w = bl.take((size_t)F * D), *f1b = bl.take(F), *f2w = bl.take((size_t)D * F), *f2b = bl.take(D);
+    const float *l2w = bl.take(D), *l2b = bl.take(D);
+    if (!bl.ok) return SSE_ERR_WEIGHTS;
+    if (!qw) continue;
+    LayerW L{};
+    std::vector<float> qkv((size_t)3 * D * D), qkvb((size_t)3 * D, 0.f);
+    for (size_t i = 0; i < (size_t)D * D; ++i) qkv[i] = qw[i] * scale;   // (xWq + bq) * s == x(sWq) + s bq, s = 2^-3
+    std::memcpy(qkv.data() + (size_t)D * D, kw, (size_t)D * D * 4);
+    std::memcpy(qkv.data() + (size_t)2 * D * D, vw, (size_t)D * D * 4);
+    for (int i = 0; i < D; ++i) qkvb[i] = qb[i] * scale;
+    std::memcpy(qkvb.data() + 2 * D, vb, D * 4);                           // k_proj has no bias
+    L.qkv_w = ar.put_elem(qkv, BF);
+    L.qkv_b = ar.put_f32(qkvb.data(), 3 * D);
+    L.o_w = ar.put_elem(std::vector<float>(ow, ow + (size_t)D * D), BF);
+    L.o_b = ar.put_f32(ob, D);
+    L.ln1_w = ar.put_f32(l1w, D);
+    L.ln1_b = ar.put_f32(l1b, D);
+    L.f1_w = ar.put_elem(std::vector<float>(f1w, f1w + (size_t)F * D), BF);
+    L.f1_b = ar.put_f32(f1b, F);
+    L.f2_w = ar.put_elem(std::vector<float>(f2w, f2w + (size_t)D * F), BF);
+    L.f2_b = ar.put_f32(f2b, D);
+    L.ln2_w = ar.put_f32(l2w, D);
+    L.ln2_b = ar.put_f32(l2b, D);
+    m->layers.push_back(L);
+  }
+  const float *elw = bl.take(D), *elb = bl.take(D);
+  if (!bl.ok) return SSE_ERR_WEIGHTS;
+  if (elw) {
+    m->enc_ln_w = ar.put_f32(elw, D);
+    m->enc_ln_b = ar.put_f32(elb, D);
+  }
+  return SSE_OK;
+}
+
+// ---- workspace planning ----------------------------------------------------------------
+struct Plan {
+  size_t total = 0;
+  size_t add(size_t bytes) {
+    const size_t o = total;
+    total = (total + bytes + 255) & ~(size_t)255;
+    return o;
+  }
+};
+
+// Runs `launch` between two recorded events when profiling is on (tag, algorithmic FLOPs and
+// bytes of that launch are kept for sse_profile_read).
+template <typename F>
+int prof(sse_model* m, hipStream_t s, const char* tag, double flops, double bytes, F&& launch) {
+  auto& P = m->prof;
+  const bool rec = P.on && P.used + 2 <= (int)P.ev.size();
+  if (rec && hipEventRecord(P.ev[P.used], s) != hipSuccess) return SSE_ERR_HIP;
+  const int rc = launch();
+  if (rc) return rc;
+  if (rec) {
+    if (hipEventRecord(P.ev[P.used + 1], s) != hipSuccess) return SSE_ERR_HIP;
+    P.used += 2;
+    P.tag.emplace_back(tag);
+    P.flops.push_back(flops);
+    P.bytes.push_back(bytes);
+  }
+  return 0;
+}
+
+inline double gflops(const GemmArgs& g, int groups = 1) { return 2.0 * g.M * (double)g.N * g.K * groups; }
+
+int wavlm_frames(const sse_cfg& c, int L, int* Ts) {
+  int t = L;
+  for (int i = 0; i < c.n_conv; ++i) {
+    t = (t - c.conv_kernel[i]) / c.conv_stride[i] + 1;
+    if (Ts) Ts[i] = t;
+    if (t <= 0) return 0;
+  }
+  return t;
+}
+
+struct WavlmWs {
+  size_t zero, norm, part, ss, bufA, bufB, x, xt, xb, qkv, ctx, ff, hf;
+};
+
+WavlmWs wavlm_plan(const sse_model* m, int B, int L, Plan& p) {
+  const sse_cfg& c = m->cfg;
+  const size_t es = m->bf() ? 2 : 4;
+  int Ts[8];
+  const int T = wavlm_frames(c, L, Ts);
+  const size_t M = (size_t)B * T;
+  const int C0 = c.conv_dim[0];
+  size_t maxA = 0, maxB = 0;
+  for (int i = 0; i < c.n_conv; ++i) {
+    const size_t sz = (size_t)B * Ts[i] * c.conv_dim[i] * (c.feat_norm_layer && i == 0 ? 4 : es);
+    if (i % 2 == 0) maxA = sz > maxA ? sz : maxA; else maxB = sz > maxB ? sz : maxB;
+  }
+  WavlmWs w;
+  w.zero = p.add(256);
+  w.norm = p.add((size_t)B * 8);
+  w.part = p.add((size_t)B * conv0_chunks(Ts[0]) * C0 * 16);
+  w.ss = p.add((size_t)B * C0 * 8);
+  w.bufA = p.add(maxA);
+  w.bufB = p.add(maxB);
+  const int H = c.hidden;
+  w.x = p.add(M * H * 4);
+  w.xt = p.add(M * H * es);
+  w.xb = p.add(M * (H > c.conv_dim[c.n_conv - 1] ? H : c.conv_dim[c.n_conv - 1]) * es);
+  w.qkv = p.add(M * 3 * H * es);
+  w.ctx = p.add(M * H * es);
+  w.ff = p.add(M * (size_t)c.ffn * es);
+  w.hf = c.stable_layer_norm ? p.add(M * H * 4) : 0;
+  return w;
+}
+
+struct WhisperWs {
+  size_t zero, lm, mel, h1, x, xb, qkv, ctx, ff, xf;
+};
+
+WhisperWs whisper_plan(const sse_model* m, int B, Plan& p) {
+  const sse_cfg& c = m->cfg;
+  const size_t es = m->bf() ? 2 : 4;
+  const int D = c.hidden, T = c.max_positions, T2 = 2 * T;
+  const size_t M = (size_t)B * T;
+  WhisperWs w;
+  w.zero = p.add(256);
+  w.lm = p.add(logmel_workspace_bytes(B, c.n_mels));
+  w.mel = p.add((size_t)B * T2 * c.n_mels * es);
+  w.h1 = p.add((size_t)B * T2 * D * es);
+  w.x = p.add(M * D * 4);
+  w.xb = p.add(M * D * es);
+  w.qkv = p.add(M * 3 * D * es);
+  w.ctx = p.add(M * D * es);
+  w.ff = p.add(M * (size_t)c.ffn * es);
+  w.xf = p.add(M * D * 4);
+  return w;
+}
+
+#define RC(expr)                \
+  do {                          \
+    const int _rc = (expr);     \
+    if (_rc) return _rc;        \
+  } while (0)
+
+// Emits one hidden state: pooled into its output slots and/or copied into d_hs.
+struct Sink {
+  const int32_t* ids;
+  int n_ids;
+  float* pooled;         // [B][n_ids][H]
+  float* hs;             // [n_hs][B][T][H]
+  int B, T, H;
+  hipStream_t s;
+  int emit(int idx, const float* x) const {
+    for (int i = 0; i < n_ids; ++i)
+      if (ids[i] == idx) RC(launch_pool_mean(x, B, T, H, pooled + (size_t)i * H, (long long)n_ids * H, s));
+    if (hs) {
+      const size_t bytes = (size_t)B * T * H * 4;
+      if (hipMemcpyAsync(hs + (size_t)idx * B * T * H, x, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
+        return SSE_ERR_HIP;
+    }
+    return 0;
+  }
+};
+
+template <typename T>
+int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sink, char* ws, hipStream_t s) {
+  const sse_cfg& c = m->cfg;
+  Plan p;
+  const WavlmWs w = wavlm_plan(m, B, L, p);
+  int Ts[8];
+  const int Tf = wavlm_frames(c, L, Ts);
+  const int H = c.hidden, nh = c.heads, F = c.ffn;
+  const int M = B * Tf;
+  const float eps = c.ln_eps;
+  void* zero = ws + w.zero;
+  if (hipMemsetAsync(zero, 0, 256, s) != hipSuccess) return SSE_ERR_HIP;
+  const float* norm = nullptr;
+  if (c.do_normalize) {
+    RC(launch_wave_stats(wave, B, L, (float*)(ws + w.norm), s));
+    norm = (const float*)(ws + w.norm);
+  }
+  // ---- conv feature encoder ----
+  const int C0 = c.conv_dim[0];
+  T* bufs[2] = {(T*)(ws + w.bufA), (T*)(ws + w.bufB)};
+  if (c.feat_norm_layer) return SSE_ERR_UNSUPPORTED;   // WavLM-large frontend: SURVEY §8(f) next-2
+  RC(prof(m, s, "conv0_gn", 2.0 * B * (double)Ts[0] * C0 * c.conv_kernel[0], 0, [&] { return launch_conv0_gn<T>(wave, B, L, norm, m->ptr<float>(m->conv_w[0]),
+                        m->conv_b[0] ? m->ptr<float>(m->conv_b[0]) : nullptr, C0, c.conv_kernel[0],
+                        c.conv_stride[0], Ts[0], m->ptr<float>(m->conv_ln_w[0]), m->ptr<float>(m->conv_ln_b[0]),
+                        1e-5f, (double2*)(ws + w.part), (float2*)(ws + w.ss), bufs[0], s); }));
+  for (int i = 1; i < c.n_conv; ++i) {
+    const int cin = c.conv_dim[i - 1], co = c.conv_dim[i], k = c.conv_kernel[i], st = c.conv_stride[i];
+    GemmArgs g{};
+    g.A = bufs[(i - 1) & 1]; g.B = m->ptr(m->conv_w[i]);
+    g.M = B * Ts[i]; g.N = co; g.K = k * cin;
+    g.rows_per_seg = Ts[i]; g.seg_stride = (long long)Ts[i - 1] * cin; g.lda = (long long)st * cin;
+    g.bias = m->conv_b[i] ? m->ptr<float>(m->conv_b[i]) : nullptr;
+    g.Ct = bufs[i & 1]; g.ldc = co; g.act = ACT_GELU; g.zero = zero;
+    RC(prof(m, s, "gemm:conv", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+  }
+  const T* feat = bufs[(c.n_conv - 1) & 1];
+  const int C = c.conv_dim[c.n_conv - 1];
+  // ---- feature projection ----
+  float* x = (float*)(ws + w.x);
+  T* xt = (T*)(ws + w.xt);
+  T* xb = (T*)(ws + w.xb);
+  RC((launch_layernorm<T, T>(feat, m->ptr<float>(m->fp_ln_w), m->ptr<float>(m->fp_ln_b), M, C, eps, ACT_NONE,
+                             nullptr, xb, s)));
+  {
+    GemmArgs g{};
+    g.A = xb; g.B = m->ptr(m->fp_w); g.M = M; g.N = H; g.K = C;
+    g.rows_per_seg = M; g.seg_stride = 0; g.lda = C;
+    g.bias = m->ptr<float>(m->fp_b); g.Cf = x; g.Ct = xt; g.ldc = H; g.act = ACT_NONE; g.zero = zero;
+    RC(prof(m, s, "gemm:proj", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+  }
+  // ---- positional conv embedding: x = x + gelu(conv(x) + b) ----
+  {
+    const int G = c.pos_groups, cg = H / G, K = c.pos_kernel;
+    GemmArgs g{};
+    g.A = xt; g.B = m->ptr(m->pos_w); g.M = M; g.N = cg; g.K = K * cg;
+    g.rows_per_seg = Tf; g.T_in = Tf; g.stride = 1; g.pad = K / 2; g.cin = cg; g.ld_in = H;
+    g.bias = m->ptr<float>(m->pos_b); g.resid = x; g.Cf = x; g.ldc = H; g.act = ACT_GELU; g.zero = zero;
+    RC(prof(m, s, "gemm_conv:posconv", gflops(g, G), 0, [&] { return launch_gemm<T>(g, AMODE_CONV, G, s); }));
+  }
+  if (!c.stable_layer_norm)
+    RC((launch_layernorm<float, T>(x, m->ptr<float>(m->enc_ln_w), m->ptr<float>(m->enc_ln_b), M, H, eps, ACT_NONE,
+                                   x, xb, s)));
+  RC(sink.emit(0, x));
+  // ---- encoder layers ----
+  T* qkv = (T*)(ws + w.qkv);
+  T* ctx = (T*)(ws + w.ctx);
+  T* ff = (T*)(ws + w.ff);
+  float* hf = c.stable_layer_norm ? (float*)(ws + w.hf) : nullptr;
+  for (int l = 0; l < c.layers; ++l) {
+    const LayerW& Lw = m->layers[l];
+    const float* gate_in = x;
+    if (c.stable_layer_norm) {
+      RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, ACT_NONE, hf,
+                                     xb, s)));
+      gate_in = hf;
+    }
+    GemmArgs g{};
+    g.A = xb; g.B = m->ptr(Lw.qkv_w); g.M = M; g.N = 3 * H; g.K = H;
+    g.rows_per_seg = M; g.lda = H; g.bias = m->ptr<float>(Lw.qkv_b); g.Ct = qkv; g.ldc = 3 * H; g.zero = zero;
+    RC(prof(m, s, "gemm:qkv", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    AttnArgs a{};
+    a.qkv = qkv; a.out = ctx; a.T = Tf; a.H = H; a.nh = nh; a.scale = 0.125f;
+    a.gx = gate_in; a.gw = m->ptr<float>(Lw.g_w); a.gb = m->ptr<float>(Lw.g_b);
+    a.gconst = m->ptr<float>(Lw.g_const); a.relb = m->ptr<float>(m->relb); a.maxd = MAXD;
+    if (Tf > MAXD) return SSE_ERR_UNSUPPORTED;
+    RC(prof(m, s, "attn", 4.0 * B * (double)Tf * Tf * H, 0, [&] { return launch_attention<T>(a, B, s); }));
+    g = GemmArgs{};
+    g.A = ctx; g.B = m->ptr(Lw.o_w); g.M = M; g.N = H; g.K = H; g.rows_per_seg = M; g.lda = H;
+    g.bias = m->ptr<float>(Lw.o_b); g.resid = x; g.Cf = x; g.ldc = H; g.zero = zero;
+    RC(prof(m, s, "gemm:oproj", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    if (!c.stable_layer_norm) {
+      RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, ACT_NONE, x,
+                                     xb, s)));
+    } else {
+      RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, H, eps, ACT_NONE,
+                                     nullptr, xb, s)));
+    }
+    g = GemmArgs{};
+    g.A = xb; g.B = m->ptr(Lw.f1_w); g.M = M; g.N = F; g.K = H; g.rows_per_seg = M; g.lda = H;
+    g.bias = m->ptr<float>(Lw.f1_b); g.Ct = ff; g.ldc = F; g.act = ACT_GELU; g.zero = zero;
+    RC(prof(m, s, "gemm:ffn1", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    g = GemmArgs{};
+    g.A = ff; g.B = m->ptr(Lw.f2_w); g.M = M; g.N = H; g.K = F; g.rows_per_seg = M; g.lda = F;
+    g.bias = m->ptr<float>(Lw.f2_b); g.resid = x; g.Cf = x; g.ldc = H; g.zero = zero;
+    RC(prof(m, s, "gemm:ffn2", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    if (!c.stable_layer_norm) {
+      RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, H, eps, ACT_NONE, x,
+                                     xb, s)));
+    }
+    if (l + 1 < c.layers || !c.stable_layer_norm) RC(sink.emit(l + 1, x));
+  }
+  if (c.stable_layer_norm) {
+    RC((launch_layernorm<float, T>(x, m->ptr<float>(m->enc_ln_w), m->ptr<float>(m->enc_ln_b), M, H, eps, ACT_NONE,
+                                   x, xb, s)));
+    RC(sink.emit(c.layers, x));
+  }
+  return 0;
+}
+
+template <typename T>
+int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& sink, char* ws, hipStream_t s,
+                    const float* mel_hf = nullptr) {
+  const sse_cfg& c = m->cfg;
+  Plan p;
+  const WhisperWs w = whisper_plan(m, B, p);
+  const int D = c.hidden, F = c.ffn, nh = c.heads, Tq = c.max_positions, T2 = 2 * Tq, nm = c.n_mels;
+  const int M = B * Tq;
+  const float eps = c.ln_eps;
+  void* zero = ws + w.zero;
+  if (hipMemsetAsync(zero, 0, 256, s) != hipSuccess) return SSE_ERR_HIP;
+  T* mel = (T*)(ws + w.mel);
+  if (mel_hf)
+    RC(launch_mel_to_cl<T>(mel_hf, B, nm, mel, s));
+  else
+    RC(prof(m, s, "logmel", 2.0 * B * 3000.0 * LM_NB * 400, (double)B * (480000.0 * 4 + 3000.0 * nm * sizeof(T)),
+            [&] { return launch_logmel<T>(wave, B, L, nm, nullptr, mel, ws + w.lm, logmel_workspace_bytes(B, nm), s); }));
+  T* h1 = (T*)(ws + w.h1);
+  float* x = (float*)(ws + w.x);
+  T* xb = (T*)(ws + w.xb);
+  {
+    GemmArgs g{};   // conv1: k3 pad1, 80 -> D, GELU
+    g.A = mel; g.B = m->ptr(m->c1_w); g.M = B * T2; g.N = D; g.K = 3 * nm;
+    g.rows_per_seg = T2; g.T_in = T2; g.stride = 1; g.pad = 1; g.cin = nm; g.ld_in = nm;
+    g.bias = m->ptr<float>(m->c1_b); g.Ct = h1; g.ldc = D; g.act = ACT_GELU; g.zero = zero;
+    RC(prof(m, s, "gemm_conv:conv1", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_CONV, 1, s); }));
+    g = GemmArgs{};   // conv2: k3 s2 pad1, GELU, + embed_positions
+    g.A = h1; g.B = m->ptr(m->c2_w); g.M = M; g.N = D; g.K = 3 * D;
+    g.rows_per_seg = Tq; g.T_in = T2; g.stride = 2; g.pad = 1; g.cin = D; g.ld_in = D;
+    g.bias = m->ptr<float>(m->c2_b); g.resid = m->ptr<float>(m->positions); g.resid_rows = Tq;
+    g.Cf = x; g.ldc = D; g.act = ACT_GELU; g.zero = zero;
+    RC(prof(m, s, "gemm_conv:conv2", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_CONV, 1, s); }));
+  }
+  RC(sink.emit(0, x));
+  T* qkv = (T*)(ws + w.qkv);
+  T* ctx = (T*)(ws + w.ctx);
+  T* ff = (T*)(ws + w.ff);
+  for (int l = 0; l < c.layers; ++l) {
+    const LayerW& Lw = m->layers[l];
+    RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, D, eps, ACT_NONE, nullptr,
+                                   xb, s)));
+    GemmArgs g{};
+    g.A = xb; g.B = m->ptr(Lw.qkv_w); g.M = M; g.N = 3 * D; g.K = D; g.rows_per_seg = M; g.lda = D;
+    g.bias = m->ptr<float>(Lw.qkv_b); g.Ct = qkv; g.ldc = 3 * D; g.zero = zero;
+    RC(prof(m, s, "gemm:qkv", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    AttnArgs a{};
+    a.qkv = qkv; a.out = ctx; a.T = Tq; a.H = D; a.nh = nh; a.scale = 1.0f;
+    RC(prof(m, s, "attn", 4.0 * B * (double)Tq * Tq * D, 0, [&] { return launch_attention<T>(a, B, s); }));
+    g = GemmArgs{};
+    g.A = ctx; g.B = m->ptr(Lw.o_w); g.M = M; g.N = D; g.K = D; g.rows_per_seg = M; g.lda = D;
+    g.bias = m->ptr<float>(Lw.o_b); g.resid = x; g.Cf = x; g.ldc = D; g.zero = zero;
+    RC(prof(m, s, "gemm:oproj", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, D, eps, ACT_NONE, nullptr,
+                                   xb, s)));
+    g = GemmArgs{};
+    g.A = xb; g.B = m->ptr(Lw.f1_w); g.M = M; g.N = F; g.K = D; g.rows_per_seg = M; g.lda = D;
+    g.bias = m->ptr<float>(Lw.f1_b); g.Ct = ff; g.ldc = F; g.act = ACT_GELU; g.zero = zero;
+    RC(prof(m, s, "gemm:ffn1", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    g = GemmArgs{};
+    g.A = ff; g.B = m->ptr(Lw.f2_w); g.M = M; g.N = D; g.K = F; g.rows_per_seg = M; g.lda = F;
+    g.bias = m->ptr<float>(Lw.f2_b); g.resid = x; g.Cf = x; g.ldc = D; g.zero = zero;
+    RC(prof(m, s, "gemm:ffn2", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    if (l + 1 < c.layers) RC(sink.emit(l + 1, x));
+  }
+  // hidden_states[-1] is the post-LN last_hidden_state (HF/utils/output_capturing.py:268-279)
+  float* xf = (float*)(ws + w.xf);
+  RC((launch_layernorm<float, T>(x, m->ptr<float>(m->enc_ln_w), m->ptr<float>(m->enc_ln_b), M, D, eps, ACT_NONE, xf,
+                                 (T*)nullptr, s)));
+  RC(sink.emit(c.layers, xf));
+  return 0;
+}
+
+int forward(sse_model* m, const float* d_in, int B, int L, const Sink& sink, void* d_ws, size_t ws_bytes,
+            hipStream_t s, bool from_mel = false) {
+  if (!m || !d_in || B <= 0 || L <= 0) return SSE_ERR_INVALID;
+  if (ws_bytes < sse_workspace_bytes(m, B, L)) return SSE_ERR_WORKSPACE;
+  if (m->cfg.kind == SSE_KIND_WAVLM && wavlm_frames(m->cfg, L, nullptr) <= 0) return SSE_ERR_INVALID;
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) return SSE_ERR_HIP;
+  if (dev != m->device && hipSetDevice(m->device) != hipSuccess) return SSE_ERR_HIP;
+  int rc;
+  if (m->cfg.kind == SSE_KIND_WAVLM)
+    rc = m->bf() ? wavlm_forward<bf16>(m, d_in, B, L, sink, (char*)d_ws, s)
+                 : wavlm_forward<float>(m, d_in, B, L, sink, (char*)d_ws, s);
+  else
+    rc = m->bf() ? whisper_forward<bf16>(m, d_in, B, L, sink, (char*)d_ws, s, from_mel ? d_in : nullptr)
+                 : whisper_forward<float>(m, d_in, B, L, sink, (char*)d_ws, s, from_mel ? d_in : nullptr);
+  if (dev != m->device) (void)hipSetDevice(dev);
+  return rc;
+}
+
+int hs_frames(const sse_model* m, int L) {
+  return m->cfg.kind == SSE_KIND_WAVLM ? wavlm_frames(m->cfg, L, nullptr) : m->cfg.max_positions;
+}
+
+}  // namespace
+
+// ======================================= C-ABI ==========================================
+extern "C" {
+
+const char* sse_version(void) { return SSE_VERSION; }
+
+const char* sse_strerror(int err) {
+  switch (err) {
+    case SSE_OK: return "ok";
+    case SSE_ERR_INVALID: return "invalid argument";
+    case SSE_ERR_HIP: return "HIP runtime error";
+    case SSE_ERR_UNSUPPORTED: return "unsupported shape";
+    case SSE_ERR_WORKSPACE: return "workspace too small";
+    case SSE_ERR_WEIGHTS: return "weight blob size does not match the config";
+    case SSE_ERR_OOM: return "HIP out of memory";
+    default: return "unknown error";
+  }
+}
+
+int sse_rel_bucket(int d, int num_buckets, int max_distance) { return rel_bucket(d, num_buckets, max_distance); }
+
+int sse_mel_filters(int n_mels, float* out) {
+  if (n_mels <= 0 || !out) return SSE_ERR_INVALID;
+  auto h2m = [](double f) { return f >= 1000.0 ? 15.0 + std::log(f / 1000.0) * (27.0 / std::log(6.4)) : 3.0 * f / 200.0; };
+  auto m2h = [](double m) { return m >= 15.0 ? 1000.0 * std::exp((std::log(6.4) / 27.0) * (m - 15.0)) : 200.0 * m / 3.0; };
+  const int NF = 201;
+  const double mmin = h2m(0.0), mmax = h2m(8000.0), step = (mmax - mmin) / (n_mels + 1);
+  for (int f = 0; f < NF; ++f)
+    for (int m = 0; m < n_mels; ++m) {
+      const double f0 = m2h(mmin + step * m), f1 = m2h(mmin + step * (m + 1)), f2 = m2h(mmin + step * (m + 2));
+      const double ff = 8000.0 * f / (NF - 1);
+      double v = std::fmin((ff - f0) / (f1 - f0), (f2 - ff) / (f2 - f1));
+      v = v > 0.0 ? v : 0.0;
+      out[f * n_mels + m] = (float)(v * (2.0 / (f2 - f0)));
+    }
+  return SSE_OK;
+}
+
+size_t sse_weight_floats(const sse_cfg* cfg) {
+  if (!cfg_valid(cfg)) return 0;
+  sse_model tmp{};
+  tmp.cfg = *cfg;
+  Blob bl{nullptr, (size_t)-1};
+  Arena ar;
+  const int rc = cfg->kind == SSE_KIND_WAVLM ? build_wavlm(&tmp, bl, ar) : build_whisper(&tmp, bl, ar);
+  return rc == SSE_OK ? bl.off : 0;
+}
+
+int sse_model_create(const sse_cfg* cfg, const float* host_weights, size_t nbytes, int device, int dtype,
+                     sse_model** out) {
+  if (!out || !host_weights || !cfg_valid(cfg) || (dtype != SSE_DTYPE_F32 && dtype != SSE_DTYPE_BF16))
+    return SSE_ERR_INVALID;
+  *out = nullptr;
+  const size_t need = sse_weight_floats(cfg);
+  if (need == 0 || nbytes != need * 4) return SSE_ERR_WEIGHTS;
+  sse_model* m = new (std::nothrow) sse_model();
+  if (!m) return SSE_ERR_OOM;
+  m->cfg = *cfg;
+  m->device = device;
+  m->dtype = dtype;
+  Blob bl{host_weights, need};
+  Arena ar;
+  const int rc = cfg->kind == SSE_KIND_WAVLM ? build_wavlm(m, bl, ar) : build_whisper(m, bl, ar);
+  if (rc != SSE_OK || bl.off != need) { delete m; return SSE_ERR_WEIGHTS; }
+  m->zero = ar.put(nullptr, 256);
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) { delete m; return SSE_ERR_HIP; }
+  m->dbytes = ar.size;
+  if (hipMalloc((void**)&m->dmem, ar.size) != hipSuccess) {
+    (void)hipSetDevice(prev);
+    delete m;
+    return SSE_ERR_OOM;
+  }
+  std::vector<char> staging(ar.size, 0);
+  for (auto& pr : ar.pending) std::memcpy(staging.data() + pr.first, pr.second.data(), pr.second.size());
+  const bool okc = hipMemcpy(m->dmem, staging.data(), ar.size, hipMemcpyHostToDevice) == hipSuccess;
+  (void)hipSetDevice(prev);
+  if (!okc) { (void)hipFree(m->dmem); delete m; return SSE_ERR_HIP; }
+  *out = m;
+  return SSE_OK;
+}
+
+void sse_model_destroy(sse_model* m) {
+  if (!m) return;
+  for (auto e : m->prof.ev) (void)hipEventDestroy(e);
+  if (m->dmem) {
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(m->device);
+    (void)hipFree(m->dmem);
+    (void)hipSetDevice(prev);
+  }
+  delete m;
+}
+
+int sse_output_frames(const sse_model* m, int L) {
+  if (!m || L <= 0) return SSE_ERR_INVALID;
+  return hs_frames(m, L);
+}
+
+size_t sse_workspace_bytes(const sse_model* m, int B, int L) {
+  if (!m || B <= 0 || L <= 0) return 0;
+  Plan p;
+  if (m->cfg.kind == SSE_KIND_WAVLM) {
+    if (wavlm_frames(m->cfg, L, nullptr) <= 0) return 0;
+    wavlm_plan(m, B, L, p);
+  } else {
+    whisper_plan(m, B, p);
+  }
+  return p.total;
+}
+
+size_t sse_logmel_workspace_bytes(int B, int n_mels) { return logmel_workspace_bytes(B, n_mels); }
+
+int sse_logmel(const float* d_wave, int B, int L, int n_mels, float* d_mel, void* d_ws, size_t ws_bytes,
+               void* stream) {
+  if (!d_wave || !d_mel || !d_ws) return SSE_ERR_INVALID;
+  return launch_logmel<float>(d_wave, B, L, n_mels, d_mel, (float*)nullptr, d_ws, ws_bytes, (hipStream_t)stream);
+}
+
+int sse_embed(sse_model* m, const float* d_in, int B, int L, const int32_t* layer_ids, int n_layers, float* d_out,
+              void* d_ws, size_t ws_bytes, void* stream) {
+  if (!m || !layer_ids || n_layers <= 0 || !d_out) return SSE_ERR_INVALID;
+  for (int i = 0; i < n_layers; ++i)
+    if (layer_ids[i] < 0 || layer_ids[i] > m->cfg.layers) return SSE_ERR_INVALID;
+  Sink sk{layer_ids, n_layers, d_out, nullptr, B, hs_frames(m, L), m->cfg.hidden, (hipStream_t)stream};
+  return forward(m, d_in, B, L, sk, d_ws, ws_bytes, (hipStream_t)stream);
+}
+
+int sse_hidden_states(sse_model* m, const float* d_in, int B, int L, float* d_hs, void* d_ws, size_t ws_bytes,
+                      void* stream) {
+  if (!m || !d_hs) return SSE_ERR_INVALID;
+  Sink sk{nullptr, 0, nullptr, d_hs, B, hs_frames(m, L), m->cfg.hidden, (hipStream_t)stream};
+  return forward(m, d_in, B, L, sk, d_ws, ws_bytes, (hipStream_t)stream);
+}
+
+int sse_whisper_hidden_states_from_mel(sse_model* m, const float* d_mel, int B, float* d_hs, void* d_ws,
+                                       size_t ws_bytes, void* stream) {
+  if (!m || !d_hs || m->cfg.kind != SSE_KIND_WHISPER) return SSE_ERR_INVALID;
+  Sink sk{nullptr, 0, nullptr, d_hs, B, m->cfg.max_positions, m->cfg.hidden, (hipStream_t)stream};
+  return forward(m, d_mel, B, 2 * m->cfg.max_positions, sk, d_ws, ws_bytes, (hipStream_t)stream, true);
+}
+
+int sse_profile_start(sse_model* m, int max_launches) {
+  if (!m || max_launches <= 0) return SSE_ERR_INVALID;
+  auto& P = m->prof;
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(m->device) != hipSuccess) return SSE_ERR_HIP;
+  while ((int)P.ev.size() < 2 * max_launches) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) { (void)hipSetDevice(prev); return SSE_ERR_HIP; }
+    P.ev.push_back(e);
+  }
+  (void)hipSetDevice(prev);
+  P.on = true;
+  P.used = 0;
+  P.tag.clear(); P.flops.clear(); P.bytes.clear();
+  return SSE_OK;
+}
+
+int sse_profile_read(sse_model* m, int cap, char* tags, float* ms, double* flops, double* bytes) {
+  if (!m || cap < 0) return SSE_ERR_INVALID;
+  auto& P = m->prof;
+  const int n = (int)P.tag.size();
+  if (n > 0 && hipEventSynchronize(P.ev[2 * n - 1]) != hipSuccess) return SSE_ERR_HIP;
+  for (int i = 0; i < n && i < cap; ++i) {
+    float t = 0.f;
+    if (hipEventElapsedTime(&t, P.ev[2 * i], P.ev[2 * i + 1]) != hipSuccess) return SSE_ERR_HIP;
+    if (ms) ms[i] = t;
+    if (flops) flops[i] = P.flops[i];
+    if (bytes) bytes[i] = P.bytes[i];
+    if (tags) { std::strncpy(tags + 32 * i, P.tag[i].c_str(), 31); tags[32 * i + 31] = 0; }
+  }
+  P.used = 0;
+  P.tag.clear(); P.flops.clear(); P.bytes.clear();
+  return n;
+}
+
+int sse_profile_stop(sse_model* m) {
+  if (!m) return SSE_ERR_INVALID;
+  m->prof.on = false;
+  m->prof.used = 0;
+  m->prof.tag.clear(); m->prof.flops.clear(); m->prof.bytes.clear();
+  return SSE_OK;
+}
+
+size_t sse_normalize_workspace_bytes(int B) { return (size_t)B * 8; }
+
+int sse_normalize(const float* d_in, int B, int L, float* d_out, void* d_ws, size_t ws_bytes, void* stream) {
+  if (!d_in || !d_out || !d_ws || B <= 0 || L <= 0) return SSE_ERR_INVALID;
+  if (ws_bytes < (size_t)B * 8) return SSE_ERR_WORKSPACE;
+  RC(launch_wave_stats(d_in, B, L, (float*)d_ws, (hipStream_t)stream));
+  return launch_normalize_apply(d_in, B, L, (const float*)d_ws, d_out, (hipStream_t)stream);
+}
+
+}  // extern "C"

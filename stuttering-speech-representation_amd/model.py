@@ -1,0 +1,216 @@
+"""Host-side model handle over libsse.so: weights in, batched embeddings out.
+
+``SSEModel`` is the perf surface of SURVEY.md §8(b):
+``embed(wave[B, L]) -> [B, n_layers, H]`` (the fused mean-pooled output of
+``extract_wavlm_embeddings`` / ``extract_whisper_embeddings_fixed`` for a whole batch),
+plus ``hidden_states`` (the full HF-shaped tuple, materialised only on request).
+
+Every tensor argument lives on the model's GPU; all compute runs in the HIP kernels of
+``csrc/`` on the current torch stream.  There is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import WavLMSpec, WhisperSpec, param_specs
+
+DTYPES = {"fp32": _lib.SSE_DTYPE_F32, "float32": _lib.SSE_DTYPE_F32, "f32": _lib.SSE_DTYPE_F32,
+          "bf16": _lib.SSE_DTYPE_BF16, "bfloat16": _lib.SSE_DTYPE_BF16}
+
+
+def _as_numpy(v) -> np.ndarray:
+    if isinstance(v, torch.Tensor):
+        v = v.detach().to("cpu", torch.float32).numpy()
+    return np.ascontiguousarray(np.asarray(v, dtype=np.float32))
+
+
+def pack_weights(spec, state_dict: dict) -> np.ndarray:
+    """Concatenate an HF state dict into the canonical fp32 blob (config.param_specs order).
+
+    Accepts WavLMModel / WhisperModel state dicts (``encoder.``-prefixed keys for Whisper, as
+    ``WhisperModel.state_dict()`` has them) with numpy arrays or torch tensors; the legacy
+    ``weight_g`` / ``weight_v`` names of the WavLM pos-conv weight norm are mapped to the
+    parametrization names.
+    """
+    sd = dict(state_dict)
+    pre = "encoder.pos_conv_embed.conv."
+    if pre + "weight_g" in sd and pre + "parametrizations.weight.original0" not in sd:
+        sd[pre + "parametrizations.weight.original0"] = sd.pop(pre + "weight_g")
+        sd[pre + "parametrizations.weight.original1"] = sd.pop(pre + "weight_v")
+    parts = []
+    for key, shape in param_specs(spec):
+        if key not in sd:
+            raise KeyError(f"state dict lacks {key}")
+        a = _as_numpy(sd[key])
+        if tuple(a.shape) != tuple(shape):
+            raise ValueError(f"{key}: shape {tuple(a.shape)} != expected {tuple(shape)}")
+        parts.append(a.ravel())
+    return np.concatenate(parts)
+
+
+class SSEModel:
+    """One model on one GPU.  ``dtype``: "bf16" (throughput path) or "fp32" (parity path)."""
+
+    def __init__(self, spec, state_dict: dict, device="cuda:0", dtype: str = "bf16", do_normalize: bool = False):
+        if not isinstance(spec, (WavLMSpec, WhisperSpec)):
+            raise TypeError(spec)
+        self.spec = spec
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("SSEModel runs on a GPU device (no CPU fallback)")
+        self.dtype = dtype
+        self.do_normalize = bool(do_normalize)
+        L = _lib.lib()
+        self._cfg = _lib.make_cfg(spec, do_normalize)
+        blob = pack_weights(spec, state_dict)
+        need = L.sse_weight_floats(ctypes.byref(self._cfg))
+        if need != blob.size:
+            raise ValueError(f"weight blob has {blob.size} floats, library expects {need}")
+        h = ctypes.c_void_p()
+        idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self.device = torch.device("cuda", idx)
+        torch.cuda.set_device(self.device)   # make sure the HIP context exists on this device
+        _lib.check(L.sse_model_create(ctypes.byref(self._cfg), blob.ctypes.data, blob.nbytes, idx,
+                                      DTYPES[dtype], ctypes.byref(h)), "sse_model_create")
+        self._h = h
+        self._ws = None
+
+    # -- plumbing -------------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _lib.lib().sse_model_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def hidden_size(self) -> int:
+        return self.spec.hidden
+
+    def output_frames(self, n_samples: int) -> int:
+        return _lib.lib().sse_output_frames(self._h, int(n_samples))
+
+    def workspace(self, B: int, L: int) -> torch.Tensor:
+        n = _lib.lib().sse_workspace_bytes(self._h, int(B), int(L))
+        if n == 0:
+            raise _lib.SSEError(-1, f"sse_workspace_bytes(B={B}, L={L})")
+        if self._ws is None or self._ws.numel() < n:
+            self._ws = None
+            self._ws = torch.empty(n, dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _check_wave(self, wave: torch.Tensor) -> torch.Tensor:
+        if not isinstance(wave, torch.Tensor) or wave.device != self.device:
+            raise ValueError(f"expected a tensor on {self.device}")
+        if wave.dim() == 1:
+            wave = wave[None]
+        if wave.dim() != 2:
+            raise ValueError("expected [B, L] waves")
+        return wave.to(torch.float32).contiguous()
+
+    # -- live launch timing (bench.py) ------------------------------------------------------
+    def profile_start(self, max_launches: int = 8192) -> None:
+        _lib.check(_lib.lib().sse_profile_start(self._h, int(max_launches)), "sse_profile_start")
+        self._prof_cap = int(max_launches)
+
+    def profile_read(self) -> list:
+        """[(tag, ms, flops, bytes)] for every launch since profile_start / the last read."""
+        cap = self._prof_cap
+        tags = ctypes.create_string_buffer(32 * cap)
+        ms = np.zeros(cap, np.float32)
+        fl = np.zeros(cap, np.float64)
+        by = np.zeros(cap, np.float64)
+        n = _lib.lib().sse_profile_read(self._h, cap, tags, ms.ctypes.data, fl.ctypes.data, by.ctypes.data)
+        if n < 0:
+            _lib.check(n, "sse_profile_read")
+        raw = tags.raw
+        return [(raw[32 * i:32 * i + 32].split(b"\0", 1)[0].decode(), float(ms[i]), float(fl[i]), float(by[i]))
+                for i in range(min(n, cap))]
+
+    def profile_stop(self) -> None:
+        _lib.check(_lib.lib().sse_profile_stop(self._h), "sse_profile_stop")
+
+    # -- compute --------------------------------------------------------------------------
+    def embed(self, wave: torch.Tensor, layer_indices, out: torch.Tensor | None = None) -> torch.Tensor:
+        """[B, L] fp32 16 kHz waves -> [B, len(layer_indices), H] fp32 time-means of hidden states."""
+        wave = self._check_wave(wave)
+        B, L = wave.shape
+        ids = torch.tensor([int(i) for i in layer_indices], dtype=torch.int32)
+        n = ids.numel()
+        if out is None:
+            out = torch.empty((B, n, self.spec.hidden), dtype=torch.float32, device=self.device)
+        ws = self.workspace(B, L)
+        _lib.check(_lib.lib().sse_embed(self._h, wave.data_ptr(), B, L, ids.data_ptr(), n, out.data_ptr(),
+                                        ws.data_ptr(), ws.numel(), self._stream()), "sse_embed")
+        return out
+
+    def hidden_states(self, wave: torch.Tensor) -> tuple:
+        """[B, L] -> tuple of layers+1 tensors [B, T, H] (HF ``output_hidden_states`` semantics)."""
+        wave = self._check_wave(wave)
+        B, L = wave.shape
+        T = self.output_frames(L)
+        n_hs = self.spec.layers + 1
+        hs = torch.empty((n_hs, B, T, self.spec.hidden), dtype=torch.float32, device=self.device)
+        ws = self.workspace(B, L)
+        _lib.check(_lib.lib().sse_hidden_states(self._h, wave.data_ptr(), B, L, hs.data_ptr(), ws.data_ptr(),
+                                                ws.numel(), self._stream()), "sse_hidden_states")
+        return tuple(hs.unbind(0))
+
+    def hidden_states_from_mel(self, mel: torch.Tensor) -> tuple:
+        """Whisper only: [B, n_mels, 3000] log-mel -> layers+1 tensors [B, 1500, H]."""
+        if not isinstance(self.spec, WhisperSpec):
+            raise TypeError("hidden_states_from_mel is Whisper-only")
+        if mel.device != self.device:
+            raise ValueError(f"expected a tensor on {self.device}")
+        mel = mel.to(torch.float32).contiguous()
+        if mel.dim() != 3 or mel.shape[1] != self.spec.n_mels or mel.shape[2] != 2 * self.spec.max_positions:
+            raise ValueError(f"expected [B, {self.spec.n_mels}, {2 * self.spec.max_positions}] log-mel, "
+                             f"got {tuple(mel.shape)}")
+        B = mel.shape[0]
+        T = self.spec.max_positions
+        hs = torch.empty((self.spec.layers + 1, B, T, self.spec.hidden), dtype=torch.float32, device=self.device)
+        ws = self.workspace(B, self.spec.n_samples)
+        _lib.check(_lib.lib().sse_whisper_hidden_states_from_mel(self._h, mel.data_ptr(), B, hs.data_ptr(),
+                                                                 ws.data_ptr(), ws.numel(), self._stream()),
+                   "sse_whisper_hidden_states_from_mel")
+        return tuple(hs.unbind(0))
+
+
+def logmel(wave: torch.Tensor, n_mels: int = 80) -> torch.Tensor:
+    """Whisper log-mel on device: [B, L] (L <= 480000) -> [B, n_mels, 3000] (HF layout)."""
+    if wave.dim() == 1:
+        wave = wave[None]
+    wave = wave.to(torch.float32).contiguous()
+    B, L = wave.shape
+    L_ = _lib.lib()
+    n = L_.sse_logmel_workspace_bytes(B, n_mels)
+    ws = torch.empty(n, dtype=torch.uint8, device=wave.device)
+    out = torch.empty((B, n_mels, 3000), dtype=torch.float32, device=wave.device)
+    _lib.check(L_.sse_logmel(wave.data_ptr(), B, L, n_mels, out.data_ptr(), ws.data_ptr(), n,
+                             ctypes.c_void_p(torch.cuda.current_stream(wave.device).cuda_stream)), "sse_logmel")
+    return out
+
+
+def normalize(wave: torch.Tensor) -> torch.Tensor:
+    """Wav2Vec2FeatureExtractor(do_normalize=True) on device: per-clip zero mean / unit variance."""
+    if wave.dim() == 1:
+        wave = wave[None]
+    wave = wave.to(torch.float32).contiguous()
+    B, L = wave.shape
+    ws = torch.empty(8 * B, dtype=torch.uint8, device=wave.device)
+    out = torch.empty_like(wave)
+    _lib.check(_lib.lib().sse_normalize(wave.data_ptr(), B, L, out.data_ptr(), ws.data_ptr(), ws.numel(),
+                                        ctypes.c_void_p(torch.cuda.current_stream(wave.device).cuda_stream)),
+               "sse_normalize")
+    return out

@@ -1,0 +1,206 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures by running the REFERENCE's own glue (container only).
+
+Runs ``extract_wavlm_embeddings`` (REF/WavLM_embeddings.py:267-341) and
+``extract_whisper_embeddings_fixed`` (REF/whisper_embeddings_large.py:234-299) exactly as
+the reference calls them, on HF models (transformers, third-party, version recorded in
+the manifest) built offline and loaded with the deterministic synthetic weights of
+``synth.py`` (no hub access: SURVEY.md §8(c)).
+
+* ``torchaudio`` is absent here; a stub whose ``load(path)`` returns the synthetic clip
+  registered for that path is installed AFTER ``import transformers``.
+* The reference is imported by path from a temp cwd (it creates ``logs/`` at import) with
+  ``sys.dont_write_bytecode = True`` so nothing is written under /root/reference.
+* Only inputs and outputs are written (small .npz files + manifest.json); nothing from the
+  reference travels with them.
+
+Usage: python tests/golden/make_golden.py [--skip-large]
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import importlib
+import importlib.util
+import json
+import os
+import sys
+import tempfile
+import time
+import types
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import transformers  # noqa: E402  (must precede the torchaudio stub)
+
+ssr = importlib.import_module("stuttering-speech-representation_amd")
+from ssr_amd import config as C, synth  # noqa: E402
+
+REF = "/root/reference"
+_CLIPS: dict[str, np.ndarray] = {}
+
+
+def _install_torchaudio_stub():
+    ta = types.ModuleType("torchaudio")
+
+    def load(path):
+        return torch.from_numpy(_CLIPS[path][None, :].copy()), 16000
+
+    ta.load = load
+    tr = types.ModuleType("torchaudio.transforms")
+
+    class Resample:  # never used: every synthetic clip is already 16 kHz
+        def __init__(self, *a, **k):
+            raise RuntimeError("resample not expected")
+
+    tr.Resample = Resample
+    ta.transforms = tr
+    sys.modules["torchaudio"] = ta
+    sys.modules["torchaudio.transforms"] = tr
+
+
+def _import_ref(name, fname):
+    spec = importlib.util.spec_from_file_location(name, os.path.join(REF, fname))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def _sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def _sd_sha(sd: dict) -> str:
+    h = hashlib.sha256()
+    for k in sorted(sd):
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(sd[k]).tobytes())
+    return h.hexdigest()
+
+
+def _register(prefix, clips):
+    paths = []
+    for i, c in enumerate(clips):
+        p = f"/synthetic/{prefix}_{i:03d}.wav"
+        _CLIPS[p] = c
+        paths.append(p)
+    return paths
+
+
+def wavlm_golden(ref_w, manifest):
+    from transformers import Wav2Vec2FeatureExtractor, WavLMConfig, WavLMModel
+    spec = C.WAVLM_BASE
+    sd = synth.synth_wavlm_state_dict(spec, seed=7)
+    model = WavLMModel(WavLMConfig())
+    missing, unexpected = model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=False)
+    assert not unexpected and set(missing) == {"masked_spec_embed"}, (missing, unexpected)
+    model.eval()
+    clips = synth.synth_clips(16, 48000, seed=1234)
+    paths = _register("wavlm", clips)
+    out = {}
+    idx = spec.default_layer_indices()                  # [12, 11, 10, 6] (REF :506)
+    for do_norm in (False, True):
+        fe = Wav2Vec2FeatureExtractor(do_normalize=do_norm)
+        n = 16 if not do_norm else 4
+        t0 = time.time()
+        embs = []
+        for p in paths[:n]:
+            d = ref_w.extract_wavlm_embeddings(p, model, fe, "cpu", idx)
+            embs.append(np.stack([d[f"layer_{i}"] for i in idx]))
+        out[f"emb_norm{int(do_norm)}"] = np.stack(embs).astype(np.float32)
+        manifest[f"wavlm_emb_norm{int(do_norm)}_s"] = time.time() - t0
+    # all 13 pooled layers for 2 clips through the same reference function
+    fe = Wav2Vec2FeatureExtractor(do_normalize=False)
+    all_idx = list(range(spec.num_hidden_states))
+    out["emb_all_layers"] = np.stack([
+        np.stack([ref_w.extract_wavlm_embeddings(p, model, fe, "cpu", all_idx)[f"layer_{i}"] for i in all_idx])
+        for p in paths[:2]]).astype(np.float32)
+    # intermediates of clip 0 for kernel-level tests
+    with torch.no_grad():
+        x = torch.from_numpy(clips[:1])
+        feats = model.feature_extractor(x)                          # [1, 512, 149]
+        hs = model(x, output_hidden_states=True).hidden_states
+    out["frontend_clip0"] = feats[0].numpy().T.copy()           # [149, 512] channels-last
+    out["hs0_clip0"] = hs[0][0].numpy().copy()
+    out["hs1_clip0"] = hs[1][0].numpy().copy()
+    out["layer_indices"] = np.array(idx, dtype=np.int32)
+    np.savez_compressed(os.path.join(HERE, "wavlm_base.npz"), **out)
+    manifest["wavlm_base"] = {
+        "spec": spec.name, "weight_seed": 7, "clip_seed": 1234, "n_clips": 16, "n_samples": 48000,
+        "weights_sha256": _sd_sha(sd), "clips_sha256": _sha(clips), "layer_indices": idx,
+        "reference_fn": "REF/WavLM_embeddings.py:extract_wavlm_embeddings",
+        "feature_extractor": "Wav2Vec2FeatureExtractor(do_normalize=False|True)",
+    }
+
+
+def whisper_golden(ref_h, manifest, spec, tag, n_clips, seed, durations):
+    from transformers import WhisperConfig, WhisperFeatureExtractor, WhisperModel
+    sd = synth.synth_whisper_state_dict(spec, seed=seed)
+    cfg = WhisperConfig(d_model=spec.d_model, encoder_layers=spec.layers, encoder_attention_heads=spec.heads,
+                        decoder_layers=2, decoder_attention_heads=spec.heads, encoder_ffn_dim=spec.ffn,
+                        decoder_ffn_dim=spec.ffn, num_mel_bins=spec.n_mels, vocab_size=51865)
+    torch.manual_seed(0)
+    model = WhisperModel(cfg)
+    missing, unexpected = model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=False)
+    assert not unexpected and all(k.startswith("decoder.") for k in missing), unexpected
+    model.eval()
+    clips = [synth.synth_clips(1, int(16000 * d), seed=4321, first_clip=i)[0] for i, d in enumerate(durations)]
+    paths = _register(tag, clips)
+    proc = WhisperFeatureExtractor(feature_size=spec.n_mels)
+    enc_idx = spec.default_layer_indices()
+    dec_idx = [2, 1, 0]
+    t0 = time.time()
+    embs, decs = [], []
+    for p in paths[:n_clips]:
+        d = ref_h.extract_whisper_embeddings_fixed(p, model, proc, "cpu", enc_idx, dec_idx)
+        embs.append(np.stack([d[f"encoder_layer_{i}"] for i in enc_idx]))
+        decs.append(np.stack([d[f"decoder_layer_{i}"] for i in dec_idx]))
+    manifest[f"{tag}_s"] = time.time() - t0
+    mels = np.stack([proc(c, sampling_rate=16000, return_tensors="np").input_features[0] for c in clips[:n_clips]])
+    out = {"emb": np.stack(embs).astype(np.float32), "layer_indices": np.array(enc_idx, np.int32),
+           "mel": mels.astype(np.float32), "decoder_emb_unpinned": np.stack(decs).astype(np.float32)}
+    np.savez_compressed(os.path.join(HERE, f"{tag}.npz"), **out)
+    manifest[tag] = {"spec": spec.name, "weight_seed": seed, "clip_seed": 4321, "durations_s": durations[:n_clips],
+                     "clips_sha256": [_sha(c) for c in clips[:n_clips]],
+                     "weights_sha256": _sd_sha(sd), "layer_indices": enc_idx,
+                     "reference_fn": "REF/whisper_embeddings_large.py:extract_whisper_embeddings_fixed",
+                     "note": "decoder_emb_unpinned uses torch.manual_seed(0) decoder weights not reproducible "
+                             "off this container; kept for the next-1 row, not used by tests"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--skip-large", action="store_true")
+    args = ap.parse_args()
+    torch.set_num_threads(os.cpu_count())
+    manifest = {"transformers": transformers.__version__, "torch": torch.__version__, "numpy": np.__version__}
+    cwd = os.getcwd()
+    with tempfile.TemporaryDirectory() as td:
+        os.chdir(td)
+        try:
+            _install_torchaudio_stub()
+            ref_w = _import_ref("ref_wavlm_embeddings", "WavLM_embeddings.py")
+            ref_h = _import_ref("ref_whisper_embeddings_large", "whisper_embeddings_large.py")
+            wavlm_golden(ref_w, manifest)
+            whisper_golden(ref_h, manifest, C.WHISPER_TINY, "whisper_tiny", 2, 11, [3.0, 30.0])
+            if not args.skip_large:
+                whisper_golden(ref_h, manifest, C.WHISPER_LARGE_V2, "whisper_large_v2", 1, 11, [3.0])
+        finally:
+            os.chdir(cwd)
+    old = {}
+    mp = os.path.join(HERE, "manifest.json")
+    if os.path.exists(mp):
+        old = json.load(open(mp))
+    old.update(manifest)
+    with open(mp, "w") as f:
+        json.dump(old, f, indent=1, sort_keys=True)
+    print(json.dumps(manifest, indent=1))
+
+
+if __name__ == "__main__":
+    main()

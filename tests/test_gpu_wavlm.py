@@ -1,0 +1,120 @@
+"""GPU parity of the WavLM hot path (libsse.so HIP kernels) against the reference's own
+outputs (golden fixtures from REF/WavLM_embeddings.py:extract_wavlm_embeddings) and the
+numpy oracle.
+
+Tolerances (written here, stated in DESIGN.md):
+  fp32 path: max rel-L2 per pooled vector <= 1e-4 (north star), per hidden state <= 1e-4.
+  bf16 path: max rel-L2 per pooled vector <= 3e-2 and min cosine >= 0.999.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+FP32_TOL = 1e-4
+BF16_TOL = 3e-2
+BF16_COS = 0.999
+
+
+def _rel(a, b):
+    return np.linalg.norm(a - b, axis=-1) / np.linalg.norm(b, axis=-1)
+
+
+def _cos(a, b):
+    return (a * b).sum(-1) / (np.linalg.norm(a, axis=-1) * np.linalg.norm(b, axis=-1))
+
+
+@pytest.fixture(scope="module")
+def m32(wavlm_sd):
+    from ssr_amd import config as C
+    from ssr_amd.model import SSEModel
+    return SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype="fp32")
+
+
+@pytest.fixture(scope="module")
+def m16(wavlm_sd):
+    from ssr_amd import config as C
+    from ssr_amd.model import SSEModel
+    return SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype="bf16")
+
+
+def test_fp32_embed_matches_reference(m32, wavlm_clips, golden_wavlm):
+    idx = [int(i) for i in golden_wavlm["layer_indices"]]
+    got = m32.embed(torch.from_numpy(wavlm_clips).cuda(), idx).cpu().numpy()
+    ref = golden_wavlm["emb_norm0"]
+    rel = _rel(got, ref)
+    print("fp32 max rel-L2", rel.max())
+    assert rel.max() <= FP32_TOL
+
+
+def test_bf16_embed_matches_reference(m16, wavlm_clips, golden_wavlm):
+    idx = [int(i) for i in golden_wavlm["layer_indices"]]
+    got = m16.embed(torch.from_numpy(wavlm_clips).cuda(), idx).cpu().numpy()
+    ref = golden_wavlm["emb_norm0"]
+    rel, cos = _rel(got, ref), _cos(got, ref)
+    print("bf16 max rel-L2", rel.max(), "min cos", cos.min())
+    assert rel.max() <= BF16_TOL and cos.min() >= BF16_COS
+
+
+def test_fp32_all_hidden_states(m32, wavlm_clips, golden_wavlm):
+    hs = m32.hidden_states(torch.from_numpy(wavlm_clips[:2]).cuda())
+    assert len(hs) == 13
+    pooled = torch.stack([h.mean(dim=1) for h in hs], dim=1).cpu().numpy()   # [2, 13, 768]
+    rel = _rel(pooled, golden_wavlm["emb_all_layers"])
+    assert rel.max() <= FP32_TOL, rel.max()
+    h0 = hs[0][0].cpu().numpy()
+    assert np.linalg.norm(h0 - golden_wavlm["hs0_clip0"]) / np.linalg.norm(golden_wavlm["hs0_clip0"]) <= FP32_TOL
+    h1 = hs[1][0].cpu().numpy()
+    assert np.linalg.norm(h1 - golden_wavlm["hs1_clip0"]) / np.linalg.norm(golden_wavlm["hs1_clip0"]) <= FP32_TOL
+
+
+def test_fp32_do_normalize(wavlm_sd, wavlm_clips, golden_wavlm):
+    from ssr_amd import config as C
+    from ssr_amd.model import SSEModel
+    m = SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype="fp32", do_normalize=True)
+    idx = [int(i) for i in golden_wavlm["layer_indices"]]
+    got = m.embed(torch.from_numpy(wavlm_clips[:4]).cuda(), idx).cpu().numpy()
+    assert _rel(got, golden_wavlm["emb_norm1"]).max() <= FP32_TOL
+
+
+def test_batch_invariance_full_batch(m16, m32):
+    """Size-independent property at the bench shape (B=256): every clip's embedding in the
+    batch equals the embedding of that clip run alone, bit for bit (no cross-clip reduction)."""
+    from ssr_amd import synth
+    clips = torch.from_numpy(synth.synth_clips(256, 48000, seed=99)).cuda()
+    idx = [12, 11, 10, 6]
+    for m in (m16, m32):
+        full = m.embed(clips, idx)
+        for i in (0, 77, 255):
+            one = m.embed(clips[i:i + 1], idx)
+            assert torch.equal(full[i:i + 1], one), (m.dtype, i)
+        assert torch.isfinite(full).all()
+
+
+def test_oracle_subset_at_full_batch(m32):
+    """Full-size run, a subset of clips checked against the numpy oracle."""
+    from oracle.wavlm import WavLMOracle
+    from ssr_amd import config as C, synth
+    sd = synth.synth_wavlm_state_dict(C.WAVLM_BASE, seed=7)
+    clips = synth.synth_clips(256, 48000, seed=5)
+    idx = [12, 11, 10, 6]
+    got = m32.embed(torch.from_numpy(clips).cuda(), idx).cpu().numpy()
+    o = WavLMOracle(C.WAVLM_BASE, sd)
+    sel = [3, 128, 250]
+    ref = o.embed(clips[sel], idx)
+    assert _rel(got[sel], ref).max() <= FP32_TOL
+
+
+def test_edge_lengths(m32, wavlm_sd):
+    """Ragged clip lengths: shortest valid clip (T=1 frame), odd lengths, 10 s clip."""
+    from oracle.wavlm import WavLMOracle
+    from ssr_amd import config as C, synth
+    o = WavLMOracle(C.WAVLM_BASE, wavlm_sd)
+    for L in (400, 12345, 160000):
+        clip = synth.synth_clips(1, L, seed=L)
+        got = m32.embed(torch.from_numpy(clip).cuda(), [12, 6, 0]).cpu().numpy()
+        ref = o.embed(clip, [12, 6, 0])
+        assert _rel(got, ref).max() <= FP32_TOL, L
+    with pytest.raises(Exception):
+        m32.embed(torch.zeros((1, 399), device="cuda:0"), [12])    # shorter than the receptive field

@@ -1,0 +1,77 @@
+"""CPU-side checks of the C-ABI library: it loads, exports every symbol include/sse.h
+declares, and its host-only helpers agree with the reference-side math (no GPU calls)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+
+def _header_symbols():
+    txt = open(os.path.join(ROOT, "include", "sse.h")).read()
+    return sorted(set(re.findall(r"\b(sse_[a-z_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    from ssr_amd import _lib
+    L = _lib.lib()
+    syms = _header_symbols()
+    assert len(syms) >= 15
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+    assert set(_lib.EXPORTED) <= set(syms)
+    assert L.sse_version().decode().startswith("sse ")
+
+
+def test_weight_floats_match_param_specs():
+    from ssr_amd import _lib, config as C
+    L = _lib.lib()
+    for spec in (C.WAVLM_BASE, C.WAVLM_LARGE, C.WHISPER_TINY, C.WHISPER_LARGE_V2):
+        cfg = _lib.make_cfg(spec)
+        assert L.sse_weight_floats(ctypes.byref(cfg)) == C.weight_floats(spec), spec.name
+
+
+def test_invalid_config_rejected():
+    from ssr_amd import _lib, config as C
+    L = _lib.lib()
+    cfg = _lib.make_cfg(C.WAVLM_BASE)
+    cfg.heads = 7                                   # head_dim != 64
+    assert L.sse_weight_floats(ctypes.byref(cfg)) == 0
+    h = ctypes.c_void_p()
+    blob = np.zeros(10, np.float32)
+    assert L.sse_model_create(ctypes.byref(cfg), blob.ctypes.data, blob.nbytes, 0, 0, ctypes.byref(h)) == -1
+    cfg = _lib.make_cfg(C.WAVLM_BASE)
+    assert L.sse_model_create(ctypes.byref(cfg), blob.ctypes.data, blob.nbytes, 0, 0, ctypes.byref(h)) == -5
+    assert L.sse_strerror(-5).decode().startswith("weight blob")
+
+
+def test_rel_bucket_table_matches_torch():
+    """The C++ bucket (used to build the device bias table) equals HF's float32 torch path
+    for every distance the table covers (|d| <= 4095)."""
+    import torch
+    from ssr_amd import _lib
+    from transformers.models.wavlm.modeling_wavlm import WavLMAttention
+    L = _lib.lib()
+    d = torch.arange(-4095, 4096)[None, :]
+    ref = WavLMAttention(768, 12)._relative_positions_bucket(d)[0].numpy()
+    ours = np.array([L.sse_rel_bucket(int(x), 320, 800) for x in range(-4095, 4096)])
+    assert np.array_equal(ours, ref)
+
+
+def test_mel_filters_match_hf():
+    from ssr_amd import _lib
+    from transformers.audio_utils import mel_filter_bank
+    fb = np.zeros((201, 80), np.float32)
+    assert _lib.lib().sse_mel_filters(80, fb.ctypes.data) == 0
+    hf = mel_filter_bank(201, 80, 0.0, 8000.0, 16000, norm="slaney", mel_scale="slaney").astype(np.float32)
+    assert np.allclose(fb, hf, rtol=0, atol=1e-12)
+
+
+def test_ssemodel_refuses_cpu_device(wavlm_sd):
+    from ssr_amd import config as C
+    from ssr_amd.model import SSEModel
+    with pytest.raises(ValueError):
+        SSEModel(C.WAVLM_BASE, wavlm_sd, device="cpu")

@@ -1,0 +1,89 @@
+"""Pins the oracle (oracle/*.py) to the reference: fixtures in tests/golden/ were produced by
+running REF/WavLM_embeddings.py:extract_wavlm_embeddings and
+REF/whisper_embeddings_large.py:extract_whisper_embeddings_fixed themselves
+(tests/golden/make_golden.py).  Inputs are regenerated from seeds and checked by SHA-256."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+ORACLE_TOL = 1e-5     # fp32 restatement vs fp32 reference (observed ~1e-6)
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def _rel(a, b):
+    return np.linalg.norm(a - b, axis=-1) / np.linalg.norm(b, axis=-1)
+
+
+def test_inputs_match_manifest(wavlm_clips, wavlm_sd, golden_manifest):
+    m = golden_manifest["wavlm_base"]
+    assert _sha(wavlm_clips) == m["clips_sha256"]
+    h = hashlib.sha256()
+    for k in sorted(wavlm_sd):
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(wavlm_sd[k]).tobytes())
+    assert h.hexdigest() == m["weights_sha256"]
+
+
+def test_wavlm_oracle_vs_reference(wavlm_clips, wavlm_sd, golden_wavlm):
+    from oracle.wavlm import WavLMOracle
+    from ssr_amd import config as C
+    o = WavLMOracle(C.WAVLM_BASE, wavlm_sd)
+    idx = [int(i) for i in golden_wavlm["layer_indices"]]
+    got = o.embed(wavlm_clips[:3], idx)
+    assert _rel(got, golden_wavlm["emb_norm0"][:3]).max() <= ORACLE_TOL
+    got1 = o.embed(wavlm_clips[:2], idx, do_normalize=True)
+    assert _rel(got1, golden_wavlm["emb_norm1"][:2]).max() <= ORACLE_TOL
+
+
+def test_wavlm_oracle_intermediates(wavlm_clips, wavlm_sd, golden_wavlm):
+    from oracle.wavlm import WavLMOracle
+    from ssr_amd import config as C
+    o = WavLMOracle(C.WAVLM_BASE, wavlm_sd)
+    fe = o.feature_encoder(wavlm_clips[0])
+    ref = golden_wavlm["frontend_clip0"]
+    assert np.linalg.norm(fe - ref) / np.linalg.norm(ref) <= ORACLE_TOL
+    hs = o.hidden_states(wavlm_clips[0])
+    for k, i in (("hs0_clip0", 0), ("hs1_clip0", 1)):
+        assert np.linalg.norm(hs[i] - golden_wavlm[k]) / np.linalg.norm(golden_wavlm[k]) <= ORACLE_TOL
+    pooled = np.stack([h.mean(0) for h in hs])
+    assert _rel(pooled, golden_wavlm["emb_all_layers"][0]).max() <= ORACLE_TOL
+
+
+def test_whisper_oracle_vs_reference(golden_manifest):
+    from oracle.whisper import WhisperOracle, log_mel
+    from ssr_amd import config as C, synth
+    g = np.load(os.path.join(GOLDEN, "whisper_tiny.npz"))
+    man = golden_manifest["whisper_tiny"]
+    clips = [synth.synth_clips(1, int(16000 * d), seed=4321, first_clip=i)[0] for i, d in enumerate(man["durations_s"])]
+    assert [_sha(c) for c in clips] == man["clips_sha256"]
+    for i, c in enumerate(clips):
+        assert np.abs(log_mel(c) - g["mel"][i]).max() <= 2e-5
+    o = WhisperOracle(C.WHISPER_TINY, synth.synth_whisper_state_dict(C.WHISPER_TINY, seed=11))
+    got = np.concatenate([o.embed(c[None], [int(i) for i in g["layer_indices"]]) for c in clips])
+    assert _rel(got, g["emb"]).max() <= ORACLE_TOL
+
+
+def test_mel_filters_match_hf():
+    from oracle.whisper import mel_filters
+    from transformers.audio_utils import mel_filter_bank
+    hf = mel_filter_bank(201, 80, 0.0, 8000.0, 16000, norm="slaney", mel_scale="slaney")
+    assert np.abs(mel_filters(80) - hf).max() <= 1e-12
+
+
+def test_rel_buckets_match_hf():
+    import torch
+    from oracle.wavlm import rel_position_buckets
+    from transformers.models.wavlm.modeling_wavlm import WavLMAttention
+    att = WavLMAttention(768, 12)
+    T = 600
+    ctx = torch.arange(T)[:, None]
+    mem = torch.arange(T)[None, :]
+    ref = att._relative_positions_bucket(mem - ctx).numpy()
+    assert np.array_equal(rel_position_buckets(T, T), ref)
