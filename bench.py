@@ -100,10 +100,18 @@ def roofline(records, dtype):
     peak = PEAK_TFLOPS[dtype]
     breakdown = {k: {"ms": round(v[0], 3), "launches": v[3], "share": round(v[0] / total, 4),
                      "tflops": round(v[1] / max(v[0], 1e-9) / 1e9, 1)} for k, v in sorted(by_kernel.items())}
+    by_role = {}
+    for tag, ms, fl, by in records:
+        d = by_role.setdefault(tag, [0.0, 0.0, 0])
+        d[0] += ms
+        d[1] += fl
+        d[2] += 1
+    roles = {k: {"ms": round(v[0], 3), "launches": v[2], "tflops": round(v[1] / max(v[0], 1e-9) / 1e9, 1)}
+             for k, v in sorted(by_role.items())}
     return {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": None,
             "flop_per_launch": fl / n, "mean_launch_ms": round(ms / n, 4), "launches": n,
-            "device_ms_per_step_sum": None, "breakdown": breakdown}
+            "device_ms_per_step_sum": None, "breakdown": breakdown, "roles": roles}
 
 
 def main():

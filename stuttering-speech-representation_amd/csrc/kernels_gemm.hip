@@ -16,7 +16,7 @@
 
 namespace {
 
-template <typename T, int BM, int BN, int WAVES_M, int WAVES_N, int AMODE>
+template <typename T, int BM, int BN, int WAVES_M, int WAVES_N, int AMODE, int STAGES>
 __global__ __launch_bounds__(WAVES_M * WAVES_N * 64)
 void gemm_kernel(GemmArgs g) {
   constexpr int NW = WAVES_M * WAVES_N;
@@ -29,13 +29,24 @@ void gemm_kernel(GemmArgs g) {
   constexpr int A_INSTR = BM / 8, B_INSTR = BN / 8;            // 1-KiB glds pieces per tile
   constexpr int SA = (A_INSTR + NW - 1) / NW, SB = (B_INSTR + NW - 1) / NW;
   static_assert(WM % 16 == 0 && WN % 16 == 0, "wave tile");
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  // STAGES == 3: every wave issues the same number of pieces per tile, so one counted
+  // vmcnt retires exactly the oldest tile while the next one stays in flight.
+  static_assert(STAGES == 2 || (A_INSTR % NW == 0 && B_INSTR % NW == 0), "uniform pieces per wave");
+  constexpr int P = SA + SB;   // glds per wave per tile (STAGES == 3)
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   const int n_tiles_n = g.N / BN;
-  const int tile_n = blockIdx.x % n_tiles_n, tile_m = blockIdx.x / n_tiles_n;
+  // XCD-aware remap (bijective): blocks b, b+8, ... share an XCD, so give each XCD a
+  // contiguous run of tiles; the N-tiles of one M-tile then reuse the A panel in one L2.
+  int bid = blockIdx.x;
+  {
+    const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
+    bid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
+  }
+  const int tile_n = bid % n_tiles_n, tile_m = bid / n_tiles_n;
   const int grp = blockIdx.y;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int M = g.M, N = g.N, K = g.K;
@@ -118,11 +129,26 @@ void gemm_kernel(GemmArgs g) {
   const int q = lane >> 4, r16 = lane & 15;
   const int nk = (K + BK - 1) / BK;
   issue(0, 0);
+  if (STAGES == 3 && nk > 1) issue(1, 1);
+  int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
-    const char* As = smem + (kt & 1) * STAGE;
+    if constexpr (STAGES == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
+      cur = kt & 1;
+    } else {
+      // tile kt landed (tile kt+1 may stay in flight); no wave still reads buffer (kt+2)%3
+      if (kt + 1 < nk)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (kt + 2 < nk) issue(kt + 2, cur == 0 ? 2 : cur - 1);
+    }
+    const char* As = smem + cur * STAGE;
     const char* Bs = As + A_BYTES;
     if constexpr (sizeof(T) == 2) {
       #pragma unroll
@@ -177,6 +203,7 @@ void gemm_kernel(GemmArgs g) {
           for (int j = 0; j < TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][e], b1[j][e], acc[i][j], 0, 0, 0);
     }
+    if constexpr (STAGES == 3) cur = cur == 2 ? 0 : cur + 1;
   }
 
   // ---- epilogue: bias -> act -> +resid -> stores --------------------------------------
@@ -204,14 +231,14 @@ void gemm_kernel(GemmArgs g) {
   }
 }
 
-template <typename T, int BM, int BN, int WAVES_M, int WAVES_N>
+template <typename T, int BM, int BN, int WAVES_M, int WAVES_N, int STAGES>
 int launch_cfg(const GemmArgs& a, int amode, int groups, hipStream_t s) {
   dim3 grid((unsigned)(((a.M + BM - 1) / BM) * (a.N / BN)), (unsigned)groups);
   dim3 block(WAVES_M * WAVES_N * 64);
   if (amode == AMODE_SEG)
-    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WAVES_M, WAVES_N, AMODE_SEG>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WAVES_M, WAVES_N, AMODE_SEG, STAGES>), grid, block, 0, s, a);
   else
-    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WAVES_M, WAVES_N, AMODE_CONV>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WAVES_M, WAVES_N, AMODE_CONV, STAGES>), grid, block, 0, s, a);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -220,9 +247,11 @@ int launch_any(const GemmArgs& a, int amode, int groups, hipStream_t s) {
   constexpr int E = 16 / (int)sizeof(T);
   if (a.M <= 0 || a.N <= 0 || a.K <= 0 || a.K % E) return -3;
   if (amode == AMODE_CONV && (a.cin % E)) return -3;
-  if (a.N % 128 == 0) return launch_cfg<T, 128, 128, 2, 2>(a, amode, groups, s);
-  if (a.N % 64 == 0) return launch_cfg<T, 128, 64, 4, 1>(a, amode, groups, s);
-  if (a.N % 48 == 0) return launch_cfg<T, 128, 48, 4, 1>(a, amode, groups, s);
+  // main config: 256x128 tile, 8 waves (4x2) of 64x64, 3-stage LDS ring (144 KiB, 1 block/CU)
+  if (a.N % 128 == 0 && a.M >= 2048) return launch_cfg<T, 256, 128, 4, 2, 3>(a, amode, groups, s);
+  if (a.N % 128 == 0) return launch_cfg<T, 128, 128, 2, 2, 2>(a, amode, groups, s);
+  if (a.N % 64 == 0) return launch_cfg<T, 128, 64, 4, 1, 2>(a, amode, groups, s);
+  if (a.N % 48 == 0) return launch_cfg<T, 128, 48, 4, 1, 2>(a, amode, groups, s);
   return -3;
 }
 

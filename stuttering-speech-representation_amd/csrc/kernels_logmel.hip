@@ -74,7 +74,8 @@ __device__ __forceinline__ float unord_f32(unsigned u) {
   return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
 }
 
-constexpr int MEL_FR = 16;   // frames per block
+constexpr int MEL_FR = 20;   // frames per block (3000 = 150 x 20)
+static_assert(NFR % MEL_FR == 0, "mel grid must cover every frame");
 
 __global__ __launch_bounds__(256) void lm_mel_kernel(const float* __restrict__ S, const float* __restrict__ fb,
                                                      int n_mels, float* __restrict__ logv,

@@ -137,8 +137,8 @@ template int launch_conv0_gn<bf16>(const float*, int, int, const float*, const f
                                    hipStream_t);
 
 // ---------------------------------------------------------------------------------------
-// LayerNorm over rows of H (H % 256 == 0, H <= 2048).  One wave per row, 4 rows per block,
-// 4 consecutive elements per lane per step (16-B fp32 / 8-B bf16 accesses).
+// LayerNorm over rows of H (H % 4 == 0, H <= 2048).  One wave per row, 4 rows per block;
+// lane l handles 4-element groups l, l+64, ... (16-B fp32 / 8-B bf16 accesses).
 template <typename TI> SSE_DEV f32x4 load4(const TI* p);
 template <> SSE_DEV f32x4 load4<float>(const float* p) { return *(const f32x4*)p; }
 template <> SSE_DEV f32x4 load4<bf16>(const bf16* p) {
@@ -154,21 +154,23 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TI* __restrict__ i
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int lane = threadIdx.x & 63;
-  const int nv = H >> 8;
+  const int n4 = H >> 2;
   const TI* x = in + (long long)row * H;
   f32x4 v[8];
   float s = 0.f;
   #pragma unroll
-  for (int i = 0; i < 8; ++i)
-    if (i < nv) {
-      v[i] = load4<TI>(x + i * 256 + lane * 4);
+  for (int i = 0; i < 8; ++i) {
+    const int g = lane + 64 * i;
+    if (g < n4) {
+      v[i] = load4<TI>(x + 4 * g);
       s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
     }
+  }
   const float mean = wave_sum(s) / H;
   float q = 0.f;
   #pragma unroll
   for (int i = 0; i < 8; ++i)
-    if (i < nv)
+    if (lane + 64 * i < n4)
       #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float d = v[i][e] - mean;
@@ -176,9 +178,10 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TI* __restrict__ i
       }
   const float rstd = 1.0f / sqrtf(wave_sum(q) / H + eps);
   #pragma unroll
-  for (int i = 0; i < 8; ++i)
-    if (i < nv) {
-      const int c = i * 256 + lane * 4;
+  for (int i = 0; i < 8; ++i) {
+    const int g = lane + 64 * i;
+    if (g < n4) {
+      const int c = 4 * g;
       const f32x4 wv = *(const f32x4*)(w + c), bv = *(const f32x4*)(bta + c);
       f32x4 o;
       #pragma unroll
@@ -197,12 +200,13 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TI* __restrict__ i
         }
       }
     }
+  }
 }
 
 template <typename TI, typename TO>
 int launch_layernorm(const TI* in, const float* w, const float* b, int rows, int H, float eps, int act,
                      float* out_f, TO* out_t, hipStream_t s) {
-  if (H % 256 || H > 2048) return -3;
+  if (H % 4 || H > 2048) return -3;
   hipLaunchKernelGGL((layernorm_kernel<TI, TO>), dim3((rows + 3) / 4), dim3(256), 0, s, in, w, b, rows, H, eps,
                      act, out_f, out_t);
   return hipGetLastError() == hipSuccess ? 0 : -2;

@@ -338,6 +338,7 @@ inline double gflops(const GemmArgs& g, int groups = 1) { return 2.0 * g.M * (do
 int wavlm_frames(const sse_cfg& c, int L, int* Ts) {
   int t = L;
   for (int i = 0; i < c.n_conv; ++i) {
+    if (t < c.conv_kernel[i]) return 0;       // shorter than the receptive field
     t = (t - c.conv_kernel[i]) / c.conv_stride[i] + 1;
     if (Ts) Ts[i] = t;
     if (t <= 0) return 0;

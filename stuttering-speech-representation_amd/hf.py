@@ -1,0 +1,191 @@
+"""HF-duck-typed objects over the HIP path (the reference's operator API).
+
+The reference's glue only touches a narrow surface of the HF objects it is handed:
+  model(input_values, output_hidden_states=True, return_dict=True).hidden_states / .last_hidden_state
+                                               REF/WavLM_embeddings.py:76, 257, 302-310
+  model.config.hidden_size, next(model.parameters()).device     REF/WavLM_embeddings.py:66, 83
+  model.encoder(input_features, output_hidden_states=True, return_dict=True)
+                                               REF/whisper_embeddings_large.py:64, 250-254
+  feature_extractor(audio, sampling_rate=16000, return_tensors="pt").to(device).input_values
+                                               REF/WavLM_embeddings.py:289-293
+  processor(audio, sampling_rate=16000, return_tensors="pt").input_features
+                                               REF/whisper_embeddings_large.py:242-246
+These classes provide exactly that surface, so the reference's own functions (and
+model_training_*.py) run unchanged on them, with every tensor op in libsse.so on the GPU.
+The decoder half of WhisperModel (REF/whisper_embeddings_large.py:257-262) is SURVEY §8(f)
+next-1 and raises NotImplementedError here.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from types import SimpleNamespace
+
+import numpy as np
+import torch
+
+from . import config as C
+from .model import SSEModel, logmel, normalize
+
+
+@dataclass
+class BaseModelOutput:
+    last_hidden_state: torch.Tensor
+    hidden_states: tuple | None = None
+    attentions: tuple | None = None
+
+    def __getitem__(self, i):
+        return (self.last_hidden_state, self.hidden_states)[i]
+
+
+class BatchFeature(dict):
+    """Minimal transformers.BatchFeature: attribute access + .to(device)."""
+
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:
+            raise AttributeError(k) from e
+
+    def to(self, device):
+        return BatchFeature({k: (v.to(device) if isinstance(v, torch.Tensor) else v) for k, v in self.items()})
+
+
+def _to_batch(raw, device) -> torch.Tensor:
+    if isinstance(raw, (list, tuple)) and raw and not np.isscalar(raw[0]):
+        arrs = [np.asarray(r, dtype=np.float32) for r in raw]
+        if len({a.shape[-1] for a in arrs}) != 1:
+            raise ValueError("ragged batches are not supported: pass one clip or equal lengths")
+        raw = np.stack(arrs)
+    if isinstance(raw, torch.Tensor):
+        t = raw.to(torch.float32)
+    else:
+        t = torch.from_numpy(np.ascontiguousarray(np.asarray(raw, dtype=np.float32)))
+    if t.dim() == 1:
+        t = t[None]
+    return t.to(device)
+
+
+class Wav2Vec2FeatureExtractor:
+    """Wav2Vec2FeatureExtractor twin (HF feature_extraction_wav2vec2.py:99-236): float32 cast,
+    optional zero-mean/unit-variance normalisation on the GPU (sse_normalize)."""
+
+    def __init__(self, do_normalize: bool = False, sampling_rate: int = 16000, device="cuda:0", **_):
+        self.do_normalize = do_normalize
+        self.sampling_rate = sampling_rate
+        self.device = torch.device(device)
+
+    def __call__(self, raw_speech, sampling_rate=None, return_tensors="pt", **_):
+        if sampling_rate is not None and sampling_rate != self.sampling_rate:
+            raise ValueError(f"expected sampling_rate={self.sampling_rate}, got {sampling_rate}")
+        x = _to_batch(raw_speech, self.device)
+        if self.do_normalize:
+            x = normalize(x)
+        return BatchFeature(input_values=x)
+
+
+class WhisperFeatureExtractor:
+    """WhisperFeatureExtractor / WhisperProcessor twin: pad/truncate to 30 s and log-mel on the
+    GPU (sse_logmel, HF feature_extraction_whisper.py:135-168, 300-307)."""
+
+    def __init__(self, feature_size: int = 80, sampling_rate: int = 16000, device="cuda:0", **_):
+        self.feature_size = feature_size
+        self.sampling_rate = sampling_rate
+        self.device = torch.device(device)
+
+    def __call__(self, raw_speech, sampling_rate=None, return_tensors="pt", **_):
+        if sampling_rate is not None and sampling_rate != self.sampling_rate:
+            raise ValueError(f"expected sampling_rate={self.sampling_rate}, got {sampling_rate}")
+        return BatchFeature(input_features=logmel(_to_batch(raw_speech, self.device), self.feature_size))
+
+
+WhisperProcessor = WhisperFeatureExtractor
+
+
+class _DuckModel:
+    def __init__(self, sse: SSEModel):
+        self.sse = sse
+        self.config = SimpleNamespace(hidden_size=sse.spec.hidden, d_model=sse.spec.hidden,
+                                      num_hidden_layers=sse.spec.layers, model_type=sse.spec.name)
+        self._p = torch.zeros(1, device=sse.device)
+
+    def parameters(self):
+        yield self._p
+
+    @property
+    def device(self):
+        return self.sse.device
+
+    def to(self, device):
+        if torch.device(device) != self.sse.device and not (torch.device(device).type == "cuda"
+                                                             and torch.device(device).index is None):
+            raise ValueError(f"model lives on {self.sse.device}; build a new one for {device}")
+        return self
+
+    def eval(self):
+        return self
+
+    def embed(self, wave, layer_indices):
+        return self.sse.embed(wave, layer_indices)
+
+
+class WavLMModel(_DuckModel):
+    """WavLMModel twin.  ``WavLMModel.from_hf(hf_model)`` takes the weights of a real
+    transformers WavLMModel (e.g. a hub checkpoint loaded elsewhere)."""
+
+    @classmethod
+    def from_state_dict(cls, spec, state_dict, device="cuda:0", dtype="fp32"):
+        return cls(SSEModel(spec, state_dict, device=device, dtype=dtype))
+
+    @classmethod
+    def from_hf(cls, hf_model, device="cuda:0", dtype="fp32"):
+        c = hf_model.config
+        spec = C.WavLMSpec(hidden=c.hidden_size, layers=c.num_hidden_layers, heads=c.num_attention_heads,
+                           ffn=c.intermediate_size, conv_dim=tuple(c.conv_dim), conv_kernel=tuple(c.conv_kernel),
+                           conv_stride=tuple(c.conv_stride), conv_bias=bool(c.conv_bias),
+                           feat_norm_layer=c.feat_extract_norm == "layer",
+                           stable_layer_norm=bool(c.do_stable_layer_norm), pos_kernel=c.num_conv_pos_embeddings,
+                           pos_groups=c.num_conv_pos_embedding_groups, num_buckets=c.num_buckets,
+                           max_distance=c.max_bucket_distance, ln_eps=c.layer_norm_eps)
+        return cls.from_state_dict(spec, hf_model.state_dict(), device, dtype)
+
+    def __call__(self, input_values, attention_mask=None, output_hidden_states=None, return_dict=True, **_):
+        if attention_mask is not None:
+            raise NotImplementedError("padded batches (attention_mask) are not supported")
+        hs = self.sse.hidden_states(_to_batch(input_values, self.sse.device))
+        return BaseModelOutput(last_hidden_state=hs[-1], hidden_states=hs if output_hidden_states else None)
+
+    forward = __call__
+
+
+class _WhisperEncoder:
+    def __init__(self, sse: SSEModel):
+        self.sse = sse
+
+    def __call__(self, input_features, attention_mask=None, output_hidden_states=None, return_dict=True, **_):
+        hs = self.sse.hidden_states_from_mel(input_features.to(self.sse.device))
+        return BaseModelOutput(last_hidden_state=hs[-1], hidden_states=hs if output_hidden_states else None)
+
+
+class _WhisperDecoder:
+    def __call__(self, *a, **k):
+        raise NotImplementedError("the 1-token Whisper decoder pass is SURVEY §8(f) next-1 (not built yet)")
+
+
+class WhisperModel(_DuckModel):
+    """WhisperModel twin: ``.encoder`` runs on the HIP path; ``.decoder`` is not built yet."""
+
+    def __init__(self, sse: SSEModel):
+        super().__init__(sse)
+        self.encoder = _WhisperEncoder(sse)
+        self.decoder = _WhisperDecoder()
+
+    @classmethod
+    def from_state_dict(cls, spec, state_dict, device="cuda:0", dtype="fp32"):
+        return cls(SSEModel(spec, state_dict, device=device, dtype=dtype))
+
+    @classmethod
+    def from_hf(cls, hf_model, device="cuda:0", dtype="fp32"):
+        c = hf_model.config
+        spec = C.WhisperSpec(d_model=c.d_model, layers=c.encoder_layers, heads=c.encoder_attention_heads,
+                             ffn=c.encoder_ffn_dim, n_mels=c.num_mel_bins, max_positions=c.max_source_positions)
+        return cls.from_state_dict(spec, hf_model.state_dict(), device, dtype)

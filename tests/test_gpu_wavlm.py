@@ -117,4 +117,4 @@ def test_edge_lengths(m32, wavlm_sd):
         ref = o.embed(clip, [12, 6, 0])
         assert _rel(got, ref).max() <= FP32_TOL, L
     with pytest.raises(Exception):
-        m32.embed(torch.zeros((1, 399), device="cuda:0"), [12])    # shorter than the receptive field
+        m32.embed(torch.zeros((1, 399), device="cuda:0"), [12])    # shorter than the receptive field (T = 0)
