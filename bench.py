@@ -101,10 +101,10 @@ def roofline(records, dtype):
     breakdown = {k: {"ms": round(v[0], 3), "launches": v[3], "share": round(v[0] / total, 4),
                      "tflops": round(v[1] / max(v[0], 1e-9) / 1e9, 1)} for k, v in sorted(by_kernel.items())}
     by_role = {}
-    for tag, ms, fl, by in records:
+    for tag, t_ms, t_fl, _ in records:
         d = by_role.setdefault(tag, [0.0, 0.0, 0])
-        d[0] += ms
-        d[1] += fl
+        d[0] += t_ms
+        d[1] += t_fl
         d[2] += 1
     roles = {k: {"ms": round(v[0], 3), "launches": v[2], "tflops": round(v[1] / max(v[0], 1e-9) / 1e9, 1)}
              for k, v in sorted(by_role.items())}

@@ -12,6 +12,8 @@
 // Math: v_mfma_f32_16x16x32_bf16 (bf16 path) or v_mfma_f32_16x16x4_f32 (exact-f32 path);
 // both read the same LDS image: lane group q = lane>>4 consumes 16-B chunks q and q+4.
 // Epilogue fuses bias, erf-GELU, fp32 residual add and dual fp32/bf16 stores.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -33,7 +35,9 @@ void gemm_kernel(GemmArgs g) {
   // vmcnt retires exactly the oldest tile while the next one stays in flight.
   static_assert(STAGES == 2 || (A_INSTR % NW == 0 && B_INSTR % NW == 0), "uniform pieces per wave");
   constexpr int P = SA + SB;   // glds per wave per tile (STAGES == 3)
-  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE];
+  constexpr int CLD = BN + 4;                 // epilogue: padded fp32 C row (conflict-free b32 writes)
+  constexpr int SMEM = STAGES * STAGE > BM * CLD * 4 ? STAGES * STAGE : BM * CLD * 4;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -206,25 +210,61 @@ void gemm_kernel(GemmArgs g) {
     if constexpr (STAGES == 3) cur = cur == 2 ? 0 : cur + 1;
   }
 
-  // ---- epilogue: bias -> act -> +resid -> stores --------------------------------------
-  const int col0 = grp * N;
+  // ---- epilogue: stage the fp32 tile through LDS, then one coalesced pass per 16-B chunk:
+  //      v = acc + bias (act) (+resid) -> fp32 and/or element-type stores -----------------
+  float* Cs = (float*)smem;
+  __syncthreads();                            // every wave is done reading the operand stages
   #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * WN + j * 16 + r16;
-    const float bv = g.bias ? g.bias[col0 + n] : 0.f;
+  for (int i = 0; i < TM; ++i)
     #pragma unroll
-    for (int i = 0; i < TM; ++i) {
+    for (int j = 0; j < TN; ++j)
       #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * WM + i * 16 + q * 4 + r;
-        if (m < M) {
-          float v = acc[i][j][r] + bv;
-          if (g.act == ACT_GELU) v = gelu_erf(v);
-          const long long o = (long long)m * g.ldc + col0 + n;
-          if (g.resid)
-            v += g.resid[g.resid_rows ? (long long)(m % g.resid_rows) * g.ldc + col0 + n : o];
-          if (g.Cf) g.Cf[o] = v;
-          if (g.Ct) ((T*)g.Ct)[o] = from_f32<T>(v);
+      for (int r = 0; r < 4; ++r)
+        Cs[(wm * WM + i * 16 + q * 4 + r) * CLD + wn * WN + j * 16 + r16] = acc[i][j][r];
+  __syncthreads();
+  constexpr int NT = NW * 64;
+  constexpr int CH = BM * BN / 4;             // 16-B chunks in the tile
+  constexpr int UNR = 4;
+  const int col0 = grp * N;
+  const bool has_bias = g.bias != nullptr, has_res = g.resid != nullptr, gelu = g.act == ACT_GELU;
+  for (int base = threadIdx.x; base < CH; base += NT * UNR) {
+    f32x4 v[UNR], rv[UNR], bv[UNR];
+    long long off[UNR];
+    bool ok[UNR];
+    #pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int c0 = base + u * NT;
+      const int c = c0 < CH ? c0 : CH - 1;
+      const int row = c / (BN / 4), cc = (c % (BN / 4)) * 4;
+      const int m = m0 + row, n = n0 + cc;
+      ok[u] = m < M && c0 < CH;
+      off[u] = (long long)(ok[u] ? m : 0) * g.ldc + col0 + n;
+      v[u] = *(const f32x4*)(Cs + row * CLD + cc);
+      bv[u] = has_bias ? *(const f32x4*)(g.bias + col0 + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+      rv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (has_res) {
+        const long long ro = g.resid_rows ? (long long)((ok[u] ? m : 0) % g.resid_rows) * g.ldc + col0 + n : off[u];
+        rv[u] = *(const f32x4*)(g.resid + ro);
+      }
+    }
+    #pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      f32x4 o;
+      #pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x = v[u][e] + bv[u][e];
+        if (gelu) x = gelu_erf(x);
+        o[e] = x + rv[u][e];
+      }
+      if (ok[u]) {
+        if (g.Cf) *(f32x4*)(g.Cf + off[u]) = o;
+        if (g.Ct) {
+          if constexpr (sizeof(T) == 2) {
+            bf16x4 ob = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+            *(bf16x4*)((T*)g.Ct + off[u]) = ob;
+          } else {
+            *(f32x4*)((T*)g.Ct + off[u]) = o;
+          }
         }
       }
     }
@@ -247,8 +287,11 @@ int launch_any(const GemmArgs& a, int amode, int groups, hipStream_t s) {
   constexpr int E = 16 / (int)sizeof(T);
   if (a.M <= 0 || a.N <= 0 || a.K <= 0 || a.K % E) return -3;
   if (amode == AMODE_CONV && (a.cin % E)) return -3;
-  // main config: 256x128 tile, 8 waves (4x2) of 64x64, 3-stage LDS ring (144 KiB, 1 block/CU)
-  if (a.N % 128 == 0 && a.M >= 2048) return launch_cfg<T, 256, 128, 4, 2, 3>(a, amode, groups, s);
+  // default: 128x128 tile, 4 waves of 64x64, 2-stage LDS (2 blocks/CU overlap one block's
+  // epilogue with the other's MFMA loop: measured 656 vs 637 TF/s on the WavLM-base step).
+  // SSE_GEMM_CFG=2 selects the 256x128, 8-wave, 3-stage ring (144 KiB, 1 block/CU) for A/B runs.
+  static const int force = [] { const char* e = getenv("SSE_GEMM_CFG"); return e ? atoi(e) : 0; }();
+  if (a.N % 128 == 0 && a.M >= 2048 && force == 2) return launch_cfg<T, 256, 128, 4, 2, 3>(a, amode, groups, s);
   if (a.N % 128 == 0) return launch_cfg<T, 128, 128, 2, 2, 2>(a, amode, groups, s);
   if (a.N % 64 == 0) return launch_cfg<T, 128, 64, 4, 1, 2>(a, amode, groups, s);
   if (a.N % 48 == 0) return launch_cfg<T, 128, 48, 4, 1, 2>(a, amode, groups, s);
