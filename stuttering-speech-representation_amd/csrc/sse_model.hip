@@ -107,6 +107,7 @@ struct sse_model {
   size_t fp_ln_w, fp_ln_b, fp_w, fp_b, pos_w, pos_b, enc_ln_w, enc_ln_b, relb, zero;
   // Whisper
   size_t c1_w, c1_b, c2_w, c2_b, positions;
+  int ldq = 0;   // QKV GEMM width: 3H (+ 8*heads gate columns for WavLM), padded to 128
   std::vector<LayerW> layers;
   // live per-launch timing (sse_profile_*): events pre-created outside any capture
   struct Prof {
@@ -216,15 +217,25 @@ int build_wavlm(sse_model* m, Blob& bl, Arena& ar) {
     if (!bl.ok) return SSE_ERR_WEIGHTS;
     if (!qw) continue;
     LayerW L{};
-    std::vector<float> qkv((size_t)3 * H * H), qkvb((size_t)3 * H);
+    // rows [q | k | v | gate: head h, output o at 3H + 8h + o, block-diagonal over the
+    // head's 64 input channels (gru_rel_pos_linear, HF :158-163) | zero pad to ldq]
+    const int ldq = ((3 * H + 8 * nh + 127) / 128) * 128;
+    m->ldq = ldq;
+    std::vector<float> qkv((size_t)ldq * H, 0.f), qkvb((size_t)ldq, 0.f);
     std::memcpy(qkv.data(), qw, (size_t)H * H * 4);
     std::memcpy(qkv.data() + (size_t)H * H, kw, (size_t)H * H * 4);
     std::memcpy(qkv.data() + (size_t)2 * H * H, vw, (size_t)H * H * 4);
     std::memcpy(qkvb.data(), qb, H * 4);
     std::memcpy(qkvb.data() + H, kb, H * 4);
     std::memcpy(qkvb.data() + 2 * H, vb, H * 4);
+    for (int hh = 0; hh < nh; ++hh)
+      for (int o = 0; o < 8; ++o) {
+        const size_t row = (size_t)3 * H + 8 * hh + o;
+        for (int d = 0; d < 64; ++d) qkv[row * H + hh * 64 + d] = gw[o * 64 + d];
+        qkvb[row] = gbb[o];
+      }
     L.qkv_w = ar.put_elem(qkv, BF);
-    L.qkv_b = ar.put_f32(qkvb.data(), 3 * H);
+    L.qkv_b = ar.put_f32(qkvb.data(), ldq);
     L.o_w = ar.put_elem(std::vector<float>(ow, ow + (size_t)H * H), BF);
     L.o_b = ar.put_f32(ob, H);
     L.g_const = ar.put_f32(gc, nh);
@@ -283,6 +294,7 @@ int build_whisper(sse_model* m, Blob& bl, Arena& ar) {
     std::memcpy(qkvb.data() + 2 * D, vb, D * 4);                           // k_proj has no bias
     L.qkv_w = ar.put_elem(qkv, BF);
     L.qkv_b = ar.put_f32(qkvb.data(), 3 * D);
+    m->ldq = 3 * D;
     L.o_w = ar.put_elem(std::vector<float>(ow, ow + (size_t)D * D), BF);
     L.o_b = ar.put_f32(ob, D);
     L.ln1_w = ar.put_f32(l1w, D);
@@ -365,7 +377,7 @@ WavlmWs wavlm_plan(const sse_model* m, int B, int L, Plan& p) {
   WavlmWs w;
   w.zero = p.add(256);
   w.norm = p.add((size_t)B * 8);
-  w.part = p.add((size_t)B * conv0_chunks(Ts[0]) * C0 * 16);
+  w.part = p.add(conv0_moments_bytes(B));
   w.ss = p.add((size_t)B * C0 * 8);
   w.bufA = p.add(maxA);
   w.bufB = p.add(maxB);
@@ -373,7 +385,7 @@ WavlmWs wavlm_plan(const sse_model* m, int B, int L, Plan& p) {
   w.x = p.add(M * H * 4);
   w.xt = p.add(M * H * es);
   w.xb = p.add(M * (H > c.conv_dim[c.n_conv - 1] ? H : c.conv_dim[c.n_conv - 1]) * es);
-  w.qkv = p.add(M * 3 * H * es);
+  w.qkv = p.add(M * (size_t)(((3 * H + 8 * c.heads + 127) / 128) * 128) * es);
   w.ctx = p.add(M * H * es);
   w.ff = p.add(M * (size_t)c.ffn * es);
   w.hf = c.stable_layer_norm ? p.add(M * H * 4) : 0;
@@ -453,7 +465,7 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
   RC(prof(m, s, "conv0_gn", 2.0 * B * (double)Ts[0] * C0 * c.conv_kernel[0], 0, [&] { return launch_conv0_gn<T>(wave, B, L, norm, m->ptr<float>(m->conv_w[0]),
                         m->conv_b[0] ? m->ptr<float>(m->conv_b[0]) : nullptr, C0, c.conv_kernel[0],
                         c.conv_stride[0], Ts[0], m->ptr<float>(m->conv_ln_w[0]), m->ptr<float>(m->conv_ln_b[0]),
-                        1e-5f, (double2*)(ws + w.part), (float2*)(ws + w.ss), bufs[0], s); }));
+                        1e-5f, (double*)(ws + w.part), (float2*)(ws + w.ss), bufs[0], s); }));
   for (int i = 1; i < c.n_conv; ++i) {
     const int cin = c.conv_dim[i - 1], co = c.conv_dim[i], k = c.conv_kernel[i], st = c.conv_stride[i];
     GemmArgs g{};
@@ -499,19 +511,15 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
   float* hf = c.stable_layer_norm ? (float*)(ws + w.hf) : nullptr;
   for (int l = 0; l < c.layers; ++l) {
     const LayerW& Lw = m->layers[l];
-    const float* gate_in = x;
-    if (c.stable_layer_norm) {
-      RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, ACT_NONE, hf,
-                                     xb, s)));
-      gate_in = hf;
-    }
+    if (c.stable_layer_norm)
+      RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, ACT_NONE,
+                                     nullptr, xb, s)));
     GemmArgs g{};
-    g.A = xb; g.B = m->ptr(Lw.qkv_w); g.M = M; g.N = 3 * H; g.K = H;
-    g.rows_per_seg = M; g.lda = H; g.bias = m->ptr<float>(Lw.qkv_b); g.Ct = qkv; g.ldc = 3 * H; g.zero = zero;
+    g.A = xb; g.B = m->ptr(Lw.qkv_w); g.M = M; g.N = m->ldq; g.K = H;
+    g.rows_per_seg = M; g.lda = H; g.bias = m->ptr<float>(Lw.qkv_b); g.Ct = qkv; g.ldc = m->ldq; g.zero = zero;
     RC(prof(m, s, "gemm:qkv", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     AttnArgs a{};
-    a.qkv = qkv; a.out = ctx; a.T = Tf; a.H = H; a.nh = nh; a.scale = 0.125f;
-    a.gx = gate_in; a.gw = m->ptr<float>(Lw.g_w); a.gb = m->ptr<float>(Lw.g_b);
+    a.qkv = qkv; a.out = ctx; a.T = Tf; a.H = H; a.nh = nh; a.ldq = m->ldq; a.scale = 0.125f;
     a.gconst = m->ptr<float>(Lw.g_const); a.relb = m->ptr<float>(m->relb); a.maxd = MAXD;
     if (Tf > MAXD) return SSE_ERR_UNSUPPORTED;
     RC(prof(m, s, "attn", 4.0 * B * (double)Tf * Tf * H, 0, [&] { return launch_attention<T>(a, B, s); }));
@@ -594,7 +602,7 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
     g.bias = m->ptr<float>(Lw.qkv_b); g.Ct = qkv; g.ldc = 3 * D; g.zero = zero;
     RC(prof(m, s, "gemm:qkv", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     AttnArgs a{};
-    a.qkv = qkv; a.out = ctx; a.T = Tq; a.H = D; a.nh = nh; a.scale = 1.0f;
+    a.qkv = qkv; a.out = ctx; a.T = Tq; a.H = D; a.nh = nh; a.ldq = m->ldq; a.scale = 1.0f;
     RC(prof(m, s, "attn", 4.0 * B * (double)Tq * Tq * D, 0, [&] { return launch_attention<T>(a, B, s); }));
     g = GemmArgs{};
     g.A = ctx; g.B = m->ptr(Lw.o_w); g.M = M; g.N = D; g.K = D; g.rows_per_seg = M; g.lda = D;
