@@ -128,6 +128,12 @@ int sse_profile_start(sse_model* m, int max_launches);
 int sse_profile_read(sse_model* m, int cap, char* tags, float* ms, double* flops, double* bytes);
 int sse_profile_stop(sse_model* m);
 
+/* The MFMA GEMM the path is built on, exposed for kernel tests and microbenchmarks:
+ * C[M][N] = A[M][K] . B[N][K]^T (+bias[N]) (GELU if act == 1) (+resid[M][N] fp32), written to
+ * d_cf (fp32) and/or d_ct (bf16 or fp32 = dtype).  A, B in the dtype; d_zero >= 64 zero bytes. */
+int sse_gemm(int dtype, const void* d_a, const void* d_b, const float* d_bias, const float* d_resid, float* d_cf,
+             void* d_ct, int M, int N, int K, int act, const void* d_zero, void* stream);
+
 /* Host-only helpers (no device work; usable without a GPU). */
 const char* sse_strerror(int err);
 /* WavLM relative-position bucket of distance d = key - query (HF _relative_positions_bucket). */

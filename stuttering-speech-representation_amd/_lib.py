@@ -22,7 +22,7 @@ EXPORTED = ("sse_weight_floats", "sse_model_create", "sse_model_destroy", "sse_o
             "sse_workspace_bytes", "sse_logmel_workspace_bytes", "sse_logmel", "sse_embed",
             "sse_hidden_states", "sse_strerror", "sse_rel_bucket", "sse_mel_filters", "sse_version",
             "sse_normalize", "sse_normalize_workspace_bytes", "sse_whisper_hidden_states_from_mel",
-            "sse_profile_start", "sse_profile_read", "sse_profile_stop")
+            "sse_profile_start", "sse_profile_read", "sse_profile_stop", "sse_gemm")
 
 
 class SSEError(RuntimeError):
@@ -114,6 +114,8 @@ def lib() -> ctypes.CDLL:
     L.sse_profile_read.restype = i32
     L.sse_profile_stop.argtypes = [vp]
     L.sse_profile_stop.restype = i32
+    L.sse_gemm.argtypes = [i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, vp]
+    L.sse_gemm.restype = i32
     L.sse_strerror.argtypes = [i32]
     L.sse_strerror.restype = ctypes.c_char_p
     L.sse_rel_bucket.argtypes = [i32, i32, i32]

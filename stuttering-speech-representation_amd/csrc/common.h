@@ -14,7 +14,28 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 #define GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
 #define LPTR(p) ((__attribute__((address_space(3))) void*)(p))
 
-SSE_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// erf-GELU, branch-free: gelu(x) = x - x/2 erfc(x/sqrt2) (x >= 0), x/2 erfc(-x/sqrt2) (x < 0), with
+// erfc from the Chebyshev fit of Numerical Recipes (erfcc, relative error < 1.2e-7 over the
+// whole line).  fp32 evaluation: max |err| 2.4e-7, relative 2.4e-6 wherever |gelu| > 1e-6
+// (checked against scipy erf on 2.2M points); the negative tail keeps relative precision.
+// One v_rcp, one v_exp and ~14 FMA, no divergent branches (ocml erff branches on |x|).
+SSE_DEV float gelu_erf(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.0f));
+  float p = 0.17087277f;
+  p = fmaf(p, t, -0.82215223f);
+  p = fmaf(p, t, 1.48851587f);
+  p = fmaf(p, t, -1.13520398f);
+  p = fmaf(p, t, 0.27886807f);
+  p = fmaf(p, t, -0.18628806f);
+  p = fmaf(p, t, 0.09678418f);
+  p = fmaf(p, t, 0.37409196f);
+  p = fmaf(p, t, 1.00002368f);
+  p = fmaf(p, t, -1.26551223f);
+  const float erfc = t * __expf(fmaf(-z, z, p));
+  const float h = 0.5f * x * erfc;
+  return x >= 0.f ? x - h : h;
+}
 
 template <typename T> SSE_DEV T from_f32(float v);
 template <> SSE_DEV float from_f32<float>(float v) { return v; }

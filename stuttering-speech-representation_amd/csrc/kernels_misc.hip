@@ -558,9 +558,9 @@ __global__ __launch_bounds__(512) void attention_full_kernel(AttnArgs a) {
       if (kr < T) kv = *(const bf16x8*)(qkv + (long long)kr * H3 + H + h * AT_HD + ch * 8);
       *(bf16x8*)(Ks + kr * 128 + ((ch ^ ((kr >> 1) & 7)) * 16)) = kv;
     }
-    for (int i = tid; i < (TP / 4) * 8; i += nthr) {      // (4-key group, 8-dim chunk)
-      const int kg = i >> 3, ch = i & 7;
-      bf16x8 v4[4];
+    for (int i = tid; i < (TP / 4) * 8; i += nthr) {      // (8-dim chunk, 4-key group): key group
+      const int ch = i / (TP / 4), kg = i - ch * (TP / 4);  // fastest, so a wave's 8-B writes are
+      bf16x8 v4[4];                                         // contiguous (conflict-free)
       #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int key = kg * 4 + u;

@@ -840,6 +840,16 @@ int sse_profile_stop(sse_model* m) {
 
 size_t sse_normalize_workspace_bytes(int B) { return (size_t)B * 8; }
 
+int sse_gemm(int dtype, const void* d_a, const void* d_b, const float* d_bias, const float* d_resid, float* d_cf,
+             void* d_ct, int M, int N, int K, int act, const void* d_zero, void* stream) {
+  if (!d_a || !d_b || !d_zero || M <= 0 || N <= 0 || K <= 0 || (!d_cf && !d_ct)) return SSE_ERR_INVALID;
+  GemmArgs g{};
+  g.A = d_a; g.B = d_b; g.M = M; g.N = N; g.K = K; g.rows_per_seg = M; g.lda = K;
+  g.bias = d_bias; g.resid = d_resid; g.Cf = d_cf; g.Ct = d_ct; g.ldc = N; g.act = act; g.zero = d_zero;
+  return dtype == SSE_DTYPE_BF16 ? launch_gemm_bf16(g, AMODE_SEG, 1, (hipStream_t)stream)
+                                 : launch_gemm_f32(g, AMODE_SEG, 1, (hipStream_t)stream);
+}
+
 int sse_normalize(const float* d_in, int B, int L, float* d_out, void* d_ws, size_t ws_bytes, void* stream) {
   if (!d_in || !d_out || !d_ws || B <= 0 || L <= 0) return SSE_ERR_INVALID;
   if (ws_bytes < (size_t)B * 8) return SSE_ERR_WORKSPACE;

@@ -214,3 +214,32 @@ def normalize(wave: torch.Tensor) -> torch.Tensor:
                                         ctypes.c_void_p(torch.cuda.current_stream(wave.device).cuda_stream)),
                "sse_normalize")
     return out
+
+
+_ZERO = {}
+
+
+def gemm(a: torch.Tensor, b: torch.Tensor, bias=None, resid=None, act: str | None = None,
+         out_dtype=torch.float32) -> torch.Tensor:
+    """The path's MFMA GEMM on its own: a [M, K] @ b[N, K]^T (+bias) (gelu) (+resid).
+    a, b both bf16 (bf16 MFMA) or both fp32 (exact-f32 MFMA)."""
+    if a.dtype != b.dtype or a.dtype not in (torch.bfloat16, torch.float32):
+        raise TypeError("a and b must both be bf16 or both fp32")
+    M, K = a.shape
+    N = b.shape[0]
+    dev = a.device
+    z = _ZERO.get(dev)
+    if z is None:
+        z = _ZERO[dev] = torch.zeros(64, dtype=torch.float32, device=dev)
+    a, b = a.contiguous(), b.contiguous()
+    cf = torch.empty((M, N), dtype=torch.float32, device=dev) if out_dtype == torch.float32 else None
+    ct = torch.empty((M, N), dtype=a.dtype, device=dev) if out_dtype != torch.float32 else None
+    dt = _lib.SSE_DTYPE_BF16 if a.dtype == torch.bfloat16 else _lib.SSE_DTYPE_F32
+    bias_p = bias.contiguous().data_ptr() if bias is not None else None
+    res_p = resid.contiguous().data_ptr() if resid is not None else None
+    _lib.check(_lib.lib().sse_gemm(dt, a.data_ptr(), b.data_ptr(), bias_p, res_p,
+                                   cf.data_ptr() if cf is not None else None,
+                                   ct.data_ptr() if ct is not None else None, M, N, K, 1 if act == "gelu" else 0,
+                                   z.data_ptr(), ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
+               "sse_gemm")
+    return cf if cf is not None else ct

@@ -1,0 +1,30 @@
+#!/usr/bin/env python3
+"""Microbenchmark of the MFMA GEMM on the WavLM-base B=256 shapes (HIP-event timing)."""
+import importlib, os, sys, json
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+importlib.import_module("stuttering-speech-representation_amd")
+from ssr_amd.model import gemm
+
+SHAPES = {"qkv": (38144, 2432, 768, None), "oproj": (38144, 768, 768, "res"), "ffn1": (38144, 3072, 768, "gelu"),
+          "ffn2": (38144, 768, 3072, "res"), "proj": (38144, 768, 512, None), "sq4096": (4096, 4096, 4096, None)}
+res = {}
+for name, (M, N, K, epi) in SHAPES.items():
+    a = torch.randn(M, K, device="cuda").bfloat16()
+    b = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    bias = torch.randn(N, device="cuda")
+    resid = torch.randn(M, N, device="cuda") if epi == "res" else None
+    act = "gelu" if epi == "gelu" else None
+    outd = torch.float32 if epi == "res" else torch.bfloat16
+    for _ in range(3):
+        gemm(a, b, bias, resid, act, out_dtype=outd)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = 20
+    e0.record()
+    for _ in range(n):
+        gemm(a, b, bias, resid, act, out_dtype=outd)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / n
+    res[name] = {"ms": round(ms, 4), "tflops": round(2 * M * N * K / ms / 1e9, 1)}
+print(json.dumps(res))
