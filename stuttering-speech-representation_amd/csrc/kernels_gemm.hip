@@ -19,8 +19,7 @@
 namespace {
 
 template <typename T, int BM, int BN, int WAVES_M, int WAVES_N, int AMODE, int STAGES>
-__global__ __launch_bounds__(WAVES_M * WAVES_N * 64)
-void gemm_kernel(GemmArgs g) {
+__device__ __forceinline__ void gemm_body(const GemmArgs& g) {
   constexpr int NW = WAVES_M * WAVES_N;
   constexpr int E = 16 / (int)sizeof(T);   // elements per 16-B chunk
   constexpr int BK = 8 * E;                 // elements per 128-B row
@@ -55,71 +54,95 @@ void gemm_kernel(GemmArgs g) {
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int M = g.M, N = g.N, K = g.K;
 
-  // ---- per-lane source descriptors for the glds pieces this wave issues -------------
+  // ---- per-lane source descriptors for the LDS-DMA pieces this wave issues ------------
+  // SEG mode: one buffer descriptor per operand based at the block's first row; every lane's
+  // byte offset is fixed for the whole K loop and only the scalar soffset advances per K-step
+  // (no per-step VALU address math).  Chunks past K read as zero through an out-of-range
+  // offset (the descriptor's range check returns 0).  CONV mode keeps per-chunk addresses.
+  constexpr unsigned NREC = 0x7FFFFFF0u, OOB = 0x7FFFFFF0u;
+  __amdgpu_buffer_rsrc_t a_rsrc, b_rsrc;
+  unsigned a_voff[SA], b_voff[SB];
   const char* a_src[SA];
   int a_chunk[SA];
   int a_tb[SA], a_to[SA];     // CONV: seg*T_in, t_out*stride - pad
-  #pragma unroll
-  for (int s = 0; s < SA; ++s) {
-    const int piece = wave + NW * s;
-    const int row = piece * 8 + (lane >> 3);
-    const int ch = (lane & 7) ^ ((row >> 1) & 7);
-    int m = m0 + row;
-    m = m < M ? m : M - 1;
-    a_chunk[s] = ch;
-    const int seg = m / g.rows_per_seg, r = m - seg * g.rows_per_seg;
-    if (AMODE == AMODE_SEG) {
-      a_src[s] = (const char*)g.A + ((long long)seg * g.seg_stride + (long long)r * g.lda + ch * E) * sizeof(T);
-      a_tb[s] = 0; a_to[s] = 0;
-    } else {
+  {
+    const int mf = m0 < M ? m0 : M - 1;
+    const int seg0 = mf / g.rows_per_seg, r0 = mf - seg0 * g.rows_per_seg;
+    const long long a_base_el = (long long)seg0 * g.seg_stride + (long long)r0 * g.lda;
+    a_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)g.A + a_base_el * (long long)sizeof(T)), (short)0,
+                                               (int)NREC, 0x00020000);
+    const char* b_base = (const char*)g.B + ((long long)grp * N + n0) * K * (long long)sizeof(T);
+    b_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)b_base, (short)0, (int)NREC, 0x00020000);
+    #pragma unroll
+    for (int s = 0; s < SA; ++s) {
+      const int piece = wave + NW * s;
+      const int row = piece * 8 + (lane >> 3);
+      const int ch = (lane & 7) ^ ((row >> 1) & 7);
+      int m = m0 + row;
+      m = m < M ? m : M - 1;
+      a_chunk[s] = ch;
+      const int seg = m / g.rows_per_seg, r = m - seg * g.rows_per_seg;
+      const long long el = (long long)seg * g.seg_stride + (long long)r * g.lda + ch * E;
+      a_voff[s] = (unsigned)((el - a_base_el) * (long long)sizeof(T));
       a_src[s] = (const char*)g.A;
       a_tb[s] = seg * g.T_in;
       a_to[s] = r * g.stride - g.pad;
     }
+    #pragma unroll
+    for (int s = 0; s < SB; ++s) {
+      const int piece = wave + NW * s;
+      const int row = piece * 8 + (lane >> 3);
+      const int ch = (lane & 7) ^ ((row >> 1) & 7);
+      b_voff[s] = (unsigned)(((row < BN ? row : 0) * (long long)K + ch * E) * (long long)sizeof(T));
+    }
   }
-  const char* b_src[SB];
-  #pragma unroll
-  for (int s = 0; s < SB; ++s) {
-    const int piece = wave + NW * s;
-    const int row = piece * 8 + (lane >> 3);
-    const int ch = (lane & 7) ^ ((row >> 1) & 7);
-    const int n = n0 + (row < BN ? row : 0);
-    b_src[s] = (const char*)g.B + (((long long)grp * N + n) * K + ch * E) * sizeof(T);
-  }
-  const int b_kbase = 0;
-  (void)b_kbase;
 
   auto issue = [&](int kt, int buf) {
     char* st = smem + buf * STAGE;
     const int k0 = kt * BK;
+    const unsigned soff = (unsigned)k0 * (unsigned)sizeof(T);
+    if (AMODE == AMODE_SEG && k0 + BK <= K) {   // wave-uniform fast path: no per-lane work at all
+      #pragma unroll
+      for (int s = 0; s < SA; ++s) {
+        const int piece = wave + NW * s;
+        if (A_INSTR % NW == 0 || piece < A_INSTR)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, LPTR(st + piece * 1024), 16, a_voff[s], soff, 0, 0);
+      }
+      #pragma unroll
+      for (int s = 0; s < SB; ++s) {
+        const int piece = wave + NW * s;
+        if (B_INSTR % NW == 0 || piece < B_INSTR)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, LPTR(st + A_BYTES + piece * 1024), 16, b_voff[s], soff, 0, 0);
+      }
+      return;
+    }
     #pragma unroll
     for (int s = 0; s < SA; ++s) {
       const int piece = wave + NW * s;
-      if (piece < A_INSTR) {
-        const void* src;
-        const int k = k0 + a_chunk[s] * E;
+      if (A_INSTR % NW == 0 || piece < A_INSTR) {
         if (AMODE == AMODE_SEG) {
-          src = k < K ? (const void*)(a_src[s] + (long long)k0 * sizeof(T)) : g.zero;
+          const unsigned vo = k0 + a_chunk[s] * E < K ? a_voff[s] : OOB;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, LPTR(st + piece * 1024), 16, vo, soff, 0, 0);
         } else {
+          const int k = k0 + a_chunk[s] * E;
           const int j = k / g.cin, c = k - j * g.cin;
           const int t = a_to[s] + j;
-          src = (k < K && t >= 0 && t < g.T_in)
-                    ? (const void*)((const char*)g.A +
-                                    (((long long)(a_tb[s] + t)) * g.ld_in + grp * g.cin + c) * sizeof(T))
-                    : g.zero;
+          const void* src = (k < K && t >= 0 && t < g.T_in)
+                                ? (const void*)(a_src[s] + (((long long)(a_tb[s] + t)) * g.ld_in + grp * g.cin + c) *
+                                                               (long long)sizeof(T))
+                                : g.zero;
+          __builtin_amdgcn_global_load_lds(GPTR(src), LPTR(st + piece * 1024), 16, 0, 0);
         }
-        __builtin_amdgcn_global_load_lds(GPTR(src), LPTR(st + piece * 1024), 16, 0, 0);
       }
     }
     #pragma unroll
     for (int s = 0; s < SB; ++s) {
       const int piece = wave + NW * s;
-      if (piece < B_INSTR) {
+      if (B_INSTR % NW == 0 || piece < B_INSTR) {
         const int row = piece * 8 + (lane >> 3);
         const int ch = (lane & 7) ^ ((row >> 1) & 7);
-        const int k = k0 + ch * E;
-        const void* src = k < K ? (const void*)(b_src[s] + (long long)k0 * sizeof(T)) : g.zero;
-        __builtin_amdgcn_global_load_lds(GPTR(src), LPTR(st + A_BYTES + piece * 1024), 16, 0, 0);
+        const unsigned vo = k0 + ch * E < K ? b_voff[s] : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, LPTR(st + A_BYTES + piece * 1024), 16, vo, soff, 0, 0);
       }
     }
   };
@@ -269,6 +292,11 @@ void gemm_kernel(GemmArgs g) {
       }
     }
   }
+}
+
+template <typename T, int BM, int BN, int WAVES_M, int WAVES_N, int AMODE, int STAGES>
+__global__ __launch_bounds__(WAVES_M * WAVES_N * 64) void gemm_kernel(GemmArgs g) {
+  gemm_body<T, BM, BN, WAVES_M, WAVES_N, AMODE, STAGES>(g);
 }
 
 template <typename T, int BM, int BN, int WAVES_M, int WAVES_N, int STAGES>
