@@ -10,6 +10,10 @@ int launch_conv0_gn(const float* x, int B, int L, const float* norm, const float
                     int k0, int s0, int T0, const float* gamma, const float* beta, float eps, double* mom,
                     float2* ss, TO* out, hipStream_t s);
 
+template <typename TO>
+int launch_conv0_raw(const float* x, int B, int L, const float* norm, const float* w0, const float* b0, int C,
+                     int k0, int s0, int T0, TO* out, hipStream_t s);
+
 template <typename TI, typename TO>
 int launch_layernorm(const TI* in, const float* w, const float* b, int rows, int H, float eps, int act,
                      float* out_f, TO* out_t, hipStream_t s);

@@ -121,7 +121,7 @@ __global__ void gn_finalize_kernel(const double* __restrict__ mom, int B, int C,
   ss[i] = make_float2(sc, beta[c] - (float)mean * sc);
 }
 
-template <typename TO>
+template <typename TO, bool RAW>
 __global__ __launch_bounds__(512) void conv0_apply_kernel(const float* __restrict__ x, int L,
                                                           const float* __restrict__ norm,
                                                           const float* __restrict__ w0, const float* __restrict__ b0,
@@ -143,7 +143,7 @@ __global__ __launch_bounds__(512) void conv0_apply_kernel(const float* __restric
     #pragma unroll
     for (int j = 0; j < K0; ++j) w[j] = w0[c * K0 + j];
     const float bias = b0 ? b0[c] : 0.f;
-    const float2 sc = ss[(long long)b * C + c];
+    const float2 sc = RAW ? make_float2(1.f, 0.f) : ss[(long long)b * C + c];
     TO* ob = out + ((long long)b * T0 + t0) * C + c;
     // sliding window: frame t+1 reuses samples 5..9 of frame t, so 5 new LDS reads per frame
     float win[K0];
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(512) void conv0_apply_kernel(const float* __restric
       float y = bias;
       #pragma unroll
       for (int j = 0; j < K0; ++j) y = fmaf(w[j], win[j], y);
-      ob[(long long)t * C] = from_f32<TO>(gelu_erf(fmaf(y, sc.x, sc.y)));
+      ob[(long long)t * C] = from_f32<TO>(RAW ? y : gelu_erf(fmaf(y, sc.x, sc.y)));
       #pragma unroll
       for (int j = 0; j < K0 - S0; ++j) win[j] = win[j + S0];
       if (t + 1 < nt) {
@@ -175,9 +175,24 @@ int launch_conv0_gn(const float* x, int B, int L, const float* norm, const float
   hipLaunchKernelGGL(gn_finalize_kernel, dim3((B * C + 255) / 256), dim3(256), 0, s, mom, B, C, T0, w0, b0, gamma,
                      beta, eps, ss);
   dim3 grid((T0 + C0_T - 1) / C0_T, B), block(C < 512 ? C : 512);
-  hipLaunchKernelGGL((conv0_apply_kernel<TO>), grid, block, 0, s, x, L, norm, w0, b0, C, T0, ss, out);
+  hipLaunchKernelGGL((conv0_apply_kernel<TO, false>), grid, block, 0, s, x, L, norm, w0, b0, C, T0, ss, out);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// conv0 without GroupNorm/GELU (WavLM-large "layer" frontend: LN + GELU follow per frame)
+template <typename TO>
+int launch_conv0_raw(const float* x, int B, int L, const float* norm, const float* w0, const float* b0, int C,
+                     int k0, int s0, int T0, TO* out, hipStream_t s) {
+  if (k0 != K0 || s0 != 5) return -3;
+  dim3 grid((T0 + C0_T - 1) / C0_T, B), block(C < 512 ? C : 512);
+  hipLaunchKernelGGL((conv0_apply_kernel<TO, true>), grid, block, 0, s, x, L, norm, w0, b0, C, T0,
+                     (const float2*)nullptr, out);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+template int launch_conv0_raw<float>(const float*, int, int, const float*, const float*, const float*, int, int, int,
+                                     int, float*, hipStream_t);
+template int launch_conv0_raw<bf16>(const float*, int, int, const float*, const float*, const float*, int, int, int,
+                                    int, bf16*, hipStream_t);
 template int launch_conv0_gn<float>(const float*, int, int, const float*, const float*, const float*, int, int,
                                     int, int, const float*, const float*, float, double*, float2*, float*,
                                     hipStream_t);
@@ -520,6 +535,184 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
 // K and V staged into LDS ONCE and shared by all query blocks; each wave owns query blocks of
 // 16 and keeps the whole score row (NKB 16-key blocks) in registers: exact softmax, no
 // online rescaling.  Keys are padded to a multiple of 32 (not 64): at T = 149, 160 keys.
+// Long-sequence bf16 variant (Whisper T = 1500, WavLM clips > 160 frames): block = 128 queries
+// of one (head, clip) = 4 waves x 32 queries (two 16-query MFMA blocks per wave, so every K and
+// V fragment read from LDS feeds two MFMAs).  K/V tiles of 64 keys are double-buffered: the
+// next tile's global loads are issued into registers before the current tile's MFMAs and
+// written to the other LDS buffer after them — one barrier per tile.
+constexpr int F2_QPW = 32, F2_Q = 128, F2_K = 64;
+constexpr int F2_SVD = 36;                         // V^T row stride, dwords (16k+4): conflict-free b64 reads
+constexpr int F2_KS = F2_K * 128, F2_VS = AT_HD * F2_SVD * 4, F2_BUF = F2_KS + F2_VS;
+
+template <bool BIAS>
+__global__ __launch_bounds__(256) void attention_flash2_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* gate = (float*)(smem + 2 * F2_BUF);       // [F2_Q]
+  float* rb = gate + F2_Q;                         // [2*Tk]
+  const int qc = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int T = a.T, H = a.H, LQ = a.ldq;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  const int q0 = qc * F2_Q;
+  const int nkt = (T + F2_K - 1) / F2_K, Tk = nkt * F2_K;
+  const bf16* qkv = (const bf16*)a.qkv + (long long)b * T * LQ;
+
+  if (BIAS) {
+    if (tid < F2_Q)
+      gate[tid] = q0 + tid < T ? wavlm_gate(qkv + (long long)(q0 + tid) * LQ + 3 * H + 8 * h, a.gconst[h]) : 0.f;
+    const float* rh = a.relb + (long long)h * (2 * a.maxd + 1) + a.maxd;
+    for (int u = tid; u < 2 * Tk - 1; u += 256) {
+      int d = u - (Tk - 1);
+      d = d < -a.maxd ? -a.maxd : (d > a.maxd ? a.maxd : d);
+      rb[u] = rh[d];
+    }
+  }
+  // staging roles: K rows (2 chunks / thread), V 4-key groups x 8-dim chunks (threads 0..127)
+  const int kr0 = tid >> 3, kch = tid & 7;                     // K chunk tid and tid + 256
+  const int vch = tid >> 4, vkg = tid & 15;                    // V: chunk-major so b64 writes are contiguous
+  bf16x8 kreg[2], vreg[4];
+  auto load_tile = [&](int kt) {
+    const int kb0 = kt * F2_K;
+    #pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int key = kb0 + kr0 + 32 * u;
+      kreg[u] = key < T ? *(const bf16x8*)(qkv + (long long)key * LQ + H + h * AT_HD + kch * 8) : bf16x8{};
+    }
+    if (tid < 128) {
+      #pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int key = kb0 + vkg * 4 + u;
+        vreg[u] = key < T ? *(const bf16x8*)(qkv + (long long)key * LQ + 2 * H + h * AT_HD + vch * 8) : bf16x8{};
+      }
+    }
+  };
+  auto store_tile = [&](int buf) {
+    char* Ks = smem + buf * F2_BUF;
+    char* Vs = Ks + F2_KS;
+    #pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int kr = kr0 + 32 * u;
+      *(bf16x8*)(Ks + kr * 128 + ((kch ^ ((kr >> 1) & 7)) * 16)) = kreg[u];
+    }
+    if (tid < 128) {
+      #pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const bf16x4 pk = {vreg[0][e], vreg[1][e], vreg[2][e], vreg[3][e]};
+        *(bf16x4*)(Vs + (vch * 8 + e) * F2_SVD * 4 + vkg * 8) = pk;
+      }
+    }
+  };
+
+  // Q fragments of the wave's two 16-query blocks
+  bf16x8 qf[2][2];
+  int qi[2];
+  #pragma unroll
+  for (int qq = 0; qq < 2; ++qq) {
+    qi[qq] = q0 + wave * F2_QPW + qq * 16 + r16;
+    const bool v = qi[qq] < T;
+    const bf16* qrow = qkv + (long long)(v ? qi[qq] : 0) * LQ + h * AT_HD;
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks) qf[qq][ks] = v ? *(const bf16x8*)(qrow + ks * 32 + g * 8) : bf16x8{};
+  }
+  f32x4 o[2][4];
+  float m_run[2], l_run[2];
+  #pragma unroll
+  for (int qq = 0; qq < 2; ++qq) {
+    m_run[qq] = -INFINITY;
+    l_run[qq] = 0.f;
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) o[qq][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const float LOG2E = 1.4426950408889634f;
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) load_tile(kt + 1);           // in flight during this tile's MFMAs
+    const char* Ks = smem + cur * F2_BUF;
+    const char* Vs = Ks + F2_KS;
+    const int kbase = kt * F2_K;
+    f32x4 sc[2][4];
+    #pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      const int kr = kb * 16 + r16;
+      const bf16x8 k0 = *(const bf16x8*)(Ks + kr * 128 + (((g) ^ ((kr >> 1) & 7)) * 16));
+      const bf16x8 k1 = *(const bf16x8*)(Ks + kr * 128 + (((g + 4) ^ ((kr >> 1) & 7)) * 16));
+      #pragma unroll
+      for (int qq = 0; qq < 2; ++qq) {
+        f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf[qq][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        sc[qq][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf[qq][1], acc, 0, 0, 0);
+      }
+    }
+    bf16x8 pf[2][2];
+    #pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      float tmax = -INFINITY;
+      const float gq = BIAS ? gate[wave * F2_QPW + qq * 16 + r16] : 0.f;
+      #pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+        #pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kbase + kb * 16 + 4 * g + r;
+          float v = sc[qq][kb][r] * a.scale;
+          if (BIAS) v = fmaf(gq, rb[key - qi[qq] + (Tk - 1)], v);
+          v = key < T ? v : -INFINITY;
+          sc[qq][kb][r] = v;
+          tmax = fmaxf(tmax, v);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float m_new = fmaxf(m_run[qq], tmax);
+      const float alpha = exp2f((m_run[qq] - m_new) * LOG2E);
+      m_run[qq] = m_new;
+      l_run[qq] *= alpha;
+      #pragma unroll
+      for (int i = 0; i < 4; ++i) o[qq][i] *= alpha;
+      const float mb = m_new * LOG2E;
+      #pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+        #pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = exp2f(fmaf(sc[qq][kb][r], LOG2E, -mb));
+          l_run[qq] += p;
+          pf[qq][kb >> 1][(kb & 1) * 4 + r] = (bf16)p;
+        }
+    }
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      #pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const char* vrow = Vs + (db * 16 + r16) * F2_SVD * 4 + (ks * 32 + 4 * g) * 2;
+        const bf16x4 v0 = *(const bf16x4*)(vrow);
+        const bf16x4 v1 = *(const bf16x4*)(vrow + 32);
+        const bf16x8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        #pragma unroll
+        for (int qq = 0; qq < 2; ++qq) o[qq][db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qq][ks], o[qq][db], 0, 0, 0);
+      }
+    if (kt + 1 < nkt) store_tile(cur ^ 1);         // buffer cur^1 was last read before the previous barrier
+    __syncthreads();
+  }
+  #pragma unroll
+  for (int qq = 0; qq < 2; ++qq) {
+    float l = l_run[qq];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    if (qi[qq] < T) {
+      const float inv = 1.0f / l;
+      bf16* orow = (bf16*)a.out + ((long long)b * T + qi[qq]) * H + h * AT_HD;
+      #pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        bf16x4 ov = {(bf16)(o[qq][db][0] * inv), (bf16)(o[qq][db][1] * inv), (bf16)(o[qq][db][2] * inv),
+                     (bf16)(o[qq][db][3] * inv)};
+        *(bf16x4*)(orow + db * 16 + 4 * g) = ov;
+      }
+    }
+  }
+}
+
 template <typename TE, bool BIAS, int NKB>
 __global__ __launch_bounds__(512) void attention_full_kernel(AttnArgs a) {
   constexpr bool BF = sizeof(TE) == 2;
@@ -746,6 +939,15 @@ int launch_attention(const AttnArgs& a, int B, hipStream_t s) {
   if constexpr (BF) {   // fp32 (parity) path keeps the flash kernel: its full-row form spills
     if (a.T <= 160 && a.relb) return dispatch_full<T, true>(a, B, s);   // <= 10 key blocks: no spills
     if (a.T <= 160) return dispatch_full<T, false>(a, B, s);
+    const int Tk = ((a.T + F2_K - 1) / F2_K) * F2_K;
+    const size_t lds2 = 2 * F2_BUF + F2_Q * 4 + (a.relb ? (size_t)2 * Tk * 4 : 0);
+    if (lds2 > 160 * 1024) return -3;
+    dim3 g2((a.T + F2_Q - 1) / F2_Q, a.nh, B);
+    if (a.relb)
+      hipLaunchKernelGGL(attention_flash2_kernel<true>, g2, dim3(256), lds2, s, a);
+    else
+      hipLaunchKernelGGL(attention_flash2_kernel<false>, g2, dim3(256), lds2, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
   }
   dim3 grid((a.T + AT_Q - 1) / AT_Q, a.nh, B);
   if (a.relb)

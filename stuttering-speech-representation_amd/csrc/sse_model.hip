@@ -371,7 +371,7 @@ WavlmWs wavlm_plan(const sse_model* m, int B, int L, Plan& p) {
   const int C0 = c.conv_dim[0];
   size_t maxA = 0, maxB = 0;
   for (int i = 0; i < c.n_conv; ++i) {
-    const size_t sz = (size_t)B * Ts[i] * c.conv_dim[i] * (c.feat_norm_layer && i == 0 ? 4 : es);
+    const size_t sz = (size_t)B * Ts[i] * c.conv_dim[i] * es;
     if (i % 2 == 0) maxA = sz > maxA ? sz : maxA; else maxB = sz > maxB ? sz : maxB;
   }
   WavlmWs w;
@@ -461,11 +461,20 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
   // ---- conv feature encoder ----
   const int C0 = c.conv_dim[0];
   T* bufs[2] = {(T*)(ws + w.bufA), (T*)(ws + w.bufB)};
-  if (c.feat_norm_layer) return SSE_ERR_UNSUPPORTED;   // WavLM-large frontend: SURVEY §8(f) next-2
-  RC(prof(m, s, "conv0_gn", 2.0 * B * (double)Ts[0] * C0 * c.conv_kernel[0], 0, [&] { return launch_conv0_gn<T>(wave, B, L, norm, m->ptr<float>(m->conv_w[0]),
-                        m->conv_b[0] ? m->ptr<float>(m->conv_b[0]) : nullptr, C0, c.conv_kernel[0],
-                        c.conv_stride[0], Ts[0], m->ptr<float>(m->conv_ln_w[0]), m->ptr<float>(m->conv_ln_b[0]),
-                        1e-5f, (double*)(ws + w.part), (float2*)(ws + w.ss), bufs[0], s); }));
+  const float* b0 = m->conv_b[0] ? m->ptr<float>(m->conv_b[0]) : nullptr;
+  if (c.feat_norm_layer) {
+    // "layer" frontend (WavLM-large, HF modeling_wavlm.py:696-720): conv -> LN over channels -> GELU
+    RC(prof(m, s, "conv0_ln", 2.0 * B * (double)Ts[0] * C0 * c.conv_kernel[0], 0, [&] {
+      return launch_conv0_raw<T>(wave, B, L, norm, m->ptr<float>(m->conv_w[0]), b0, C0, c.conv_kernel[0],
+                                 c.conv_stride[0], Ts[0], bufs[0], s); }));
+    RC((launch_layernorm<T, T>(bufs[0], m->ptr<float>(m->conv_ln_w[0]), m->ptr<float>(m->conv_ln_b[0]), B * Ts[0], C0,
+                               1e-5f, ACT_GELU, nullptr, bufs[0], s)));
+  } else {
+    RC(prof(m, s, "conv0_gn", 2.0 * B * (double)Ts[0] * C0 * c.conv_kernel[0], 0, [&] {
+      return launch_conv0_gn<T>(wave, B, L, norm, m->ptr<float>(m->conv_w[0]), b0, C0, c.conv_kernel[0],
+                                c.conv_stride[0], Ts[0], m->ptr<float>(m->conv_ln_w[0]), m->ptr<float>(m->conv_ln_b[0]),
+                                1e-5f, (double*)(ws + w.part), (float2*)(ws + w.ss), bufs[0], s); }));
+  }
   for (int i = 1; i < c.n_conv; ++i) {
     const int cin = c.conv_dim[i - 1], co = c.conv_dim[i], k = c.conv_kernel[i], st = c.conv_stride[i];
     GemmArgs g{};
@@ -473,8 +482,11 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     g.M = B * Ts[i]; g.N = co; g.K = k * cin;
     g.rows_per_seg = Ts[i]; g.seg_stride = (long long)Ts[i - 1] * cin; g.lda = (long long)st * cin;
     g.bias = m->conv_b[i] ? m->ptr<float>(m->conv_b[i]) : nullptr;
-    g.Ct = bufs[i & 1]; g.ldc = co; g.act = ACT_GELU; g.zero = zero;
+    g.Ct = bufs[i & 1]; g.ldc = co; g.act = c.feat_norm_layer ? ACT_NONE : ACT_GELU; g.zero = zero;
     RC(prof(m, s, "gemm:conv", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    if (c.feat_norm_layer)
+      RC((launch_layernorm<T, T>(bufs[i & 1], m->ptr<float>(m->conv_ln_w[i]), m->ptr<float>(m->conv_ln_b[i]),
+                                 B * Ts[i], co, 1e-5f, ACT_GELU, nullptr, bufs[i & 1], s)));
   }
   const T* feat = bufs[(c.n_conv - 1) & 1];
   const int C = c.conv_dim[c.n_conv - 1];

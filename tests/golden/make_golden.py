@@ -138,6 +138,37 @@ def wavlm_golden(ref_w, manifest):
     }
 
 
+def wavlm_large_golden(ref_w, manifest):
+    """WavLM-large shape (layer-norm conv frontend, stable-LN encoder)."""
+    from transformers import Wav2Vec2FeatureExtractor, WavLMConfig, WavLMModel
+    spec = C.WAVLM_LARGE
+    sd = synth.synth_wavlm_state_dict(spec, seed=9)
+    cfg = WavLMConfig(hidden_size=1024, num_hidden_layers=24, num_attention_heads=16, intermediate_size=4096,
+                      feat_extract_norm="layer", do_stable_layer_norm=True, conv_bias=False)
+    model = WavLMModel(cfg)
+    missing, unexpected = model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=False)
+    assert not unexpected and set(missing) == {"masked_spec_embed"}, (missing, unexpected)
+    model.eval()
+    clips = synth.synth_clips(3, 48000, seed=77)
+    paths = _register("wavlm_large", clips)
+    idx = spec.default_layer_indices()                  # [24, 23, 22, 12]
+    fe = Wav2Vec2FeatureExtractor(do_normalize=True)    # wavlm-large normalises its input
+    t0 = time.time()
+    emb = np.stack([np.stack([ref_w.extract_wavlm_embeddings(p, model, fe, "cpu", idx)[f"layer_{i}"] for i in idx])
+                    for p in paths]).astype(np.float32)
+    manifest["wavlm_large_s"] = time.time() - t0
+    with torch.no_grad():
+        feats = model.feature_extractor(torch.from_numpy(clips[:1]))
+    np.savez_compressed(os.path.join(HERE, "wavlm_large.npz"), emb=emb, layer_indices=np.array(idx, np.int32),
+                        frontend_clip0=feats[0].numpy().T.copy())
+    manifest["wavlm_large"] = {"spec": spec.name, "weight_seed": 9, "clip_seed": 77, "n_clips": 3, "n_samples": 48000,
+                               "weights_sha256": _sd_sha(sd), "clips_sha256": _sha(clips), "layer_indices": idx,
+                               "reference_fn": "REF/WavLM_embeddings.py:extract_wavlm_embeddings",
+                               "feature_extractor": "Wav2Vec2FeatureExtractor(do_normalize=True)",
+                               "config": "WavLMConfig(1024/24/16/4096, feat_extract_norm=layer, "
+                                         "do_stable_layer_norm=True, conv_bias=False)"}
+
+
 def whisper_golden(ref_h, manifest, spec, tag, n_clips, seed, durations):
     from transformers import WhisperConfig, WhisperFeatureExtractor, WhisperModel
     sd = synth.synth_whisper_state_dict(spec, seed=seed)
@@ -176,6 +207,7 @@ def whisper_golden(ref_h, manifest, spec, tag, n_clips, seed, durations):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-large", action="store_true")
+    ap.add_argument("--only", default=None, help="wavlm | wavlm_large | whisper_tiny | whisper_large_v2")
     args = ap.parse_args()
     torch.set_num_threads(os.cpu_count())
     manifest = {"transformers": transformers.__version__, "torch": torch.__version__, "numpy": np.__version__}
@@ -186,9 +218,14 @@ def main():
             _install_torchaudio_stub()
             ref_w = _import_ref("ref_wavlm_embeddings", "WavLM_embeddings.py")
             ref_h = _import_ref("ref_whisper_embeddings_large", "whisper_embeddings_large.py")
-            wavlm_golden(ref_w, manifest)
-            whisper_golden(ref_h, manifest, C.WHISPER_TINY, "whisper_tiny", 2, 11, [3.0, 30.0])
-            if not args.skip_large:
+            only = args.only
+            if only in (None, "wavlm"):
+                wavlm_golden(ref_w, manifest)
+            if only in (None, "wavlm_large"):
+                wavlm_large_golden(ref_w, manifest)
+            if only in (None, "whisper_tiny"):
+                whisper_golden(ref_h, manifest, C.WHISPER_TINY, "whisper_tiny", 2, 11, [3.0, 30.0])
+            if not args.skip_large and only in (None, "whisper_large_v2"):
                 whisper_golden(ref_h, manifest, C.WHISPER_LARGE_V2, "whisper_large_v2", 1, 11, [3.0])
         finally:
             os.chdir(cwd)

@@ -118,3 +118,20 @@ def test_edge_lengths(m32, wavlm_sd):
         assert _rel(got, ref).max() <= FP32_TOL, L
     with pytest.raises(Exception):
         m32.embed(torch.zeros((1, 399), device="cuda:0"), [12])    # shorter than the receptive field (T = 0)
+
+
+@pytest.mark.parametrize("dtype,tol", [("fp32", FP32_TOL), ("bf16", BF16_TOL)])
+def test_wavlm_large_matches_reference(dtype, tol):
+    """WavLM-large shape (layer-norm conv frontend, stable-LN encoder, do_normalize=True)."""
+    import os
+    from conftest import GOLDEN
+    from ssr_amd import config as C, synth
+    from ssr_amd.model import SSEModel
+    g = np.load(os.path.join(GOLDEN, "wavlm_large.npz"))
+    m = SSEModel(C.WAVLM_LARGE, synth.synth_wavlm_state_dict(C.WAVLM_LARGE, seed=9), device="cuda:0", dtype=dtype,
+                 do_normalize=True)
+    clips = synth.synth_clips(3, 48000, seed=77)
+    got = m.embed(torch.from_numpy(clips).cuda(), [int(i) for i in g["layer_indices"]]).cpu().numpy()
+    rel = _rel(got, g["emb"])
+    print(dtype, "wavlm-large rel", rel.max())
+    assert rel.max() <= tol and _cos(got, g["emb"]).min() >= BF16_COS

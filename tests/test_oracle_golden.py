@@ -87,3 +87,18 @@ def test_rel_buckets_match_hf():
     mem = torch.arange(T)[None, :]
     ref = att._relative_positions_bucket(mem - ctx).numpy()
     assert np.array_equal(rel_position_buckets(T, T), ref)
+
+
+def test_wavlm_large_oracle_vs_reference(golden_manifest):
+    """WavLM-large shape: layer-norm conv frontend + stable-LN encoder."""
+    from oracle.wavlm import WavLMOracle
+    from ssr_amd import config as C, synth
+    g = np.load(os.path.join(GOLDEN, "wavlm_large.npz"))
+    man = golden_manifest["wavlm_large"]
+    clips = synth.synth_clips(3, 48000, seed=77)
+    assert _sha(clips) == man["clips_sha256"]
+    o = WavLMOracle(C.WAVLM_LARGE, synth.synth_wavlm_state_dict(C.WAVLM_LARGE, seed=9))
+    fe = o.feature_encoder(clips[0])
+    assert np.linalg.norm(fe - g["frontend_clip0"]) / np.linalg.norm(g["frontend_clip0"]) <= ORACLE_TOL
+    got = o.embed(clips[:2], [int(i) for i in g["layer_indices"]], do_normalize=True)
+    assert _rel(got, g["emb"][:2]).max() <= ORACLE_TOL
