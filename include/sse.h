@@ -69,6 +69,9 @@ typedef struct sse_cfg {
   int32_t n_mels;            /* 80                                                    */
   int32_t max_positions;     /* 1500                                                  */
   float ln_eps;              /* 1e-5                                                  */
+  /* Whisper 1-token decoder pass (REF/whisper_embeddings_large.py:257-262); 0 = encoder only */
+  int32_t decoder_layers;
+  int32_t dec_ffn;           /* decoder_ffn_dim                                       */
 } sse_cfg;
 
 typedef struct sse_model sse_model;
@@ -112,6 +115,18 @@ int sse_hidden_states(sse_model* m, const float* d_in, int B, int L, float* d_hs
  * d_hs [layers+1][B][1500][hidden] fp32.  Workspace: sse_workspace_bytes(m, B, 480000). */
 int sse_whisper_hidden_states_from_mel(sse_model* m, const float* d_mel, int B, float* d_hs, void* d_ws,
                                        size_t ws_bytes, void* stream);
+
+/* Whisper encoder AND decoder embeddings in one call (extract_whisper_embeddings_fixed,
+ * REF/whisper_embeddings_large.py:234-299): waves [B][L] -> d_enc_out [B][n_enc][hidden]
+ * (time-means of encoder hidden states) and d_dec_out [B][n_dec][hidden] (decoder hidden
+ * states of the single input token id 0; needs cfg.decoder_layers > 0). */
+int sse_whisper_embed(sse_model* m, const float* d_wave, int B, int L, const int32_t* enc_ids, int n_enc,
+                      float* d_enc_out, const int32_t* dec_ids, int n_dec, float* d_dec_out, void* d_ws,
+                      size_t ws_bytes, void* stream);
+/* model.decoder(input_ids=zeros([B,1]), encoder_hidden_states=enc) twin: d_enc [B][1500][hidden]
+ * fp32 (the encoder's last_hidden_state) -> d_hs [decoder_layers+1][B][hidden] fp32. */
+int sse_whisper_decoder_hidden_states(sse_model* m, const float* d_enc, int B, float* d_hs, void* d_ws,
+                                      size_t ws_bytes, void* stream);
 
 /* Wav2Vec2FeatureExtractor zero_mean_unit_var_norm on device (feature_extraction_wav2vec2.py:94):
  * d_out[b] = (d_in[b] - mean_b) / sqrt(var_b + 1e-7).  Workspace: 8 * B bytes. */

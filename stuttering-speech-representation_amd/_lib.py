@@ -22,7 +22,8 @@ EXPORTED = ("sse_weight_floats", "sse_model_create", "sse_model_destroy", "sse_o
             "sse_workspace_bytes", "sse_logmel_workspace_bytes", "sse_logmel", "sse_embed",
             "sse_hidden_states", "sse_strerror", "sse_rel_bucket", "sse_mel_filters", "sse_version",
             "sse_normalize", "sse_normalize_workspace_bytes", "sse_whisper_hidden_states_from_mel",
-            "sse_profile_start", "sse_profile_read", "sse_profile_stop", "sse_gemm")
+            "sse_profile_start", "sse_profile_read", "sse_profile_stop", "sse_gemm", "sse_whisper_embed",
+            "sse_whisper_decoder_hidden_states")
 
 
 class SSEError(RuntimeError):
@@ -44,7 +45,8 @@ class sse_cfg(ctypes.Structure):
                 ("pos_kernel", ctypes.c_int32), ("pos_groups", ctypes.c_int32),
                 ("num_buckets", ctypes.c_int32), ("max_distance", ctypes.c_int32),
                 ("do_normalize", ctypes.c_int32), ("n_mels", ctypes.c_int32),
-                ("max_positions", ctypes.c_int32), ("ln_eps", ctypes.c_float)]
+                ("max_positions", ctypes.c_int32), ("ln_eps", ctypes.c_float),
+                ("decoder_layers", ctypes.c_int32), ("dec_ffn", ctypes.c_int32)]
 
 
 def make_cfg(spec, do_normalize: bool = False) -> sse_cfg:
@@ -65,6 +67,7 @@ def make_cfg(spec, do_normalize: bool = False) -> sse_cfg:
         c.do_normalize = int(do_normalize)
     elif isinstance(spec, WhisperSpec):
         c.n_mels, c.max_positions = spec.n_mels, spec.max_positions
+        c.decoder_layers, c.dec_ffn = spec.decoder_layers, spec.dec_ffn_dim
     else:
         raise TypeError(spec)
     assert c.kind in (KIND_WAVLM, 1)
@@ -116,6 +119,10 @@ def lib() -> ctypes.CDLL:
     L.sse_profile_stop.restype = i32
     L.sse_gemm.argtypes = [i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, vp]
     L.sse_gemm.restype = i32
+    L.sse_whisper_embed.argtypes = [vp, vp, i32, i32, vp, i32, vp, vp, i32, vp, vp, sz, vp]
+    L.sse_whisper_embed.restype = i32
+    L.sse_whisper_decoder_hidden_states.argtypes = [vp, vp, i32, vp, vp, sz, vp]
+    L.sse_whisper_decoder_hidden_states.restype = i32
     L.sse_strerror.argtypes = [i32]
     L.sse_strerror.restype = ctypes.c_char_p
     L.sse_rel_bucket.argtypes = [i32, i32, i32]

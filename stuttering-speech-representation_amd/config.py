@@ -13,8 +13,8 @@ REF/whisper_embeddings_large.py:437-438) and reads the shapes from the hub
   (HF/models/whisper/modeling_whisper.py:540-646).
 
 ``param_specs(spec)`` is the ONE canonical ordering of HF state-dict tensors that the
-C-ABI ``sse_model_create`` consumes as a flat fp32 blob.  ``csrc/sse_weights.cpp``
-walks the same order; ``sse_weight_floats`` lets the host check that both sides agree.
+C-ABI ``sse_model_create`` consumes as a flat fp32 blob.  ``csrc/sse_model.hip``
+(build_wavlm / build_whisper) walks the same order; ``sse_weight_floats`` lets the host check that both sides agree.
 """
 from __future__ import annotations
 
@@ -98,6 +98,19 @@ class WhisperSpec:
 
     n_samples: int = 480000      # 30 s @ 16 kHz (WhisperFeatureExtractor.n_samples)
     n_frames: int = 3000         # mel frames after dropping the last STFT frame
+    decoder_layers: int = 0      # >0: also the 1-token decoder pass (REF/whisper_embeddings_large.py:257-262)
+    dec_ffn: int = 0             # decoder_ffn_dim (defaults to ffn)
+    vocab_size: int = 51865
+    max_target_positions: int = 448
+
+    @property
+    def dec_ffn_dim(self) -> int:
+        return self.dec_ffn or self.ffn
+
+    def default_decoder_indices(self) -> list[int]:
+        """``decoder_indices`` of the reference: the last three decoder hidden states."""
+        n = self.decoder_layers + 1
+        return [n - 1, n - 2, n - 3]
 
     def default_layer_indices(self) -> list[int]:
         """``encoder_indices`` of the reference: the last three hidden states
@@ -108,6 +121,9 @@ class WhisperSpec:
 
 WHISPER_LARGE_V2 = WhisperSpec()
 WHISPER_TINY = WhisperSpec(d_model=384, layers=4, heads=6, ffn=1536, name="whisper-tiny")
+# encoder + the reference's 1-token decoder pass (decoder_layer_* embeddings)
+WHISPER_LARGE_V2_DEC = WhisperSpec(decoder_layers=32, name="whisper-large-v2+decoder")
+WHISPER_TINY_DEC = WhisperSpec(d_model=384, layers=4, heads=6, ffn=1536, decoder_layers=4, name="whisper-tiny+decoder")
 
 
 def param_specs(spec) -> list[tuple[str, tuple]]:
@@ -170,6 +186,26 @@ def param_specs(spec) -> list[tuple[str, tuple]]:
                     (f"{p}.fc2.weight", (D, F)), (f"{p}.fc2.bias", (D,)),
                     (f"{p}.final_layer_norm.weight", (D,)), (f"{p}.final_layer_norm.bias", (D,))]
         out += [("encoder.layer_norm.weight", (D,)), ("encoder.layer_norm.bias", (D,))]
+        if spec.decoder_layers:
+            # Only what the 1-token pass with input id 0 at position 0 reads: row 0 of both
+            # embedding tables; of the causal self-attention (one key) only v_proj / out_proj
+            # matter (softmax over a single key is exactly 1).
+            Fd = spec.dec_ffn_dim
+            out += [("decoder.embed_tokens.weight[0]", (D,)), ("decoder.embed_positions.weight[0]", (D,))]
+            for l in range(spec.decoder_layers):
+                p = f"decoder.layers.{l}"
+                out += [(f"{p}.self_attn_layer_norm.weight", (D,)), (f"{p}.self_attn_layer_norm.bias", (D,)),
+                        (f"{p}.self_attn.v_proj.weight", (D, D)), (f"{p}.self_attn.v_proj.bias", (D,)),
+                        (f"{p}.self_attn.out_proj.weight", (D, D)), (f"{p}.self_attn.out_proj.bias", (D,)),
+                        (f"{p}.encoder_attn_layer_norm.weight", (D,)), (f"{p}.encoder_attn_layer_norm.bias", (D,)),
+                        (f"{p}.encoder_attn.q_proj.weight", (D, D)), (f"{p}.encoder_attn.q_proj.bias", (D,)),
+                        (f"{p}.encoder_attn.k_proj.weight", (D, D)),
+                        (f"{p}.encoder_attn.v_proj.weight", (D, D)), (f"{p}.encoder_attn.v_proj.bias", (D,)),
+                        (f"{p}.encoder_attn.out_proj.weight", (D, D)), (f"{p}.encoder_attn.out_proj.bias", (D,)),
+                        (f"{p}.final_layer_norm.weight", (D,)), (f"{p}.final_layer_norm.bias", (D,)),
+                        (f"{p}.fc1.weight", (Fd, D)), (f"{p}.fc1.bias", (Fd,)),
+                        (f"{p}.fc2.weight", (D, Fd)), (f"{p}.fc2.bias", (D,))]
+            out += [("decoder.layer_norm.weight", (D,)), ("decoder.layer_norm.bias", (D,))]
         return out
     raise TypeError(f"unknown spec {spec!r}")
 

@@ -33,3 +33,9 @@ struct AttnArgs {
 };
 template <typename T>
 int launch_attention(const AttnArgs& a, int B, hipStream_t s);
+
+template <typename TE>
+int launch_xattn1(const TE* q, const TE* kv, int B, int T, int D, int nh, TE* out, hipStream_t s);
+int launch_bcast_rows(const float* v, int D, int B, float* out, hipStream_t s);
+template <typename TO>
+int launch_cast(const float* x, long long n, TO* y, hipStream_t s);

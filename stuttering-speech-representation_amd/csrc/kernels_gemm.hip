@@ -35,7 +35,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
   static_assert(STAGES == 2 || (A_INSTR % NW == 0 && B_INSTR % NW == 0), "uniform pieces per wave");
   constexpr int P = SA + SB;   // glds per wave per tile (STAGES == 3)
   constexpr int CLD = BN + 4;                 // epilogue: padded fp32 C row (conflict-free b32 writes)
-  constexpr int SMEM = STAGES * STAGE > BM * CLD * 4 ? STAGES * STAGE : BM * CLD * 4;
+  // the fp32 C tile goes through LDS in row chunks of EPI_ROWS (the whole tile when it fits)
+  constexpr int EPI_ROWS = (BM * CLD * 4 <= 80 * 1024 || BM * CLD * 4 <= STAGES * STAGE) ? BM : BM / 2;
+  static_assert(BM % EPI_ROWS == 0 && EPI_ROWS % WM == 0, "epilogue chunks must hold whole wave rows");
+  constexpr int SMEM = STAGES * STAGE > EPI_ROWS * CLD * 4 ? STAGES * STAGE : EPI_ROWS * CLD * 4;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int lane = threadIdx.x & 63;
@@ -236,57 +239,62 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
   // ---- epilogue: stage the fp32 tile through LDS, then one coalesced pass per 16-B chunk:
   //      v = acc + bias (act) (+resid) -> fp32 and/or element-type stores -----------------
   float* Cs = (float*)smem;
-  __syncthreads();                            // every wave is done reading the operand stages
-  #pragma unroll
-  for (int i = 0; i < TM; ++i)
-    #pragma unroll
-    for (int j = 0; j < TN; ++j)
-      #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        Cs[(wm * WM + i * 16 + q * 4 + r) * CLD + wn * WN + j * 16 + r16] = acc[i][j][r];
-  __syncthreads();
   constexpr int NT = NW * 64;
-  constexpr int CH = BM * BN / 4;             // 16-B chunks in the tile
+  constexpr int CH = EPI_ROWS * BN / 4;       // 16-B chunks per epilogue chunk
   constexpr int UNR = 4;
   const int col0 = grp * N;
   const bool has_bias = g.bias != nullptr, has_res = g.resid != nullptr, gelu = g.act == ACT_GELU;
-  for (int base = threadIdx.x; base < CH; base += NT * UNR) {
-    f32x4 v[UNR], rv[UNR], bv[UNR];
-    long long off[UNR];
-    bool ok[UNR];
-    #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const int c0 = base + u * NT;
-      const int c = c0 < CH ? c0 : CH - 1;
-      const int row = c / (BN / 4), cc = (c % (BN / 4)) * 4;
-      const int m = m0 + row, n = n0 + cc;
-      ok[u] = m < M && c0 < CH;
-      off[u] = (long long)(ok[u] ? m : 0) * g.ldc + col0 + n;
-      v[u] = *(const f32x4*)(Cs + row * CLD + cc);
-      bv[u] = has_bias ? *(const f32x4*)(g.bias + col0 + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-      rv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (has_res) {
-        const long long ro = g.resid_rows ? (long long)((ok[u] ? m : 0) % g.resid_rows) * g.ldc + col0 + n : off[u];
-        rv[u] = *(const f32x4*)(g.resid + ro);
-      }
-    }
-    #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      f32x4 o;
+  #pragma unroll
+  for (int half = 0; half < BM / EPI_ROWS; ++half) {
+    __syncthreads();                          // operand stages (or the previous chunk) fully consumed
+    if (wm * WM >= half * EPI_ROWS && wm * WM < (half + 1) * EPI_ROWS) {
       #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float x = v[u][e] + bv[u][e];
-        if (gelu) x = gelu_erf(x);
-        o[e] = x + rv[u][e];
+      for (int i = 0; i < TM; ++i)
+        #pragma unroll
+        for (int j = 0; j < TN; ++j)
+          #pragma unroll
+          for (int r = 0; r < 4; ++r)
+            Cs[(wm * WM - half * EPI_ROWS + i * 16 + q * 4 + r) * CLD + wn * WN + j * 16 + r16] = acc[i][j][r];
+    }
+    __syncthreads();
+    for (int base = threadIdx.x; base < CH; base += NT * UNR) {
+      f32x4 v[UNR], rv[UNR], bv[UNR];
+      long long off[UNR];
+      bool ok[UNR];
+      #pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int c0 = base + u * NT;
+        const int c = c0 < CH ? c0 : CH - 1;
+        const int row = c / (BN / 4), cc = (c % (BN / 4)) * 4;
+        const int m = m0 + half * EPI_ROWS + row, n = n0 + cc;
+        ok[u] = m < M && c0 < CH;
+        off[u] = (long long)(ok[u] ? m : 0) * g.ldc + col0 + n;
+        v[u] = *(const f32x4*)(Cs + row * CLD + cc);
+        bv[u] = has_bias ? *(const f32x4*)(g.bias + col0 + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+        rv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (has_res) {
+          const long long ro = g.resid_rows ? (long long)((ok[u] ? m : 0) % g.resid_rows) * g.ldc + col0 + n : off[u];
+          rv[u] = *(const f32x4*)(g.resid + ro);
+        }
       }
-      if (ok[u]) {
-        if (g.Cf) *(f32x4*)(g.Cf + off[u]) = o;
-        if (g.Ct) {
-          if constexpr (sizeof(T) == 2) {
-            bf16x4 ob = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
-            *(bf16x4*)((T*)g.Ct + off[u]) = ob;
-          } else {
-            *(f32x4*)((T*)g.Ct + off[u]) = o;
+      #pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        f32x4 o;
+        #pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = v[u][e] + bv[u][e];
+          if (gelu) x = gelu_erf(x);
+          o[e] = x + rv[u][e];
+        }
+        if (ok[u]) {
+          if (g.Cf) *(f32x4*)(g.Cf + off[u]) = o;
+          if (g.Ct) {
+            if constexpr (sizeof(T) == 2) {
+              bf16x4 ob = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+              *(bf16x4*)((T*)g.Ct + off[u]) = ob;
+            } else {
+              *(f32x4*)((T*)g.Ct + off[u]) = o;
+            }
           }
         }
       }
@@ -318,8 +326,13 @@ int launch_any(const GemmArgs& a, int amode, int groups, hipStream_t s) {
   // default: 128x128 tile, 4 waves of 64x64, 2-stage LDS (2 blocks/CU overlap one block's
   // epilogue with the other's MFMA loop: measured 656 vs 637 TF/s on the WavLM-base step).
   // SSE_GEMM_CFG=2 selects the 256x128, 8-wave, 3-stage ring (144 KiB, 1 block/CU) for A/B runs.
-  static const int force = [] { const char* e = getenv("SSE_GEMM_CFG"); return e ? atoi(e) : 0; }();
+  const char* fe = getenv("SSE_GEMM_CFG");     // read per launch so one process can A/B configs
+  const int force = fe ? atoi(fe) : 0;
   if (a.N % 128 == 0 && a.M >= 2048 && force == 2) return launch_cfg<T, 256, 128, 4, 2, 3>(a, amode, groups, s);
+  if constexpr (sizeof(T) == 2) {
+    // SSE_GEMM_CFG=3: 256x256 tile, 8 waves (2x4) of 128x64, 2-stage 128 KiB ring (1 block/CU)
+    if (a.N % 256 == 0 && a.M >= 4096 && force == 3) return launch_cfg<T, 256, 256, 2, 4, 2>(a, amode, groups, s);
+  }
   if (a.N % 128 == 0) return launch_cfg<T, 128, 128, 2, 2, 2>(a, amode, groups, s);
   if (a.N % 64 == 0) return launch_cfg<T, 128, 64, 4, 1, 2>(a, amode, groups, s);
   if (a.N % 48 == 0) return launch_cfg<T, 128, 48, 4, 1, 2>(a, amode, groups, s);

@@ -958,3 +958,87 @@ int launch_attention(const AttnArgs& a, int B, hipStream_t s) {
 }
 template int launch_attention<float>(const AttnArgs&, int, hipStream_t);
 template int launch_attention<bf16>(const AttnArgs&, int, hipStream_t);
+
+// ---------------------------------------------------------------------------------------
+// Whisper decoder cross-attention for ONE query token per clip (REF/whisper_embeddings_large.py
+// :257-262 -> HF modeling_whisper.py:284-356 with key_value_states): block = (head, clip),
+// 256 threads.  Scores over the T encoder frames in fp32, block softmax, then
+// out[d] = sum_j p_j V[j][d] with 4 key groups x 64 dims and an LDS reduction.  Memory-bound
+// (reads each K/V row once); q is pre-scaled by head_dim^-1/2 at load time.
+template <typename TE>
+__global__ __launch_bounds__(256) void xattn1_kernel(const TE* __restrict__ q, const TE* __restrict__ kv, int T,
+                                                     int D, TE* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  float* qs = sh;                 // [64]
+  float* sc = sh + 64;            // [T]
+  float* red = sc + T;            // [4][64] + reductions
+  const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const TE* kvb = kv + (long long)b * T * 2 * D;
+  if (tid < 64) qs[tid] = to_f32(q[(long long)b * D + h * 64 + tid]);
+  __syncthreads();
+  float mx = -INFINITY;
+  for (int j = tid; j < T; j += 256) {
+    const TE* kr = kvb + (long long)j * 2 * D + h * 64;
+    float s = 0.f;
+    #pragma unroll 8
+    for (int d = 0; d < 64; ++d) s = fmaf(qs[d], to_f32(kr[d]), s);
+    sc[j] = s;
+    mx = fmaxf(mx, s);
+  }
+  mx = wave_max(mx);
+  if ((tid & 63) == 0) red[tid >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float sum = 0.f;
+  for (int j = tid; j < T; j += 256) {
+    const float p = expf(sc[j] - mx);
+    sc[j] = p;
+    sum += p;
+  }
+  sum = wave_sum(sum);
+  if ((tid & 63) == 0) red[4 + (tid >> 6)] = sum;
+  __syncthreads();
+  sum = red[4] + red[5] + red[6] + red[7];
+  const int kg = tid >> 6, d = tid & 63;
+  float acc = 0.f;
+  for (int j = kg; j < T; j += 4) acc = fmaf(sc[j], to_f32(kvb[(long long)j * 2 * D + D + h * 64 + d]), acc);
+  red[8 + kg * 64 + d] = acc;
+  __syncthreads();
+  if (tid < 64) {
+    const float o = (red[8 + d] + red[8 + 64 + d] + red[8 + 128 + d] + red[8 + 192 + d]) / sum;
+    out[(long long)b * D + h * 64 + d] = from_f32<TE>(o);
+  }
+}
+
+template <typename TE>
+int launch_xattn1(const TE* q, const TE* kv, int B, int T, int D, int nh, TE* out, hipStream_t s) {
+  const size_t lds = (64 + (size_t)T + 8 + 256) * 4;
+  if (lds > 160 * 1024 || D != nh * 64) return -3;
+  hipLaunchKernelGGL((xattn1_kernel<TE>), dim3(nh, B), dim3(256), lds, s, q, kv, T, D, out);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+template int launch_xattn1<float>(const float*, const float*, int, int, int, int, float*, hipStream_t);
+template int launch_xattn1<bf16>(const bf16*, const bf16*, int, int, int, int, bf16*, hipStream_t);
+
+__global__ void bcast_rows_kernel(const float* __restrict__ v, int D, int B, float* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i < (long long)B * D) out[i] = v[i % D];
+}
+int launch_bcast_rows(const float* v, int D, int B, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(bcast_rows_kernel, dim3((unsigned)(((long long)B * D + 255) / 256)), dim3(256), 0, s, v, D, B, out);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+template <typename TO>
+__global__ void cast_kernel(const float* __restrict__ x, long long n, TO* __restrict__ y) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) y[i] = from_f32<TO>(x[i]);
+}
+template <typename TO>
+int launch_cast(const float* x, long long n, TO* y, hipStream_t s) {
+  hipLaunchKernelGGL((cast_kernel<TO>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, n, y);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+template int launch_cast<float>(const float*, long long, float*, hipStream_t);
+template int launch_cast<bf16>(const float*, long long, bf16*, hipStream_t);

@@ -94,6 +94,13 @@ struct LayerW {
   size_t g_const, g_w, g_b;   // WavLM gate
 };
 
+// Whisper decoder layer for the 1-token pass (HF/models/whisper/modeling_whisper.py:448-506)
+struct DecLayerW {
+  size_t ln1_w, ln1_b, v_w, v_b, o_w, o_b;           // self-attention: one key -> softmax == 1
+  size_t ln2_w, ln2_b, q_w, q_b, kv_w, kv_b, co_w, co_b;   // cross-attention (q pre-scaled)
+  size_t ln3_w, ln3_b, f1_w, f1_b, f2_w, f2_b;
+};
+
 }  // namespace
 
 struct sse_model {
@@ -107,6 +114,8 @@ struct sse_model {
   size_t fp_ln_w, fp_ln_b, fp_w, fp_b, pos_w, pos_b, enc_ln_w, enc_ln_b, relb, zero;
   // Whisper
   size_t c1_w, c1_b, c2_w, c2_b, positions;
+  size_t dec_x0, dec_ln_w, dec_ln_b;   // decoder: embed_tokens[0] + embed_positions[0]; final LN
+  std::vector<DecLayerW> dec;
   int ldq = 0;   // QKV GEMM width: 3H (+ 8*heads gate columns for WavLM), padded to 128
   std::vector<LayerW> layers;
   // live per-launch timing (sse_profile_*): events pre-created outside any capture
@@ -131,6 +140,7 @@ bool cfg_valid(const sse_cfg* c) {
     if (c->n_conv < 2 || c->n_conv > 8 || c->pos_groups <= 0 || c->hidden % c->pos_groups) return false;
   } else if (c->kind == SSE_KIND_WHISPER) {
     if (c->n_mels <= 0 || c->max_positions <= 0) return false;
+    if (c->decoder_layers < 0 || (c->decoder_layers > 0 && c->dec_ffn <= 0)) return false;
   } else {
     return false;
   }
@@ -313,6 +323,57 @@ int build_whisper(sse_model* m, Blob& bl, Arena& ar) {
     m->enc_ln_w = ar.put_f32(elw, D);
     m->enc_ln_b = ar.put_f32(elb, D);
   }
+  if (c.decoder_layers <= 0) return SSE_OK;
+  // ---- decoder (config.param_specs order) ----
+  const int Fd = c.dec_ffn;
+  const float *e0 = bl.take(D), *p0 = bl.take(D);
+  if (!bl.ok) return SSE_ERR_WEIGHTS;
+  if (e0) {
+    std::vector<float> x0(D);
+    for (int i = 0; i < D; ++i) x0[i] = e0[i] + p0[i];   // inputs_embeds + positions (fp32 add, as torch)
+    m->dec_x0 = ar.put_f32(x0.data(), D);
+  }
+  auto mat = [&](const float* w, size_t n, float sc) {
+    std::vector<float> v(w, w + n);
+    if (sc != 1.f) for (auto& e : v) e *= sc;
+    return v;
+  };
+  for (int l = 0; l < c.decoder_layers; ++l) {
+    const float *l1w = bl.take(D), *l1b = bl.take(D);
+    const float *vw = bl.take((size_t)D * D), *vb = bl.take(D), *ow = bl.take((size_t)D * D), *ob = bl.take(D);
+    const float *l2w = bl.take(D), *l2b = bl.take(D);
+    const float *qw = bl.take((size_t)D * D), *qb = bl.take(D), *kw = bl.take((size_t)D * D);
+    const float *cvw = bl.take((size_t)D * D), *cvb = bl.take(D), *cow = bl.take((size_t)D * D), *cob = bl.take(D);
+    const float *l3w = bl.take(D), *l3b = bl.take(D);
+    const float *f1w = bl.take((size_t)Fd * D), *f1b = bl.take(Fd), *f2w = bl.take((size_t)D * Fd), *f2b = bl.take(D);
+    if (!bl.ok) return SSE_ERR_WEIGHTS;
+    if (!l1w) continue;
+    DecLayerW W{};
+    W.ln1_w = ar.put_f32(l1w, D); W.ln1_b = ar.put_f32(l1b, D);
+    W.v_w = ar.put_elem(mat(vw, (size_t)D * D, 1.f), BF); W.v_b = ar.put_f32(vb, D);
+    W.o_w = ar.put_elem(mat(ow, (size_t)D * D, 1.f), BF); W.o_b = ar.put_f32(ob, D);
+    W.ln2_w = ar.put_f32(l2w, D); W.ln2_b = ar.put_f32(l2b, D);
+    W.q_w = ar.put_elem(mat(qw, (size_t)D * D, scale), BF);
+    std::vector<float> qbs(qb, qb + D);
+    for (auto& e : qbs) e *= scale;
+    W.q_b = ar.put_f32(qbs.data(), D);
+    std::vector<float> kv((size_t)2 * D * D), kvb((size_t)2 * D, 0.f);   // [K rows | V rows]; k_proj has no bias
+    std::memcpy(kv.data(), kw, (size_t)D * D * 4);
+    std::memcpy(kv.data() + (size_t)D * D, cvw, (size_t)D * D * 4);
+    std::memcpy(kvb.data() + D, cvb, D * 4);
+    W.kv_w = ar.put_elem(kv, BF); W.kv_b = ar.put_f32(kvb.data(), 2 * D);
+    W.co_w = ar.put_elem(mat(cow, (size_t)D * D, 1.f), BF); W.co_b = ar.put_f32(cob, D);
+    W.ln3_w = ar.put_f32(l3w, D); W.ln3_b = ar.put_f32(l3b, D);
+    W.f1_w = ar.put_elem(mat(f1w, (size_t)Fd * D, 1.f), BF); W.f1_b = ar.put_f32(f1b, Fd);
+    W.f2_w = ar.put_elem(mat(f2w, (size_t)D * Fd, 1.f), BF); W.f2_b = ar.put_f32(f2b, D);
+    m->dec.push_back(W);
+  }
+  const float *dlw = bl.take(D), *dlb = bl.take(D);
+  if (!bl.ok) return SSE_ERR_WEIGHTS;
+  if (dlw) {
+    m->dec_ln_w = ar.put_f32(dlw, D);
+    m->dec_ln_b = ar.put_f32(dlb, D);
+  }
   return SSE_OK;
 }
 
@@ -394,6 +455,7 @@ WavlmWs wavlm_plan(const sse_model* m, int B, int L, Plan& p) {
 
 struct WhisperWs {
   size_t zero, lm, mel, h1, x, xb, qkv, ctx, ff, xf;
+  size_t dx, dxb, dv, dq, dctx, dff, dxf;   // decoder rows [B][*]
 };
 
 WhisperWs whisper_plan(const sse_model* m, int B, Plan& p) {
@@ -412,6 +474,15 @@ WhisperWs whisper_plan(const sse_model* m, int B, Plan& p) {
   w.ctx = p.add(M * D * es);
   w.ff = p.add(M * (size_t)c.ffn * es);
   w.xf = p.add(M * D * 4);
+  if (c.decoder_layers > 0) {
+    w.dx = p.add((size_t)B * D * 4);
+    w.dxb = p.add((size_t)B * D * es);
+    w.dv = p.add((size_t)B * D * es);
+    w.dq = p.add((size_t)B * D * es);
+    w.dctx = p.add((size_t)B * D * es);
+    w.dff = p.add((size_t)B * c.dec_ffn * es);
+    w.dxf = p.add((size_t)B * D * 4);
+  }
   return w;
 }
 
@@ -568,9 +639,70 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
   return 0;
 }
 
+// The reference's 1-token decoder pass (REF/whisper_embeddings_large.py:257-262): input id 0 at
+// position 0, cross-attending to the encoder's last_hidden_state enc [B*Tq][D] (type T).  Rows
+// are clips (M = B); the K|V projection of the encoder output is the one large GEMM per layer.
+// hidden_states[i] = input of layer i, hidden_states[L] = final-LN output
+// (HF/models/whisper/modeling_whisper.py:739-790, HF/utils/output_capturing.py:268-279).
+template <typename T>
+int whisper_decoder(sse_model* m, const T* enc, int B, const Sink& sink, char* ws, const WhisperWs& w,
+                    hipStream_t s) {
+  const sse_cfg& c = m->cfg;
+  const int D = c.hidden, Fd = c.dec_ffn, nh = c.heads, Tq = c.max_positions;
+  const float eps = c.ln_eps;
+  void* zero = ws + w.zero;
+  float* x = (float*)(ws + w.dx);
+  T* xb = (T*)(ws + w.dxb);
+  T* v = (T*)(ws + w.dv);
+  T* q = (T*)(ws + w.dq);
+  T* ctx = (T*)(ws + w.dctx);
+  T* ff = (T*)(ws + w.dff);
+  T* kv = (T*)(ws + w.qkv);   // encoder QKV buffer [B*Tq][3D] >= [B*Tq][2D]
+  RC(launch_bcast_rows(m->ptr<float>(m->dec_x0), D, B, x, s));
+  RC(sink.emit(0, x));
+  auto lin = [&](const char* tag, const T* A, size_t wo, size_t bo, int N, int K, const float* resid, float* Cf,
+                 T* Ct, int act) {
+    GemmArgs g{};
+    g.A = A; g.B = m->ptr(wo); g.M = B; g.N = N; g.K = K; g.rows_per_seg = B; g.lda = K;
+    g.bias = m->ptr<float>(bo); g.resid = resid; g.Cf = Cf; g.Ct = Ct; g.ldc = N; g.act = act; g.zero = zero;
+    return prof(m, s, tag, gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); });
+  };
+  for (int l = 0; l < c.decoder_layers; ++l) {
+    const DecLayerW& W = m->dec[l];
+    // self-attention over the single (own) key: softmax == 1, so attn == v_proj(LN(x))
+    RC((launch_layernorm<float, T>(x, m->ptr<float>(W.ln1_w), m->ptr<float>(W.ln1_b), B, D, eps, ACT_NONE, nullptr,
+                                   xb, s)));
+    RC(lin("dec_gemm:v", xb, W.v_w, W.v_b, D, D, nullptr, nullptr, v, ACT_NONE));
+    RC(lin("dec_gemm:o", v, W.o_w, W.o_b, D, D, x, x, nullptr, ACT_NONE));
+    // cross-attention
+    RC((launch_layernorm<float, T>(x, m->ptr<float>(W.ln2_w), m->ptr<float>(W.ln2_b), B, D, eps, ACT_NONE, nullptr,
+                                   xb, s)));
+    RC(lin("dec_gemm:q", xb, W.q_w, W.q_b, D, D, nullptr, nullptr, q, ACT_NONE));
+    {
+      GemmArgs g{};
+      g.A = enc; g.B = m->ptr(W.kv_w); g.M = B * Tq; g.N = 2 * D; g.K = D; g.rows_per_seg = B * Tq; g.lda = D;
+      g.bias = m->ptr<float>(W.kv_b); g.Ct = kv; g.ldc = 2 * D; g.zero = zero;
+      RC(prof(m, s, "gemm:dec_kv", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    }
+    RC(prof(m, s, "dec_xattn", 4.0 * B * (double)Tq * D, (double)B * Tq * 2 * D * sizeof(T),
+            [&] { return launch_xattn1<T>(q, kv, B, Tq, D, nh, ctx, s); }));
+    RC(lin("dec_gemm:co", ctx, W.co_w, W.co_b, D, D, x, x, nullptr, ACT_NONE));
+    // feed-forward
+    RC((launch_layernorm<float, T>(x, m->ptr<float>(W.ln3_w), m->ptr<float>(W.ln3_b), B, D, eps, ACT_NONE, nullptr,
+                                   xb, s)));
+    RC(lin("dec_gemm:fc1", xb, W.f1_w, W.f1_b, Fd, D, nullptr, nullptr, ff, ACT_GELU));
+    RC(lin("dec_gemm:fc2", ff, W.f2_w, W.f2_b, D, Fd, x, x, nullptr, ACT_NONE));
+    if (l + 1 < c.decoder_layers) RC(sink.emit(l + 1, x));
+  }
+  float* xf = (float*)(ws + w.dxf);
+  RC((launch_layernorm<float, T>(x, m->ptr<float>(m->dec_ln_w), m->ptr<float>(m->dec_ln_b), B, D, eps, ACT_NONE, xf,
+                                 (T*)nullptr, s)));
+  return sink.emit(c.decoder_layers, xf);
+}
+
 template <typename T>
 int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& sink, char* ws, hipStream_t s,
-                    const float* mel_hf = nullptr) {
+                    const float* mel_hf = nullptr, const Sink* dsink = nullptr) {
   const sse_cfg& c = m->cfg;
   Plan p;
   const WhisperWs w = whisper_plan(m, B, p);
@@ -635,13 +767,14 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
   // hidden_states[-1] is the post-LN last_hidden_state (HF/utils/output_capturing.py:268-279)
   float* xf = (float*)(ws + w.xf);
   RC((launch_layernorm<float, T>(x, m->ptr<float>(m->enc_ln_w), m->ptr<float>(m->enc_ln_b), M, D, eps, ACT_NONE, xf,
-                                 (T*)nullptr, s)));
+                                 dsink ? xb : (T*)nullptr, s)));
   RC(sink.emit(c.layers, xf));
+  if (dsink) RC(whisper_decoder<T>(m, xb, B, *dsink, ws, w, s));
   return 0;
 }
 
 int forward(sse_model* m, const float* d_in, int B, int L, const Sink& sink, void* d_ws, size_t ws_bytes,
-            hipStream_t s, bool from_mel = false) {
+            hipStream_t s, bool from_mel = false, const Sink* dsink = nullptr) {
   if (!m || !d_in || B <= 0 || L <= 0) return SSE_ERR_INVALID;
   if (ws_bytes < sse_workspace_bytes(m, B, L)) return SSE_ERR_WORKSPACE;
   if (m->cfg.kind == SSE_KIND_WAVLM && wavlm_frames(m->cfg, L, nullptr) <= 0) return SSE_ERR_INVALID;
@@ -653,8 +786,8 @@ int forward(sse_model* m, const float* d_in, int B, int L, const Sink& sink, voi
     rc = m->bf() ? wavlm_forward<bf16>(m, d_in, B, L, sink, (char*)d_ws, s)
                  : wavlm_forward<float>(m, d_in, B, L, sink, (char*)d_ws, s);
   else
-    rc = m->bf() ? whisper_forward<bf16>(m, d_in, B, L, sink, (char*)d_ws, s, from_mel ? d_in : nullptr)
-                 : whisper_forward<float>(m, d_in, B, L, sink, (char*)d_ws, s, from_mel ? d_in : nullptr);
+    rc = m->bf() ? whisper_forward<bf16>(m, d_in, B, L, sink, (char*)d_ws, s, from_mel ? d_in : nullptr, dsink)
+                 : whisper_forward<float>(m, d_in, B, L, sink, (char*)d_ws, s, from_mel ? d_in : nullptr, dsink);
   if (dev != m->device) (void)hipSetDevice(dev);
   return rc;
 }
@@ -805,6 +938,48 @@ int sse_whisper_hidden_states_from_mel(sse_model* m, const float* d_mel, int B, 
   if (!m || !d_hs || m->cfg.kind != SSE_KIND_WHISPER) return SSE_ERR_INVALID;
   Sink sk{nullptr, 0, nullptr, d_hs, B, m->cfg.max_positions, m->cfg.hidden, (hipStream_t)stream};
   return forward(m, d_mel, B, 2 * m->cfg.max_positions, sk, d_ws, ws_bytes, (hipStream_t)stream, true);
+}
+
+int sse_whisper_embed(sse_model* m, const float* d_wave, int B, int L, const int32_t* enc_ids, int n_enc,
+                      float* d_enc_out, const int32_t* dec_ids, int n_dec, float* d_dec_out, void* d_ws,
+                      size_t ws_bytes, void* stream) {
+  if (!m || m->cfg.kind != SSE_KIND_WHISPER || n_enc < 0 || n_dec < 0 || (n_enc && (!enc_ids || !d_enc_out)) ||
+      (n_dec && (!dec_ids || !d_dec_out)) || (n_dec && m->cfg.decoder_layers <= 0))
+    return SSE_ERR_INVALID;
+  for (int i = 0; i < n_enc; ++i)
+    if (enc_ids[i] < 0 || enc_ids[i] > m->cfg.layers) return SSE_ERR_INVALID;
+  for (int i = 0; i < n_dec; ++i)
+    if (dec_ids[i] < 0 || dec_ids[i] > m->cfg.decoder_layers) return SSE_ERR_INVALID;
+  Sink sk{enc_ids, n_enc, d_enc_out, nullptr, B, m->cfg.max_positions, m->cfg.hidden, (hipStream_t)stream};
+  Sink dk{dec_ids, n_dec, d_dec_out, nullptr, B, 1, m->cfg.hidden, (hipStream_t)stream};
+  return forward(m, d_wave, B, L, sk, d_ws, ws_bytes, (hipStream_t)stream, false, n_dec ? &dk : nullptr);
+}
+
+int sse_whisper_decoder_hidden_states(sse_model* m, const float* d_enc, int B, float* d_hs, void* d_ws,
+                                      size_t ws_bytes, void* stream) {
+  if (!m || !d_enc || !d_hs || B <= 0 || m->cfg.kind != SSE_KIND_WHISPER || m->cfg.decoder_layers <= 0)
+    return SSE_ERR_INVALID;
+  if (ws_bytes < sse_workspace_bytes(m, B, 2 * m->cfg.max_positions)) return SSE_ERR_WORKSPACE;
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) return SSE_ERR_HIP;
+  if (dev != m->device && hipSetDevice(m->device) != hipSuccess) return SSE_ERR_HIP;
+  hipStream_t s = (hipStream_t)stream;
+  Plan p;
+  const WhisperWs w = whisper_plan(m, B, p);
+  char* ws = (char*)d_ws;
+  Sink dk{nullptr, 0, nullptr, d_hs, B, 1, m->cfg.hidden, s};
+  const long long n = (long long)B * m->cfg.max_positions * m->cfg.hidden;
+  int rc = hipMemsetAsync(ws + w.zero, 0, 256, s) == hipSuccess ? 0 : SSE_ERR_HIP;
+  if (!rc) {
+    if (m->bf()) {
+      rc = launch_cast<bf16>(d_enc, n, (bf16*)(ws + w.xb), s);
+      if (!rc) rc = whisper_decoder<bf16>(m, (const bf16*)(ws + w.xb), B, dk, ws, w, s);
+    } else {
+      rc = whisper_decoder<float>(m, d_enc, B, dk, ws, w, s);
+    }
+  }
+  if (dev != m->device) (void)hipSetDevice(dev);
+  return rc;
 }
 
 int sse_profile_start(sse_model* m, int max_launches) {

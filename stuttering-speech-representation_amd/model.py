@@ -43,9 +43,16 @@ def pack_weights(spec, state_dict: dict) -> np.ndarray:
         sd[pre + "parametrizations.weight.original1"] = sd.pop(pre + "weight_v")
     parts = []
     for key, shape in param_specs(spec):
-        if key not in sd:
+        if key.endswith("[0]") and key not in sd:        # row 0 of an embedding table
+            base = key[:-3]
+            if base not in sd:
+                raise KeyError(f"state dict lacks {base}")
+            v = sd[base]
+            a = _as_numpy(v[0] if isinstance(v, torch.Tensor) else np.asarray(v)[0])
+        elif key not in sd:
             raise KeyError(f"state dict lacks {key}")
-        a = _as_numpy(sd[key])
+        else:
+            a = _as_numpy(sd[key])
         if tuple(a.shape) != tuple(shape):
             raise ValueError(f"{key}: shape {tuple(a.shape)} != expected {tuple(shape)}")
         parts.append(a.ravel())

@@ -127,12 +127,37 @@ def sinusoids(length: int, channels: int, max_timescale: float = 10000.0) -> np.
     return np.concatenate([np.sin(st), np.cos(st)], axis=1).astype(np.float32)
 
 
-def synth_whisper_state_dict(spec: WhisperSpec, seed: int = 11) -> dict[str, np.ndarray]:
+def _whisper_hf_extra(spec: WhisperSpec) -> list[tuple[str, tuple]]:
+    """Decoder tensors an HF WhisperModel holds but the 1-token pass never reads (full embedding
+    tables and the self-attention q/k projections): synthesised so a HF model can be loaded."""
+    D = spec.d_model
+    out = [("decoder.embed_tokens.weight", (spec.vocab_size, D)),
+           ("decoder.embed_positions.weight", (spec.max_target_positions, D))]
+    for l in range(spec.decoder_layers):
+        p = f"decoder.layers.{l}.self_attn"
+        out += [(f"{p}.q_proj.weight", (D, D)), (f"{p}.q_proj.bias", (D,)), (f"{p}.k_proj.weight", (D, D))]
+    return out
+
+
+def synth_whisper_state_dict(spec: WhisperSpec, seed: int = 11, full_hf: bool = False) -> dict[str, np.ndarray]:
+    """Synthetic Whisper weights.  Decoder rows that the path reads through "[0]" keys are row 0
+    of the full synthetic tables, so ``full_hf=True`` (HF-loadable) and the packed blob agree."""
     sd = {}
-    for key, shape in param_specs(spec):
+    specs = [(k, s) for k, s in param_specs(spec) if not k.endswith("[0]")]
+    if spec.decoder_layers:
+        specs += _whisper_hf_extra(spec)
+    for key, shape in specs:
         n = int(np.prod(shape))
-        if key.endswith("embed_positions.weight"):
+        if key == "encoder.embed_positions.weight":
             sd[key] = sinusoids(shape[0], shape[1])
+            continue
+        if key in ("decoder.embed_tokens.weight", "decoder.embed_positions.weight"):
+            if not full_hf:                              # only row 0 is read (input id 0, position 0)
+                sd[key + "[0]"] = (0.5 * uniform_pm1_f32(seed, _stream_of(key), shape[1])).astype(np.float32)
+                continue
+            t = (0.5 * uniform_pm1_f32(seed, _stream_of(key), n)).reshape(shape).astype(np.float32)
+            t[0] = (0.5 * uniform_pm1_f32(seed, _stream_of(key), shape[1])).astype(np.float32)
+            sd[key] = t
             continue
         u = uniform_pm1_f32(seed, _stream_of(key), n)
         fan = int(np.prod(shape[1:])) if len(shape) > 1 else 1

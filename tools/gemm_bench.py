@@ -8,8 +8,12 @@ from ssr_amd.model import gemm
 
 SHAPES = {"qkv": (38144, 2432, 768, None), "oproj": (38144, 768, 768, "res"), "ffn1": (38144, 3072, 768, "gelu"),
           "ffn2": (38144, 768, 3072, "res"), "proj": (38144, 768, 512, None), "sq4096": (4096, 4096, 4096, None)}
+cfgs = sys.argv[1:] or ["0"]
 res = {}
-for name, (M, N, K, epi) in SHAPES.items():
+for cfg, (name, (M, N, K, epi)) in [(c, kv) for kv in SHAPES.items() for c in cfgs]:
+    os.environ["SSE_GEMM_CFG"] = cfg
+    if cfg == "3" and name == "qkv":
+        N = 2560
     a = torch.randn(M, K, device="cuda").bfloat16()
     b = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
     bias = torch.randn(N, device="cuda")
@@ -26,5 +30,5 @@ for name, (M, N, K, epi) in SHAPES.items():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / n
-    res[name] = {"ms": round(ms, 4), "tflops": round(2 * M * N * K / ms / 1e9, 1)}
+    res[f"{name}@{cfg}"] = {"ms": round(ms, 4), "tflops": round(2 * M * N * K / ms / 1e9, 1)}
 print(json.dumps(res))
