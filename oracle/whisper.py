@@ -8,6 +8,9 @@ Follows:
   WhisperEncoderLayer / WhisperAttention          HF/models/whisper/modeling_whisper.py:215-413
   output capture (hs[-1] = post-LN)               HF/utils/output_capturing.py:105-117, 268-279
   encoder pooling                                 REF/whisper_embeddings_large.py:264-281
+  1-token decoder pass (input id 0, position 0)   REF/whisper_embeddings_large.py:257-262,
+                                                  HF/models/whisper/modeling_whisper.py:448-506, 689-790
+  decoder "pooling" (squeeze the single token)    REF/whisper_embeddings_large.py:283-297
 """
 from __future__ import annotations
 
@@ -119,6 +122,61 @@ class WhisperOracle:
             hs.append(x)
         hs[-1] = layer_norm(x, p["encoder.layer_norm.weight"], p["encoder.layer_norm.bias"], eps)
         return hs
+
+    def _row0(self, key):
+        p = self.p
+        return p[key + "[0]"] if key + "[0]" in p else p[key][0]
+
+    def decoder_hidden_states(self, enc):
+        """enc [1500, D] (encoder last_hidden_state) -> decoder_layers+1 states [D] for input id 0.
+
+        Self-attention of one query over its own single key: softmax == 1 exactly, so the block
+        is out_proj(v_proj(LN(x))) (q_proj / k_proj do not influence the result)."""
+        s, p, eps = self.spec, self.p, self.spec.ln_eps
+        nh, hd = s.heads, s.head_dim
+        x = (self._row0("decoder.embed_tokens.weight") + self._row0("decoder.embed_positions.weight")).astype(self.dt)
+        hs = [x]
+        for l in range(s.decoder_layers):
+            q_ = f"decoder.layers.{l}"
+            h = layer_norm(x[None], p[f"{q_}.self_attn_layer_norm.weight"], p[f"{q_}.self_attn_layer_norm.bias"], eps)[0]
+            v = h @ p[f"{q_}.self_attn.v_proj.weight"].T + p[f"{q_}.self_attn.v_proj.bias"]
+            x = (x + v @ p[f"{q_}.self_attn.out_proj.weight"].T + p[f"{q_}.self_attn.out_proj.bias"]).astype(self.dt)
+            a = f"{q_}.encoder_attn"
+            h = layer_norm(x[None], p[f"{q_}.encoder_attn_layer_norm.weight"],
+                           p[f"{q_}.encoder_attn_layer_norm.bias"], eps)[0]
+            q = (h @ p[f"{a}.q_proj.weight"].T + p[f"{a}.q_proj.bias"]) * np.asarray(hd ** -0.5, self.dt)
+            k = enc @ p[f"{a}.k_proj.weight"].T
+            v = enc @ p[f"{a}.v_proj.weight"].T + p[f"{a}.v_proj.bias"]
+            qh = q.reshape(nh, hd)
+            kh = k.reshape(-1, nh, hd).transpose(1, 0, 2)
+            vh = v.reshape(-1, nh, hd).transpose(1, 0, 2)
+            sc = np.einsum("hd,htd->ht", qh, kh)
+            sc = sc - sc.max(-1, keepdims=True)
+            e = np.exp(sc)
+            pr = e / e.sum(-1, keepdims=True)
+            ctx = np.einsum("ht,htd->hd", pr, vh).reshape(-1).astype(self.dt)
+            x = (x + ctx @ p[f"{a}.out_proj.weight"].T + p[f"{a}.out_proj.bias"]).astype(self.dt)
+            h = layer_norm(x[None], p[f"{q_}.final_layer_norm.weight"], p[f"{q_}.final_layer_norm.bias"], eps)[0]
+            h = gelu((h @ p[f"{q_}.fc1.weight"].T + p[f"{q_}.fc1.bias"]).astype(self.dt))
+            x = (x + h @ p[f"{q_}.fc2.weight"].T + p[f"{q_}.fc2.bias"]).astype(self.dt)
+            hs.append(x)
+        hs[-1] = layer_norm(x[None], p["decoder.layer_norm.weight"], p["decoder.layer_norm.bias"], eps)[0]
+        return hs
+
+    def embed_both(self, waves, enc_indices, dec_indices):
+        """extract_whisper_embeddings_fixed restated: (enc [B][n_enc][D], dec [B][n_dec][D])."""
+        waves = np.atleast_2d(waves)
+        D = self.spec.d_model
+        enc = np.zeros((waves.shape[0], len(enc_indices), D), dtype=np.float32)
+        dec = np.zeros((waves.shape[0], len(dec_indices), D), dtype=np.float32)
+        for b in range(waves.shape[0]):
+            hs = self.hidden_states(log_mel(waves[b], self.spec.n_mels))
+            for j, idx in enumerate(enc_indices):
+                enc[b, j] = hs[idx].mean(axis=0)
+            ds = self.decoder_hidden_states(hs[-1])
+            for j, idx in enumerate(dec_indices):
+                dec[b, j] = ds[idx]
+        return enc, dec
 
     def embed(self, waves, layer_indices):
         waves = np.atleast_2d(waves)

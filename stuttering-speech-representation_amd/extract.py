@@ -146,25 +146,48 @@ def extract_wavlm_embeddings(audio_file, model, feature_extractor, device, layer
 
 
 def extract_embeddings_from_audio_whisper(audio_array, model, processor, device, layer_names):
-    """REF/model_training_1.py:268-316 (in-memory twin).  ``decoder_layer_*`` names need the
-    decoder pass: they are reported and skipped."""
+    """REF/model_training_1.py:268-316 (in-memory twin): ``encoder_layer_<i>`` time-means and
+    ``decoder_layer_<i>`` states of the 1-token decoder pass, in ``layer_names`` order.  A model
+    built without the decoder (decoder_layers=0) reports and skips decoder names."""
     try:
-        enc = [int(n.split("_")[-1]) for n in layer_names if n.startswith("encoder_layer_")]
-        dec = [n for n in layer_names if n.startswith("decoder_layer_")]
-        if dec:
-            logger.warning(f"decoder embeddings {dec} are not built yet (SURVEY §8(f) next-1); skipped")
+        wanted = []
+        for n in layer_names:
+            if n.startswith("encoder_layer_") or n.startswith("decoder_layer_"):
+                wanted.append((n.startswith("decoder_"), int(n.split("_")[-1]), n))
         with torch.no_grad():
             if isinstance(model, WhisperModel):
-                n_hs = model.sse.spec.layers + 1
-                valid = [i for i in enc if i < n_hs]
-                if not valid:
+                spec = model.sse.spec
+                if any(d for d, _, _ in wanted) and not spec.decoder_layers:
+                    logger.warning(f"{spec.name} was built without the decoder; decoder_layer_* skipped")
+                    wanted = [w for w in wanted if not w[0]]
+                enc = [i for d, i, _ in wanted if not d and i < spec.layers + 1]
+                dec = [i for d, i, _ in wanted if d and i < spec.decoder_layers + 1]
+                if not enc and not dec:
                     return {}
                 wave = torch.from_numpy(np.ascontiguousarray(np.asarray(audio_array, np.float32)))
-                emb = model.embed(wave.to(model.sse.device), valid).cpu().numpy()
-                return {f"encoder_layer_{i}": emb[0, j].copy() for j, i in enumerate(valid)}
+                e, dd = model.sse.whisper_embed(wave.to(model.sse.device), enc, dec)
+                e, dd = e.cpu().numpy(), dd.cpu().numpy()
+                out = {}
+                for d, i, n in wanted:
+                    if d and i in dec:
+                        out[n] = dd[0, dec.index(i)].copy()
+                    elif not d and i in enc:
+                        out[n] = e[0, enc.index(i)].copy()
+                return out
             feats = processor(audio_array, sampling_rate=16000, return_tensors="pt").input_features.to(device)
-            outputs = model.encoder(feats, output_hidden_states=True, return_dict=True)
-            return _pool_generic(outputs.hidden_states, enc, "encoder_layer_")
+            eo = model.encoder(feats, output_hidden_states=True, return_dict=True)
+            do = None
+            if any(d for d, _, _ in wanted):
+                do = model.decoder(input_ids=torch.zeros((1, 1), dtype=torch.long).to(device),
+                                   encoder_hidden_states=eo.last_hidden_state, output_hidden_states=True,
+                                   return_dict=True)
+            out = {}
+            for d, i, n in wanted:
+                states = do.hidden_states if d else eo.hidden_states
+                if i < len(states):
+                    h = states[i]
+                    out[n] = (h.squeeze(1) if d else torch.mean(h, dim=1)).cpu().numpy().flatten()
+            return out
     except Exception as e:
         if _is_oom(e):
             logger.error("HIP out of memory while extracting Whisper embeddings")
@@ -175,9 +198,16 @@ def extract_embeddings_from_audio_whisper(audio_array, model, processor, device,
 
 
 def extract_whisper_embeddings_fixed(audio_file, model, processor, device, encoder_indices, decoder_indices):
-    """REF/whisper_embeddings_large.py:234-299 (encoder part; decoder part: §8(f) next-1)."""
+    """REF/whisper_embeddings_large.py:234-299: encoder time-means + 1-token decoder states."""
     audio = load_audio(audio_file)
     if audio is None:
         return None
+    if isinstance(model, WhisperModel):
+        for i in encoder_indices:
+            if i >= model.sse.spec.layers + 1:
+                logger.warning(f"Encoder layer {i} is out of range (max: {model.sse.spec.layers})")
+        for i in decoder_indices:
+            if model.sse.spec.decoder_layers and i >= model.sse.spec.decoder_layers + 1:
+                logger.warning(f"Decoder layer {i} is out of range (max: {model.sse.spec.decoder_layers})")
     names = [f"encoder_layer_{i}" for i in encoder_indices] + [f"decoder_layer_{i}" for i in decoder_indices]
     return extract_embeddings_from_audio_whisper(audio, model, processor, device, names)

@@ -12,8 +12,9 @@ The reference's glue only touches a narrow surface of the HF objects it is hande
                                                REF/whisper_embeddings_large.py:242-246
 These classes provide exactly that surface, so the reference's own functions (and
 model_training_*.py) run unchanged on them, with every tensor op in libsse.so on the GPU.
-The decoder half of WhisperModel (REF/whisper_embeddings_large.py:257-262) is SURVEY §8(f)
-next-1 and raises NotImplementedError here.
+  model.decoder(input_ids=zeros((1, 1)), encoder_hidden_states=..., output_hidden_states=True)
+                                               REF/whisper_embeddings_large.py:257-262
+The decoder twin supports exactly that call (one token, id 0, position 0); other ids raise.
 """
 from __future__ import annotations
 
@@ -167,25 +168,49 @@ class _WhisperEncoder:
 
 
 class _WhisperDecoder:
-    def __call__(self, *a, **k):
-        raise NotImplementedError("the 1-token Whisper decoder pass is SURVEY §8(f) next-1 (not built yet)")
+    """The reference's decoder call: one start token (id 0) per clip at position 0."""
+
+    def __init__(self, sse: SSEModel):
+        self.sse = sse
+
+    def __call__(self, input_ids=None, encoder_hidden_states=None, output_hidden_states=None, return_dict=True,
+                 attention_mask=None, past_key_values=None, **_):
+        if not self.sse.spec.decoder_layers:
+            raise NotImplementedError(f"{self.sse.spec.name} was built without the decoder (decoder_layers=0)")
+        if encoder_hidden_states is None or input_ids is None:
+            raise ValueError("the decoder twin needs input_ids and encoder_hidden_states")
+        if attention_mask is not None or past_key_values is not None:
+            raise NotImplementedError("only the 1-token pass of REF/whisper_embeddings_large.py:257-262")
+        ids = torch.as_tensor(input_ids)
+        if ids.dim() != 2 or ids.shape[1] != 1 or bool((ids != 0).any()):
+            raise NotImplementedError("only input_ids == zeros((B, 1)) (the reference's start token) is built")
+        enc = encoder_hidden_states.to(self.sse.device)
+        if enc.shape[0] != ids.shape[0]:
+            raise ValueError(f"batch mismatch: input_ids {tuple(ids.shape)} vs encoder states {tuple(enc.shape)}")
+        hs = self.sse.decoder_hidden_states(enc)
+        return BaseModelOutput(last_hidden_state=hs[-1], hidden_states=hs if output_hidden_states else None)
 
 
 class WhisperModel(_DuckModel):
-    """WhisperModel twin: ``.encoder`` runs on the HIP path; ``.decoder`` is not built yet."""
+    """WhisperModel twin: ``.encoder`` and the 1-token ``.decoder`` pass run on the HIP path."""
 
     def __init__(self, sse: SSEModel):
         super().__init__(sse)
         self.encoder = _WhisperEncoder(sse)
-        self.decoder = _WhisperDecoder()
+        self.decoder = _WhisperDecoder(sse)
 
     @classmethod
     def from_state_dict(cls, spec, state_dict, device="cuda:0", dtype="fp32"):
         return cls(SSEModel(spec, state_dict, device=device, dtype=dtype))
 
     @classmethod
-    def from_hf(cls, hf_model, device="cuda:0", dtype="fp32"):
+    def from_hf(cls, hf_model, device="cuda:0", dtype="fp32", with_decoder=True):
         c = hf_model.config
+        if c.decoder_attention_heads != c.encoder_attention_heads:
+            raise NotImplementedError("decoder and encoder head counts differ")
         spec = C.WhisperSpec(d_model=c.d_model, layers=c.encoder_layers, heads=c.encoder_attention_heads,
-                             ffn=c.encoder_ffn_dim, n_mels=c.num_mel_bins, max_positions=c.max_source_positions)
+                             ffn=c.encoder_ffn_dim, n_mels=c.num_mel_bins, max_positions=c.max_source_positions,
+                             decoder_layers=c.decoder_layers if with_decoder else 0, dec_ffn=c.decoder_ffn_dim,
+                             vocab_size=c.vocab_size, max_target_positions=c.max_target_positions,
+                             name=getattr(c, "_name_or_path", "") or "whisper")
         return cls.from_state_dict(spec, hf_model.state_dict(), device, dtype)

@@ -194,6 +194,47 @@ class SSEModel:
         return tuple(hs.unbind(0))
 
 
+    def whisper_embed(self, wave: torch.Tensor, encoder_indices, decoder_indices, enc_out=None, dec_out=None):
+        """Whisper: encoder time-means AND 1-token decoder states in one pass
+        (REF/whisper_embeddings_large.py:234-299) -> ([B, n_enc, H], [B, n_dec, H]) fp32."""
+        if not isinstance(self.spec, WhisperSpec):
+            raise TypeError("whisper_embed is Whisper-only")
+        if decoder_indices and not self.spec.decoder_layers:
+            raise ValueError(f"{self.spec.name} was built without the decoder (decoder_layers=0)")
+        wave = self._check_wave(wave)
+        B, L = wave.shape
+        H = self.spec.hidden
+        eid = torch.tensor([int(i) for i in encoder_indices], dtype=torch.int32)
+        did = torch.tensor([int(i) for i in decoder_indices], dtype=torch.int32)
+        if enc_out is None:
+            enc_out = torch.empty((B, eid.numel(), H), dtype=torch.float32, device=self.device)
+        if dec_out is None:
+            dec_out = torch.empty((B, did.numel(), H), dtype=torch.float32, device=self.device)
+        ws = self.workspace(B, L)
+        _lib.check(_lib.lib().sse_whisper_embed(self._h, wave.data_ptr(), B, L, eid.data_ptr(), eid.numel(),
+                                                enc_out.data_ptr() if eid.numel() else None, did.data_ptr(),
+                                                did.numel(), dec_out.data_ptr() if did.numel() else None,
+                                                ws.data_ptr(), ws.numel(), self._stream()), "sse_whisper_embed")
+        return enc_out, dec_out
+
+    def decoder_hidden_states(self, enc: torch.Tensor) -> tuple:
+        """Whisper: ``model.decoder(input_ids=zeros([B, 1]), encoder_hidden_states=enc)`` hidden states:
+        enc [B, 1500, H] -> decoder_layers+1 tensors [B, 1, H] fp32."""
+        if not isinstance(self.spec, WhisperSpec) or not self.spec.decoder_layers:
+            raise TypeError("decoder_hidden_states needs a Whisper spec with decoder_layers > 0")
+        T, H = self.spec.max_positions, self.spec.hidden
+        if enc.device != self.device or enc.dim() != 3 or tuple(enc.shape[1:]) != (T, H):
+            raise ValueError(f"expected [B, {T}, {H}] encoder states on {self.device}, got {tuple(enc.shape)}")
+        enc = enc.to(torch.float32).contiguous()
+        B = enc.shape[0]
+        hs = torch.empty((self.spec.decoder_layers + 1, B, 1, H), dtype=torch.float32, device=self.device)
+        ws = self.workspace(B, self.spec.n_samples)
+        _lib.check(_lib.lib().sse_whisper_decoder_hidden_states(self._h, enc.data_ptr(), B, hs.data_ptr(),
+                                                                ws.data_ptr(), ws.numel(), self._stream()),
+                   "sse_whisper_decoder_hidden_states")
+        return tuple(hs.unbind(0))
+
+
 def logmel(wave: torch.Tensor, n_mels: int = 80) -> torch.Tensor:
     """Whisper log-mel on device: [B, L] (L <= 480000) -> [B, n_mels, 3000] (HF layout)."""
     if wave.dim() == 1:

@@ -19,6 +19,7 @@ Usage: python tests/golden/make_golden.py [--skip-large]
 from __future__ import annotations
 
 import argparse
+import dataclasses
 import hashlib
 import importlib
 import importlib.util
@@ -170,21 +171,26 @@ def wavlm_large_golden(ref_w, manifest):
 
 
 def whisper_golden(ref_h, manifest, spec, tag, n_clips, seed, durations):
+    """Encoder AND decoder embeddings from the reference glue.  ``spec`` carries decoder_layers;
+    the decoder weights are the synthetic ``full_hf`` tables (row 0 == the compact blob's "[0]"
+    rows), so the decoder fixture is pinned and reproducible anywhere."""
     from transformers import WhisperConfig, WhisperFeatureExtractor, WhisperModel
-    sd = synth.synth_whisper_state_dict(spec, seed=seed)
+    enc_spec = dataclasses.replace(spec, decoder_layers=0, name=spec.name.split("+")[0])
+    sd = synth.synth_whisper_state_dict(spec, seed=seed, full_hf=True)
     cfg = WhisperConfig(d_model=spec.d_model, encoder_layers=spec.layers, encoder_attention_heads=spec.heads,
-                        decoder_layers=2, decoder_attention_heads=spec.heads, encoder_ffn_dim=spec.ffn,
-                        decoder_ffn_dim=spec.ffn, num_mel_bins=spec.n_mels, vocab_size=51865)
-    torch.manual_seed(0)
+                        decoder_layers=spec.decoder_layers, decoder_attention_heads=spec.heads,
+                        encoder_ffn_dim=spec.ffn, decoder_ffn_dim=spec.dec_ffn_dim, num_mel_bins=spec.n_mels,
+                        vocab_size=spec.vocab_size, max_target_positions=spec.max_target_positions)
     model = WhisperModel(cfg)
     missing, unexpected = model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=False)
-    assert not unexpected and all(k.startswith("decoder.") for k in missing), unexpected
+    assert not unexpected and not missing, (missing, unexpected)
     model.eval()
+    del sd
     clips = [synth.synth_clips(1, int(16000 * d), seed=4321, first_clip=i)[0] for i, d in enumerate(durations)]
     paths = _register(tag, clips)
     proc = WhisperFeatureExtractor(feature_size=spec.n_mels)
     enc_idx = spec.default_layer_indices()
-    dec_idx = [2, 1, 0]
+    dec_idx = spec.default_decoder_indices() + [0]
     t0 = time.time()
     embs, decs = [], []
     for p in paths[:n_clips]:
@@ -194,14 +200,16 @@ def whisper_golden(ref_h, manifest, spec, tag, n_clips, seed, durations):
     manifest[f"{tag}_s"] = time.time() - t0
     mels = np.stack([proc(c, sampling_rate=16000, return_tensors="np").input_features[0] for c in clips[:n_clips]])
     out = {"emb": np.stack(embs).astype(np.float32), "layer_indices": np.array(enc_idx, np.int32),
-           "mel": mels.astype(np.float32), "decoder_emb_unpinned": np.stack(decs).astype(np.float32)}
+           "mel": mels.astype(np.float32), "dec_emb": np.stack(decs).astype(np.float32),
+           "decoder_indices": np.array(dec_idx, np.int32)}
     np.savez_compressed(os.path.join(HERE, f"{tag}.npz"), **out)
-    manifest[tag] = {"spec": spec.name, "weight_seed": seed, "clip_seed": 4321, "durations_s": durations[:n_clips],
-                     "clips_sha256": [_sha(c) for c in clips[:n_clips]],
-                     "weights_sha256": _sd_sha(sd), "layer_indices": enc_idx,
+    manifest[tag] = {"spec": enc_spec.name, "decoder_spec": spec.name, "weight_seed": seed, "clip_seed": 4321,
+                     "durations_s": durations[:n_clips], "clips_sha256": [_sha(c) for c in clips[:n_clips]],
+                     "weights_sha256": _sd_sha(synth.synth_whisper_state_dict(enc_spec, seed=seed)),
+                     "decoder_weights_sha256": _sd_sha(synth.synth_whisper_state_dict(spec, seed=seed)),
+                     "layer_indices": enc_idx, "decoder_indices": dec_idx,
                      "reference_fn": "REF/whisper_embeddings_large.py:extract_whisper_embeddings_fixed",
-                     "note": "decoder_emb_unpinned uses torch.manual_seed(0) decoder weights not reproducible "
-                             "off this container; kept for the next-1 row, not used by tests"}
+                     "note": "decoder: input id 0 at position 0 (REF :257-262); synthetic full_hf decoder tables"}
 
 
 def main():
@@ -224,9 +232,9 @@ def main():
             if only in (None, "wavlm_large"):
                 wavlm_large_golden(ref_w, manifest)
             if only in (None, "whisper_tiny"):
-                whisper_golden(ref_h, manifest, C.WHISPER_TINY, "whisper_tiny", 2, 11, [3.0, 30.0])
+                whisper_golden(ref_h, manifest, C.WHISPER_TINY_DEC, "whisper_tiny", 2, 11, [3.0, 30.0])
             if not args.skip_large and only in (None, "whisper_large_v2"):
-                whisper_golden(ref_h, manifest, C.WHISPER_LARGE_V2, "whisper_large_v2", 1, 11, [3.0])
+                whisper_golden(ref_h, manifest, C.WHISPER_LARGE_V2_DEC, "whisper_large_v2", 1, 11, [3.0])
         finally:
             os.chdir(cwd)
     old = {}

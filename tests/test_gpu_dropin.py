@@ -74,25 +74,41 @@ def test_normalizing_feature_extractor(wavlm_sd, wavlm_clips, golden_wavlm):
 
 
 def test_extract_whisper_embeddings_fixed_files(tmp_path, golden_manifest):
+    """Encoder AND decoder embeddings through the drop-in glue and through the reference's own
+    generic route (processor -> model.encoder -> model.decoder), against the reference fixture."""
     from ssr_amd import config as C, synth
     from ssr_amd.extract import extract_whisper_embeddings_fixed
     from ssr_amd.hf import WhisperModel, WhisperProcessor
     g = np.load(os.path.join(GOLDEN, "whisper_tiny.npz"))
-    model = WhisperModel.from_state_dict(C.WHISPER_TINY, synth.synth_whisper_state_dict(C.WHISPER_TINY, seed=11),
+    model = WhisperModel.from_state_dict(C.WHISPER_TINY_DEC,
+                                         synth.synth_whisper_state_dict(C.WHISPER_TINY_DEC, seed=11),
                                          device="cuda:0", dtype="fp32")
     proc = WhisperProcessor(feature_size=80, device="cuda:0")
     enc = [int(i) for i in g["layer_indices"]]
+    dec = [int(i) for i in g["decoder_indices"]]
     clip = synth.synth_clips(1, 48000, seed=4321, first_clip=0)[0]
     p = str(tmp_path / "w.wav")
     write_wav(p, clip, fmt="float")
-    d = extract_whisper_embeddings_fixed(p, model, proc, "cuda:0", enc, [2, 1, 0])
-    assert list(d) == [f"encoder_layer_{i}" for i in enc]        # decoder part: §8(f) next-1
+    d = extract_whisper_embeddings_fixed(p, model, proc, "cuda:0", enc, dec)
+    assert list(d) == [f"encoder_layer_{i}" for i in enc] + [f"decoder_layer_{i}" for i in dec]
     for j, k in enumerate(enc):
         assert _rel(d[f"encoder_layer_{k}"], g["emb"][0, j]) <= 1e-4
-    # generic HF route through the processor + model.encoder
+    for j, k in enumerate(dec):
+        assert d[f"decoder_layer_{k}"].shape == (384,)
+        assert _rel(d[f"decoder_layer_{k}"], g["dec_emb"][0, j]) <= 1e-4
+    # out-of-range indices are skipped (REF :274-297 logs a warning and moves on)
+    d2 = extract_whisper_embeddings_fixed(p, model, proc, "cuda:0", [enc[0], 99], [dec[0], 99])
+    assert list(d2) == [f"encoder_layer_{enc[0]}", f"decoder_layer_{dec[0]}"]
+    # generic HF route through the processor + model.encoder + model.decoder (REF :242-262)
     feats = proc(clip, sampling_rate=16000, return_tensors="pt").input_features.to("cuda:0")
     out = model.encoder(feats, output_hidden_states=True, return_dict=True)
     v = torch.mean(out.hidden_states[enc[0]], dim=1).cpu().numpy().flatten()
     assert _rel(v, g["emb"][0, 0]) <= 1e-4
+    do = model.decoder(input_ids=torch.zeros((1, 1), dtype=torch.long).to("cuda:0"),
+                       encoder_hidden_states=out.last_hidden_state, output_hidden_states=True, return_dict=True)
+    assert len(do.hidden_states) == C.WHISPER_TINY_DEC.decoder_layers + 1
+    for j, k in enumerate(dec):
+        u = do.hidden_states[k].squeeze(1).cpu().numpy().flatten()
+        assert _rel(u, g["dec_emb"][0, j]) <= 1e-4
     with pytest.raises(NotImplementedError):
-        model.decoder(input_ids=torch.zeros((1, 1), dtype=torch.long))
+        model.decoder(input_ids=torch.ones((1, 1), dtype=torch.long), encoder_hidden_states=out.last_hidden_state)

@@ -3,7 +3,8 @@ reference's own outputs (golden fixtures from
 REF/whisper_embeddings_large.py:extract_whisper_embeddings_fixed) and the numpy oracle.
 
 Tolerances: log-mel max abs error <= 2e-4 (values are O(1)); fp32 encoder pooled rel-L2 <= 1e-4;
-bf16 encoder pooled rel-L2 <= 3e-2, cosine >= 0.999.
+bf16 encoder pooled rel-L2 <= 3e-2, cosine >= 0.999.  The 1-token decoder pass (SURVEY §8(f)
+next-1): fp32 rel-L2 <= 1e-4, bf16 <= 3e-2 against the reference's decoder_layer_* outputs.
 """
 import os
 
@@ -83,6 +84,59 @@ def test_whisper_tiny_from_mel(tiny):
     assert _rel(pooled, g["emb"]).max() <= 1e-4
 
 
+@pytest.mark.parametrize("dtype,tol", [("fp32", 1e-4), ("bf16", 3e-2)])
+def test_whisper_tiny_decoder_embed(tiny, dtype, tol):
+    """sse_whisper_embed: encoder time-means + decoder states in one call, batched (B=2 copies of
+    each clip, so batch rows must agree) vs the reference fixture."""
+    from ssr_amd import config as C, synth
+    from ssr_amd.model import SSEModel
+    g, clips = tiny
+    m = SSEModel(C.WHISPER_TINY_DEC, synth.synth_whisper_state_dict(C.WHISPER_TINY_DEC, seed=11),
+                 device="cuda:0", dtype=dtype)
+    enc = [int(i) for i in g["layer_indices"]]
+    dec = [int(i) for i in g["decoder_indices"]]
+    for i, c in enumerate(clips):
+        w = torch.from_numpy(np.stack([c, c])).cuda()
+        e, d = m.whisper_embed(w, enc, dec)
+        e, d = e.cpu().numpy(), d.cpu().numpy()
+        assert np.array_equal(e[0], e[1]) and np.array_equal(d[0], d[1])
+        re, rd = _rel(e[0], g["emb"][i]).max(), _rel(d[0], g["dec_emb"][i]).max()
+        print(dtype, "whisper-tiny enc rel", re, "dec rel", rd)
+        assert re <= tol and rd <= tol
+    # decoder-only call (sse_whisper_decoder_hidden_states) from an fp32 encoder state vs the oracle
+    from oracle.whisper import WhisperOracle
+    o = WhisperOracle(C.WHISPER_TINY_DEC, synth.synth_whisper_state_dict(C.WHISPER_TINY_DEC, seed=11))
+    rng = np.random.default_rng(5)
+    encs = rng.standard_normal((3, 1500, 384)).astype(np.float32)
+    hs = m.decoder_hidden_states(torch.from_numpy(encs).cuda())
+    assert len(hs) == C.WHISPER_TINY_DEC.decoder_layers + 1 and tuple(hs[0].shape) == (3, 1, 384)
+    for b in range(3):
+        ref = np.stack(o.decoder_hidden_states(encs[b]))
+        got = np.stack([h[b, 0].cpu().numpy() for h in hs])
+        assert _rel(got, ref).max() <= tol
+
+
+def test_whisper_decoder_edge_cases():
+    """Invalid ids, encoder-only model asked for decoder states, and a larger ragged batch."""
+    from ssr_amd import config as C, synth
+    from ssr_amd._lib import SSEError
+    from ssr_amd.model import SSEModel
+    m = SSEModel(C.WHISPER_TINY_DEC, synth.synth_whisper_state_dict(C.WHISPER_TINY_DEC, seed=11),
+                 device="cuda:0", dtype="bf16")
+    w = torch.from_numpy(synth.synth_clips(5, 24000, seed=3)).cuda()
+    with pytest.raises(SSEError):
+        m.whisper_embed(w, [0], [C.WHISPER_TINY_DEC.decoder_layers + 1])
+    e, d = m.whisper_embed(w, [], [0, 4])
+    assert e.shape == (5, 0, 384) and d.shape == (5, 2, 384)
+    # row 0 of the decoder input (hidden_states[0]) is the same embedding for every clip
+    assert torch.equal(d[:, 0], d[:1, 0].expand(5, -1))
+    e2, d2 = m.whisper_embed(w[2:3], [4], [4])
+    assert _rel(d2[0, 0].cpu().numpy(), d[2, 1].cpu().numpy()) <= 2e-2
+    enc_only = SSEModel(C.WHISPER_TINY, synth.synth_whisper_state_dict(C.WHISPER_TINY, seed=11), device="cuda:0")
+    with pytest.raises(ValueError):
+        enc_only.whisper_embed(w, [4], [1])
+
+
 @pytest.mark.slow
 def test_whisper_large_v2_embed():
     p = os.path.join(GOLDEN, "whisper_large_v2.npz")
@@ -100,4 +154,16 @@ def test_whisper_large_v2_embed():
         rel = _rel(got, g["emb"][0])
         print(dtype, "whisper-large-v2 rel", rel.max())
         assert rel.max() <= tol
+        del m
+    if "dec_emb" not in g:
+        return
+    sd = synth.synth_whisper_state_dict(C.WHISPER_LARGE_V2_DEC, seed=11)
+    dec = [int(i) for i in g["decoder_indices"]]
+    for dtype, tol in (("fp32", 1e-4), ("bf16", 3e-2)):
+        m = SSEModel(C.WHISPER_LARGE_V2_DEC, sd, device="cuda:0", dtype=dtype)
+        e, d = m.whisper_embed(torch.from_numpy(clip).cuda(), idx, dec)
+        re = _rel(e.cpu().numpy()[0], g["emb"][0]).max()
+        rd = _rel(d.cpu().numpy()[0], g["dec_emb"][0]).max()
+        print(dtype, "whisper-large-v2+decoder enc rel", re, "dec rel", rd)
+        assert re <= tol and rd <= tol
         del m

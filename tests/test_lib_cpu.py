@@ -29,7 +29,8 @@ def test_library_exports_every_header_symbol():
 def test_weight_floats_match_param_specs():
     from ssr_amd import _lib, config as C
     L = _lib.lib()
-    for spec in (C.WAVLM_BASE, C.WAVLM_LARGE, C.WHISPER_TINY, C.WHISPER_LARGE_V2):
+    for spec in (C.WAVLM_BASE, C.WAVLM_LARGE, C.WHISPER_TINY, C.WHISPER_LARGE_V2, C.WHISPER_TINY_DEC,
+                 C.WHISPER_LARGE_V2_DEC):
         cfg = _lib.make_cfg(spec)
         assert L.sse_weight_floats(ctypes.byref(cfg)) == C.weight_floats(spec), spec.name
 

@@ -102,3 +102,26 @@ def test_wavlm_large_oracle_vs_reference(golden_manifest):
     assert np.linalg.norm(fe - g["frontend_clip0"]) / np.linalg.norm(g["frontend_clip0"]) <= ORACLE_TOL
     got = o.embed(clips[:2], [int(i) for i in g["layer_indices"]], do_normalize=True)
     assert _rel(got, g["emb"][:2]).max() <= ORACLE_TOL
+
+
+def test_whisper_decoder_oracle_vs_reference(golden_manifest):
+    """1-token decoder pass: decoder_layer_* embeddings of
+    REF/whisper_embeddings_large.py:283-297 with the pinned synthetic decoder weights."""
+    from oracle.whisper import WhisperOracle
+    from ssr_amd import config as C, synth
+    g = np.load(os.path.join(GOLDEN, "whisper_tiny.npz"))
+    man = golden_manifest["whisper_tiny"]
+    sd = synth.synth_whisper_state_dict(C.WHISPER_TINY_DEC, seed=11)
+    h = hashlib.sha256()
+    for k in sorted(sd):
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(sd[k]).tobytes())
+    assert h.hexdigest() == man["decoder_weights_sha256"]
+    clips = [synth.synth_clips(1, int(16000 * d), seed=4321, first_clip=i)[0] for i, d in enumerate(man["durations_s"])]
+    o = WhisperOracle(C.WHISPER_TINY_DEC, sd)
+    enc_idx = [int(i) for i in g["layer_indices"]]
+    dec_idx = [int(i) for i in g["decoder_indices"]]
+    for i, c in enumerate(clips):
+        enc, dec = o.embed_both(c[None], enc_idx, dec_idx)
+        assert _rel(enc[0], g["emb"][i]).max() <= ORACLE_TOL
+        assert _rel(dec[0], g["dec_emb"][i]).max() <= ORACLE_TOL

@@ -63,3 +63,18 @@ def test_frames_match_hf():
     assert C.WAVLM_BASE.default_layer_indices() == [12, 11, 10, 6]
     assert C.WAVLM_LARGE.default_layer_indices() == [24, 23, 22, 12]
     assert C.WHISPER_LARGE_V2.default_layer_indices() == [32, 31, 30]
+
+
+def test_whisper_decoder_compact_and_hf_tables_pack_identically():
+    """The compact "[0]"-row decoder dict and the HF-loadable full tables pack to the same blob."""
+    from ssr_amd import config as C, synth
+    from ssr_amd.model import pack_weights
+    sd = synth.synth_whisper_state_dict(C.WHISPER_TINY_DEC)
+    full = synth.synth_whisper_state_dict(C.WHISPER_TINY_DEC, full_hf=True)
+    assert full["decoder.embed_tokens.weight"].shape == (51865, 384)
+    assert np.array_equal(full["decoder.embed_tokens.weight"][0], sd["decoder.embed_tokens.weight[0]"])
+    a, b = pack_weights(C.WHISPER_TINY_DEC, sd), pack_weights(C.WHISPER_TINY_DEC, full)
+    assert a.size == C.weight_floats(C.WHISPER_TINY_DEC) and np.array_equal(a, b)
+    # the encoder part of the blob is unchanged by adding the decoder
+    enc = pack_weights(C.WHISPER_TINY, synth.synth_whisper_state_dict(C.WHISPER_TINY))
+    assert np.array_equal(a[:enc.size], enc)
