@@ -323,15 +323,17 @@ int launch_any(const GemmArgs& a, int amode, int groups, hipStream_t s) {
   constexpr int E = 16 / (int)sizeof(T);
   if (a.M <= 0 || a.N <= 0 || a.K <= 0 || a.K % E) return -3;
   if (amode == AMODE_CONV && (a.cin % E)) return -3;
-  // default: 128x128 tile, 4 waves of 64x64, 2-stage LDS (2 blocks/CU overlap one block's
-  // epilogue with the other's MFMA loop: measured 656 vs 637 TF/s on the WavLM-base step).
-  // SSE_GEMM_CFG=2 selects the 256x128, 8-wave, 3-stage ring (144 KiB, 1 block/CU) for A/B runs.
-  const char* fe = getenv("SSE_GEMM_CFG");     // read per launch so one process can A/B configs
+  // bf16 default for the big encoder GEMMs: 256x256 tile, 8 waves (2x4) of 128x64, 2-stage
+  // 128 KiB LDS ring (1 block/CU).  Measured on the WavLM-base B=256 shapes vs the 128x128 tile:
+  // qkv 837 vs 636, ffn1 691 vs 605, ffn2 931 vs 801, oproj 510 vs 489 TF/s (profiles/r1_gemm_configs.json).
+  // Otherwise 128x128, 4 waves of 64x64, 2 stages (2 blocks/CU).  SSE_GEMM_CFG (read per
+  // launch, so one process can A/B): 1 = never 256x256, 2 = 256x128 3-stage ring.
+  const char* fe = getenv("SSE_GEMM_CFG");
   const int force = fe ? atoi(fe) : 0;
   if (a.N % 128 == 0 && a.M >= 2048 && force == 2) return launch_cfg<T, 256, 128, 4, 2, 3>(a, amode, groups, s);
   if constexpr (sizeof(T) == 2) {
-    // SSE_GEMM_CFG=3: 256x256 tile, 8 waves (2x4) of 128x64, 2-stage 128 KiB ring (1 block/CU)
-    if (a.N % 256 == 0 && a.M >= 4096 && force == 3) return launch_cfg<T, 256, 256, 2, 4, 2>(a, amode, groups, s);
+    if (a.N % 256 == 0 && a.M >= 4096 && (force == 0 || force == 3))
+      return launch_cfg<T, 256, 256, 2, 4, 2>(a, amode, groups, s);
   }
   if (a.N % 128 == 0) return launch_cfg<T, 128, 128, 2, 2, 2>(a, amode, groups, s);
   if (a.N % 64 == 0) return launch_cfg<T, 128, 64, 4, 1, 2>(a, amode, groups, s);

@@ -116,7 +116,8 @@ struct sse_model {
   size_t c1_w, c1_b, c2_w, c2_b, positions;
   size_t dec_x0, dec_ln_w, dec_ln_b;   // decoder: embed_tokens[0] + embed_positions[0]; final LN
   std::vector<DecLayerW> dec;
-  int ldq = 0;   // QKV GEMM width: 3H (+ 8*heads gate columns for WavLM), padded to 128
+  int ldq = 0;   // QKV GEMM width: 3H (+ 8*heads gate columns for WavLM, then zero pad to 256 so the
+                // 256x256 MFMA tile applies)
   std::vector<LayerW> layers;
   // live per-launch timing (sse_profile_*): events pre-created outside any capture
   struct Prof {
@@ -229,7 +230,7 @@ int build_wavlm(sse_model* m, Blob& bl, Arena& ar) {
     LayerW L{};
     // rows [q | k | v | gate: head h, output o at 3H + 8h + o, block-diagonal over the
     // head's 64 input channels (gru_rel_pos_linear, HF :158-163) | zero pad to ldq]
-    const int ldq = ((3 * H + 8 * nh + 127) / 128) * 128;
+    const int ldq = ((3 * H + 8 * nh + 255) / 256) * 256;
     m->ldq = ldq;
     std::vector<float> qkv((size_t)ldq * H, 0.f), qkvb((size_t)ldq, 0.f);
     std::memcpy(qkv.data(), qw, (size_t)H * H * 4);
@@ -446,7 +447,7 @@ WavlmWs wavlm_plan(const sse_model* m, int B, int L, Plan& p) {
   w.x = p.add(M * H * 4);
   w.xt = p.add(M * H * es);
   w.xb = p.add(M * (H > c.conv_dim[c.n_conv - 1] ? H : c.conv_dim[c.n_conv - 1]) * es);
-  w.qkv = p.add(M * (size_t)(((3 * H + 8 * c.heads + 127) / 128) * 128) * es);
+  w.qkv = p.add(M * (size_t)(((3 * H + 8 * c.heads + 255) / 256) * 256) * es);
   w.ctx = p.add(M * H * es);
   w.ff = p.add(M * (size_t)c.ffn * es);
   w.hf = c.stable_layer_norm ? p.add(M * H * 4) : 0;
@@ -600,7 +601,9 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     GemmArgs g{};
     g.A = xb; g.B = m->ptr(Lw.qkv_w); g.M = M; g.N = m->ldq; g.K = H;
     g.rows_per_seg = M; g.lda = H; g.bias = m->ptr<float>(Lw.qkv_b); g.Ct = qkv; g.ldc = m->ldq; g.zero = zero;
-    RC(prof(m, s, "gemm:qkv", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    // algorithmic FLOPs count the 3H + 8*heads useful columns, not the zero pad to ldq
+    RC(prof(m, s, "gemm:qkv", 2.0 * M * (3.0 * H + 8.0 * nh) * H, 0,
+            [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     AttnArgs a{};
     a.qkv = qkv; a.out = ctx; a.T = Tf; a.H = H; a.nh = nh; a.ldq = m->ldq; a.scale = 0.125f;
     a.gconst = m->ptr<float>(Lw.g_const); a.relb = m->ptr<float>(m->relb); a.maxd = MAXD;

@@ -19,7 +19,8 @@ def _ref(a, b, bias, resid, act):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M,N,K", [(1, 128, 64), (149, 768, 768), (1000, 512, 1536), (4099, 256, 3072),
-                                   (300, 64, 40), (77, 48, 96), (2048, 2432, 768)])
+                                   (300, 64, 40), (77, 48, 96), (2048, 2432, 768), (5000, 2560, 200),
+                                   (4096, 768, 3072)])
 @pytest.mark.parametrize("epi", ["plain", "bias_gelu", "bias_resid"])
 def test_gemm_vs_torch(dtype, M, N, K, epi):
     from ssr_amd.model import gemm
@@ -45,3 +46,23 @@ def test_gemm_rejects_bad_shapes():
     b = torch.randn(100, 30, device="cuda")      # N = 100: no tile config
     with pytest.raises(Exception):
         gemm(a, b)
+
+
+@pytest.mark.parametrize("M,N,K", [(4099, 512, 768), (8192, 768, 3072), (4100, 2560, 136)])
+def test_gemm_tile_configs_agree(monkeypatch, M, N, K):
+    """The 256x256 default, the 128x128 tile (SSE_GEMM_CFG=1) and the 256x128 3-stage ring
+    (SSE_GEMM_CFG=2) accumulate every output in the same K order: results are bit-identical."""
+    from ssr_amd.model import gemm
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    b = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    bias = torch.randn(N, device="cuda", generator=g)
+    resid = torch.randn(M, N, device="cuda", generator=g)
+    outs = []
+    for cfg in ("0", "1", "2"):
+        monkeypatch.setenv("SSE_GEMM_CFG", cfg)
+        outs.append(gemm(a, b, bias, resid, None))
+    ref = _ref(a, b, bias, resid, None)
+    for o in outs:
+        assert ((o - ref).norm() / ref.norm()).item() <= 1e-5
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
