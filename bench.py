@@ -189,7 +189,7 @@ def main():
             rf["device_ms_per_step_sum"] = round(sum(r[1] for r in records) / a.steps, 3)
             res["roofline"] = rf
         res["model_flops_frac"] = round(value / world * FLOP_PER_CLIP[a.model] / 1e12 / PEAK_TFLOPS[a.dtype], 4)
-        ncpu = a.cpu_sample if a.cpu_sample is not None else (8 if wavlm else 1)
+        ncpu = a.cpu_sample if a.cpu_sample is not None else (48 if wavlm else 2)   # ~10-30 s of CPU work
         if world == 1 and ncpu > 0:
             res["cpu_baseline"] = cpu_baseline(a.model, ncpu, secs)
         print(json.dumps(res), flush=True)

@@ -6,6 +6,7 @@
 typedef __bf16 bf16;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 #define SSE_DEV __device__ __forceinline__
@@ -35,6 +36,31 @@ SSE_DEV float gelu_erf(float x) {
   const float erfc = t * __expf(fmaf(-z, z, p));
   const float h = 0.5f * x * erfc;
   return x >= 0.f ? x - h : h;
+}
+
+// Same evaluation on a channel pair with packed fp32 math (v_pk_fma_f32 / v_pk_mul_f32): the
+// polynomial runs at 2 results per instruction, only v_rcp / v_exp stay scalar.  Each lane is
+// the identical IEEE fma chain as gelu_erf, so results are bit-identical to the scalar form.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+SSE_DEV f32x2 gelu_erf2(f32x2 x) {
+  const f32x2 z = __builtin_elementwise_abs(x) * 0.70710678118654752f;
+  const f32x2 d = __builtin_elementwise_fma(f32x2{0.5f, 0.5f}, z, f32x2{1.0f, 1.0f});
+  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 p = {0.17087277f, 0.17087277f};
+  p = __builtin_elementwise_fma(p, t, f32x2{-0.82215223f, -0.82215223f});
+  p = __builtin_elementwise_fma(p, t, f32x2{1.48851587f, 1.48851587f});
+  p = __builtin_elementwise_fma(p, t, f32x2{-1.13520398f, -1.13520398f});
+  p = __builtin_elementwise_fma(p, t, f32x2{0.27886807f, 0.27886807f});
+  p = __builtin_elementwise_fma(p, t, f32x2{-0.18628806f, -0.18628806f});
+  p = __builtin_elementwise_fma(p, t, f32x2{0.09678418f, 0.09678418f});
+  p = __builtin_elementwise_fma(p, t, f32x2{0.37409196f, 0.37409196f});
+  p = __builtin_elementwise_fma(p, t, f32x2{1.00002368f, 1.00002368f});
+  p = __builtin_elementwise_fma(p, t, f32x2{-1.26551223f, -1.26551223f});
+  const f32x2 e = __builtin_elementwise_fma(-z, z, p);
+  const f32x2 erfc = t * f32x2{__expf(e.x), __expf(e.y)};
+  const f32x2 h = 0.5f * x * erfc;
+  const f32x2 pos = x - h;
+  return f32x2{x.x >= 0.f ? pos.x : h.x, x.y >= 0.f ? pos.y : h.y};
 }
 
 template <typename T> SSE_DEV T from_f32(float v);

@@ -122,7 +122,7 @@ __global__ void gn_finalize_kernel(const double* __restrict__ mom, int B, int C,
 }
 
 template <typename TO, bool RAW>
-__global__ __launch_bounds__(512) void conv0_apply_kernel(const float* __restrict__ x, int L,
+__global__ __launch_bounds__(256) void conv0_apply_kernel(const float* __restrict__ x, int L,
                                                           const float* __restrict__ norm,
                                                           const float* __restrict__ w0, const float* __restrict__ b0,
                                                           int C, int T0, const float2* __restrict__ ss,
@@ -138,22 +138,36 @@ __global__ __launch_bounds__(512) void conv0_apply_kernel(const float* __restric
   if (norm) { mu = norm[2 * b]; rs = norm[2 * b + 1]; }
   for (int i = threadIdx.x; i < nx; i += blockDim.x) xs[i] = norm ? (xb[i] - mu) * rs : xb[i];
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float w[K0];
+  // one channel PAIR per thread: both channels read the same sample window, so the 10-tap FMA,
+  // the GroupNorm affine and GELU run as packed fp32 (2 results per VALU op) and the store is 2
+  // adjacent outputs.  C is even (host-checked).
+  for (int c = 2 * threadIdx.x; c < C; c += 2 * blockDim.x) {
+    f32x2 w[K0];
     #pragma unroll
-    for (int j = 0; j < K0; ++j) w[j] = w0[c * K0 + j];
-    const float bias = b0 ? b0[c] : 0.f;
-    const float2 sc = RAW ? make_float2(1.f, 0.f) : ss[(long long)b * C + c];
+    for (int j = 0; j < K0; ++j) w[j] = f32x2{w0[c * K0 + j], w0[(c + 1) * K0 + j]};
+    const f32x2 bias = b0 ? f32x2{b0[c], b0[c + 1]} : f32x2{0.f, 0.f};
+    f32x2 sc = {1.f, 1.f}, sh = {0.f, 0.f};
+    if (!RAW) {
+      const float2 s0v = ss[(long long)b * C + c], s1v = ss[(long long)b * C + c + 1];
+      sc = f32x2{s0v.x, s1v.x};
+      sh = f32x2{s0v.y, s1v.y};
+    }
     TO* ob = out + ((long long)b * T0 + t0) * C + c;
     // sliding window: frame t+1 reuses samples 5..9 of frame t, so 5 new LDS reads per frame
     float win[K0];
     #pragma unroll
     for (int j = 0; j < K0; ++j) win[j] = xs[j];
     for (int t = 0; t < nt; ++t) {
-      float y = bias;
+      f32x2 y = bias;
       #pragma unroll
-      for (int j = 0; j < K0; ++j) y = fmaf(w[j], win[j], y);
-      ob[(long long)t * C] = from_f32<TO>(RAW ? y : gelu_erf(fmaf(y, sc.x, sc.y)));
+      for (int j = 0; j < K0; ++j) y = __builtin_elementwise_fma(w[j], f32x2{win[j], win[j]}, y);
+      if (!RAW) y = gelu_erf2(__builtin_elementwise_fma(y, sc, sh));
+      if constexpr (sizeof(TO) == 2) {
+        const bf16x2 o2 = {(bf16)y.x, (bf16)y.y};
+        *(bf16x2*)(ob + (long long)t * C) = o2;
+      } else {
+        *(f32x2*)((float*)ob + (long long)t * C) = y;
+      }
       #pragma unroll
       for (int j = 0; j < K0 - S0; ++j) win[j] = win[j + S0];
       if (t + 1 < nt) {
@@ -174,7 +188,8 @@ int launch_conv0_gn(const float* x, int B, int L, const float* norm, const float
   hipLaunchKernelGGL(conv0_moments_kernel, dim3(B), dim3(256), 0, s, x, L, norm, s0, T0, mom);
   hipLaunchKernelGGL(gn_finalize_kernel, dim3((B * C + 255) / 256), dim3(256), 0, s, mom, B, C, T0, w0, b0, gamma,
                      beta, eps, ss);
-  dim3 grid((T0 + C0_T - 1) / C0_T, B), block(C < 512 ? C : 512);
+  if (C % 2) return -3;
+  dim3 grid((T0 + C0_T - 1) / C0_T, B), block(C / 2 < 256 ? C / 2 : 256);
   hipLaunchKernelGGL((conv0_apply_kernel<TO, false>), grid, block, 0, s, x, L, norm, w0, b0, C, T0, ss, out);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
@@ -184,7 +199,8 @@ template <typename TO>
 int launch_conv0_raw(const float* x, int B, int L, const float* norm, const float* w0, const float* b0, int C,
                      int k0, int s0, int T0, TO* out, hipStream_t s) {
   if (k0 != K0 || s0 != 5) return -3;
-  dim3 grid((T0 + C0_T - 1) / C0_T, B), block(C < 512 ? C : 512);
+  if (C % 2) return -3;
+  dim3 grid((T0 + C0_T - 1) / C0_T, B), block(C / 2 < 256 ? C / 2 : 256);
   hipLaunchKernelGGL((conv0_apply_kernel<TO, true>), grid, block, 0, s, x, L, norm, w0, b0, C, T0,
                      (const float2*)nullptr, out);
   return hipGetLastError() == hipSuccess ? 0 : -2;
@@ -328,6 +344,13 @@ SSE_DEV float wavlm_gate(const TE* rp, float c) {
     for (int o = 0; o < 4; ++o) { v[o] = r0[o]; v[4 + o] = r1[o]; }
   }
   const float ra = v[0] + v[1] + v[2] + v[3], rb = v[4] + v[5] + v[6] + v[7];
+  const float ga = 1.f / (1.f + expf(-ra)), gb = 1.f / (1.f + expf(-rb));
+  return ga * (gb * c - 1.0f) + 2.0f;
+}
+
+SSE_DEV float wavlm_gate_v(const bf16x8& r, float c) {
+  const float ra = (float)r[0] + (float)r[1] + (float)r[2] + (float)r[3];
+  const float rb = (float)r[4] + (float)r[5] + (float)r[6] + (float)r[7];
   const float ga = 1.f / (1.f + expf(-ra)), gb = 1.f / (1.f + expf(-rb));
   return ga * (gb * c - 1.0f) + 2.0f;
 }
@@ -713,13 +736,18 @@ __global__ __launch_bounds__(256) void attention_flash2_kernel(AttnArgs a) {
   }
 }
 
-template <typename TE, bool BIAS, int NKB>
-__global__ __launch_bounds__(512) void attention_full_kernel(AttnArgs a) {
-  constexpr bool BF = sizeof(TE) == 2;
+// Short-sequence bf16 attention (T <= 160, WavLM 3 s clips: T = 149): one block per (head,
+// clip), one wave per 16-query block, the whole padded key row (NKB x 16 keys) in LDS.
+// Staging issues every global load of the block first (K: 2 chunks/thread, V: 4 rows for half
+// the threads, the gate's 8 projections, one relative-bias entry) and only then writes LDS, so
+// a block pays one HBM round trip before its MFMA work instead of one per loop trip.
+template <bool BIAS, int NKB>
+__global__ __launch_bounds__(640) void attention_full_kernel(AttnArgs a) {
   constexpr int TP = NKB * 16;                                   // padded keys
+  constexpr int NT = 64 * NKB;                                   // threads (one wave per query block)
   constexpr int SVD = ((TP / 2 + 15) / 16) * 16 + 4;             // V^T row stride in dwords (16k+4)
-  constexpr int KS_BYTES = BF ? TP * 128 : TP * 256;
-  constexpr int VS_BYTES = BF ? AT_HD * SVD * 4 : TP * VF_STRIDE * 4;
+  constexpr int KS_BYTES = TP * 128;
+  constexpr int VS_BYTES = AT_HD * SVD * 4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ks = smem;
   char* Vs = smem + KS_BYTES;
@@ -728,200 +756,158 @@ __global__ __launch_bounds__(512) void attention_full_kernel(AttnArgs a) {
 
   const int h = blockIdx.x, b = blockIdx.y;
   const int T = a.T, H = a.H, H3 = a.ldq;
-  const int tid = threadIdx.x, lane = tid & 63, nthr = blockDim.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), nwave = nthr >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
-  const TE* qkv = (const TE*)a.qkv + (long long)b * T * H3;
+  const bf16* qkv = (const bf16*)a.qkv + (long long)b * T * H3;
 
+  // ---- 1. issue all global loads ----
+  bf16x8 kreg[2], vreg[4], greg = bf16x8{};
+  float rbv = 0.f, gc = 0.f;
+  #pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = tid + u * NT, kr = i >> 3, ch = i & 7;
+    kreg[u] = kr < T ? *(const bf16x8*)(qkv + (long long)kr * H3 + H + h * AT_HD + ch * 8) : bf16x8{};
+  }
+  constexpr int VU = (TP / 4) * 8;                               // (8-dim chunk, 4-key group) units
+  const bool vth = tid < VU;
+  const int vch = tid / (TP / 4), vkg = tid - vch * (TP / 4);   // key group fastest: conflict-free
+  #pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int key = vkg * 4 + u;
+    vreg[u] = (vth && key < T) ? *(const bf16x8*)(qkv + (long long)key * H3 + 2 * H + h * AT_HD + vch * 8)
+                               : bf16x8{};
+  }
   if (BIAS) {
-    for (int t = tid; t < TP; t += nthr)
-      gate[t] = t < T ? wavlm_gate(qkv + (long long)t * a.ldq + 3 * H + 8 * h, a.gconst[h]) : 0.f;
-    const float* rh = a.relb + (long long)h * (2 * a.maxd + 1) + a.maxd;
-    for (int u = tid; u < 2 * TP - 1; u += nthr) {
-      int d = u - (TP - 1);
+    if (tid < T) greg = *(const bf16x8*)(qkv + (long long)tid * H3 + 3 * H + 8 * h);
+    gc = a.gconst[h];
+    if (tid < 2 * TP - 1) {
+      int d = tid - (TP - 1);
       d = d < -a.maxd ? -a.maxd : (d > a.maxd ? a.maxd : d);
-      rb[u] = rh[d];
+      rbv = a.relb[(long long)h * (2 * a.maxd + 1) + a.maxd + d];
     }
   }
-  // ---- stage K (swizzled rows) and V (transposed, 4 keys packed per 8-B write) ----
-  if constexpr (BF) {
-    for (int i = tid; i < TP * 8; i += nthr) {
-      const int kr = i >> 3, ch = i & 7;
-      bf16x8 kv = bf16x8{};
-      if (kr < T) kv = *(const bf16x8*)(qkv + (long long)kr * H3 + H + h * AT_HD + ch * 8);
-      *(bf16x8*)(Ks + kr * 128 + ((ch ^ ((kr >> 1) & 7)) * 16)) = kv;
+  // ---- 2. write LDS: K swizzled rows, V transposed (4 keys per 8-B write), gate, bias ----
+  #pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = tid + u * NT, kr = i >> 3, ch = i & 7;
+    *(bf16x8*)(Ks + kr * 128 + ((ch ^ ((kr >> 1) & 7)) * 16)) = kreg[u];
+  }
+  if (vth) {
+    #pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const bf16x4 pk = {vreg[0][e], vreg[1][e], vreg[2][e], vreg[3][e]};
+      *(bf16x4*)(Vs + (vch * 8 + e) * SVD * 4 + vkg * 8) = pk;
     }
-    for (int i = tid; i < (TP / 4) * 8; i += nthr) {      // (8-dim chunk, 4-key group): key group
-      const int ch = i / (TP / 4), kg = i - ch * (TP / 4);  // fastest, so a wave's 8-B writes are
-      bf16x8 v4[4];                                         // contiguous (conflict-free)
-      #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int key = kg * 4 + u;
-        v4[u] = key < T ? *(const bf16x8*)(qkv + (long long)key * H3 + 2 * H + h * AT_HD + ch * 8) : bf16x8{};
-      }
-      #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const bf16x4 pk = {v4[0][e], v4[1][e], v4[2][e], v4[3][e]};
-        *(bf16x4*)(Vs + (ch * 8 + e) * SVD * 4 + kg * 8) = pk;
-      }
-    }
-  } else {
-    for (int i = tid; i < TP * 16; i += nthr) {
-      const int kr = i >> 4, ch = i & 15;
-      f32x4 kv = f32x4{0.f, 0.f, 0.f, 0.f}, vv = kv;
-      if (kr < T) {
-        kv = *(const f32x4*)((const float*)(qkv + (long long)kr * H3 + H + h * AT_HD) + ch * 4);
-        vv = *(const f32x4*)((const float*)(qkv + (long long)kr * H3 + 2 * H + h * AT_HD) + ch * 4);
-      }
-      *(f32x4*)(Ks + kr * 256 + ((ch ^ (kr & 15)) * 16)) = kv;
-      *(f32x4*)((float*)Vs + kr * VF_STRIDE + ch * 4) = vv;
-    }
+  }
+  if (BIAS) {
+    if (tid < TP) gate[tid] = tid < T ? wavlm_gate_v(greg, gc) : 0.f;
+    if (tid < 2 * TP - 1) rb[tid] = rbv;
   }
   __syncthreads();
 
   const float LOG2E = 1.4426950408889634f;
-  const int nqb = (T + 15) / 16;
-  for (int qb = wave; qb < nqb; qb += nwave) {
-    const int qi = qb * 16 + r16;
-    const bool qv = qi < T;
-    const TE* qrow = qkv + (long long)(qv ? qi : 0) * H3 + h * AT_HD;
-    f32x4 s[NKB];
-    if constexpr (BF) {
-      bf16x8 qf[2];
+  const int qb = wave;
+  if (qb * 16 >= T) return;
+  const int qi = qb * 16 + r16;
+  const bool qv = qi < T;
+  const bf16* qrow = qkv + (long long)(qv ? qi : 0) * H3 + h * AT_HD;
+  f32x4 s[NKB];
+  {
+    bf16x8 qf[2];
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks) qf[ks] = qv ? *(const bf16x8*)(qrow + ks * 32 + g * 8) : bf16x8{};
+    #pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int kr = kb * 16 + r16;
       #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) qf[ks] = qv ? *(const bf16x8*)(qrow + ks * 32 + g * 8) : bf16x8{};
-      #pragma unroll
-      for (int kb = 0; kb < NKB; ++kb) {
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int kr = kb * 16 + r16;
-        #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          const bf16x8 kf = *(const bf16x8*)(Ks + kr * 128 + (((g + 4 * ks) ^ ((kr >> 1) & 7)) * 16));
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], acc, 0, 0, 0);
-        }
-        s[kb] = acc;
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 kf = *(const bf16x8*)(Ks + kr * 128 + (((g + 4 * ks) ^ ((kr >> 1) & 7)) * 16));
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], acc, 0, 0, 0);
       }
-    } else {
-      f32x4 qf[4];
-      #pragma unroll
-      for (int c = 0; c < 4; ++c)
-        qf[c] = qv ? *(const f32x4*)((const float*)qrow + (g + 4 * c) * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
-      #pragma unroll
-      for (int kb = 0; kb < NKB; ++kb) {
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int kr = kb * 16 + r16;
-        #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const f32x4 kf = *(const f32x4*)(Ks + kr * 256 + (((g + 4 * c) ^ (kr & 15)) * 16));
-          #pragma unroll
-          for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[e], qf[c][e], acc, 0, 0, 0);
-        }
-        s[kb] = acc;
-      }
+      s[kb] = acc;
     }
-    // exact softmax over the whole (padded) row: lane holds keys kb*16 + 4g + r
-    const float gq = BIAS ? gate[qb * 16 + r16] : 0.f;
-    float mx = -INFINITY;
+  }
+  // exact softmax over the whole (padded) row: lane holds keys kb*16 + 4g + r
+  const float gq = BIAS ? gate[qb * 16 + r16] : 0.f;
+  float mx = -INFINITY;
+  #pragma unroll
+  for (int kb = 0; kb < NKB; ++kb)
     #pragma unroll
-    for (int kb = 0; kb < NKB; ++kb)
-      #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kb * 16 + 4 * g + r;
-        float v = s[kb][r] * a.scale;
-        if (BIAS) v = fmaf(gq, rb[key - qi + (TP - 1)], v);
-        v = key < T ? v : -INFINITY;
-        s[kb][r] = v;
-        mx = fmaxf(mx, v);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mb = mx * LOG2E;
-    float l = 0.f;
-    #pragma unroll
-    for (int kb = 0; kb < NKB; ++kb)
-      #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(fmaf(s[kb][r], LOG2E, -mb));
-        s[kb][r] = p;
-        l += p;
-      }
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    // O^T = V^T . P^T
-    f32x4 o[4];
-    #pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (BF) {
-      #pragma unroll
-      for (int ks = 0; ks < NKB / 2; ++ks) {
-        bf16x8 pf;
-        #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          pf[r] = (bf16)s[2 * ks][r];
-          pf[4 + r] = (bf16)s[2 * ks + 1][r];
-        }
-        #pragma unroll
-        for (int db = 0; db < 4; ++db) {
-          const char* vrow = Vs + (db * 16 + r16) * SVD * 4 + (ks * 32 + 4 * g) * 2;
-          const bf16x4 v0 = *(const bf16x4*)(vrow);
-          const bf16x4 v1 = *(const bf16x4*)(vrow + 32);
-          const bf16x8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-          o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[db], 0, 0, 0);
-        }
-      }
-    } else {
-      const float* vs = (const float*)Vs;
-      #pragma unroll
-      for (int kb = 0; kb < NKB; ++kb)
-        #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float* vrow = vs + (kb * 16 + 4 * g + r) * VF_STRIDE + r16;
-          #pragma unroll
-          for (int db = 0; db < 4; ++db)
-            o[db] = __builtin_amdgcn_mfma_f32_16x16x4f32(vrow[db * 16], s[kb][r], o[db], 0, 0, 0);
-        }
+    for (int r = 0; r < 4; ++r) {
+      const int key = kb * 16 + 4 * g + r;
+      float v = s[kb][r] * a.scale;
+      if (BIAS) v = fmaf(gq, rb[key - qi + (TP - 1)], v);
+      v = key < T ? v : -INFINITY;
+      s[kb][r] = v;
+      mx = fmaxf(mx, v);
     }
-    if (qv) {
-      const float inv = 1.0f / l;
-      TE* orow = (TE*)a.out + ((long long)b * T + qi) * H + h * AT_HD;
-      #pragma unroll
-      for (int db = 0; db < 4; ++db) {
-        if constexpr (BF) {
-          bf16x4 ov = {(bf16)(o[db][0] * inv), (bf16)(o[db][1] * inv), (bf16)(o[db][2] * inv),
-                       (bf16)(o[db][3] * inv)};
-          *(bf16x4*)(orow + db * 16 + 4 * g) = ov;
-        } else {
-          *(f32x4*)((float*)orow + db * 16 + 4 * g) = o[db] * inv;
-        }
-      }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  const float mb = mx * LOG2E;
+  float l = 0.f;
+  #pragma unroll
+  for (int kb = 0; kb < NKB; ++kb)
+    #pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float p = exp2f(fmaf(s[kb][r], LOG2E, -mb));
+      s[kb][r] = p;
+      l += p;
+    }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  // O^T = V^T . P^T
+  f32x4 o[4];
+  #pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+  for (int ks = 0; ks < NKB / 2; ++ks) {
+    bf16x8 pf;
+    #pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      pf[r] = (bf16)s[2 * ks][r];
+      pf[4 + r] = (bf16)s[2 * ks + 1][r];
+    }
+    #pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const char* vrow = Vs + (db * 16 + r16) * SVD * 4 + (ks * 32 + 4 * g) * 2;
+      const bf16x4 v0 = *(const bf16x4*)(vrow);
+      const bf16x4 v1 = *(const bf16x4*)(vrow + 32);
+      const bf16x8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[db], 0, 0, 0);
+    }
+  }
+  if (qv) {
+    const float inv = 1.0f / l;
+    bf16* orow = (bf16*)a.out + ((long long)b * T + qi) * H + h * AT_HD;
+    #pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      bf16x4 ov = {(bf16)(o[db][0] * inv), (bf16)(o[db][1] * inv), (bf16)(o[db][2] * inv),
+                   (bf16)(o[db][3] * inv)};
+      *(bf16x4*)(orow + db * 16 + 4 * g) = ov;
     }
   }
 }
 
-template <typename TE, bool BIAS, int NKB>
+template <bool BIAS, int NKB>
 int launch_attention_full(const AttnArgs& a, int B, hipStream_t s) {
-  constexpr bool BF = sizeof(TE) == 2;
   constexpr int TP = NKB * 16;
   constexpr int SVD = ((TP / 2 + 15) / 16) * 16 + 4;
-  constexpr int KS_BYTES = BF ? TP * 128 : TP * 256;
-  constexpr int VS_BYTES = BF ? AT_HD * SVD * 4 : TP * VF_STRIDE * 4;
-  const size_t lds = KS_BYTES + VS_BYTES + (size_t)TP * 4 + (size_t)2 * TP * 4;
-  const int nqb = (a.T + 15) / 16;
-  const int per = (nqb + 7) / 8;                          // query blocks per wave
-  const int nwave = (nqb + per - 1) / per;
-  hipLaunchKernelGGL((attention_full_kernel<TE, BIAS, NKB>), dim3(a.nh, B), dim3(64 * nwave), lds, s, a);
+  const size_t lds = (size_t)TP * 128 + (size_t)AT_HD * SVD * 4 + (size_t)TP * 4 + (size_t)2 * TP * 4;
+  hipLaunchKernelGGL((attention_full_kernel<BIAS, NKB>), dim3(a.nh, B), dim3(64 * NKB), lds, s, a);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-template <typename TE, bool BIAS>
+template <bool BIAS>
 int dispatch_full(const AttnArgs& a, int B, hipStream_t s) {
   const int nkb = ((a.T + 31) / 32) * 2;
   switch (nkb) {
-    case 2: return launch_attention_full<TE, BIAS, 2>(a, B, s);
-    case 4: return launch_attention_full<TE, BIAS, 4>(a, B, s);
-    case 6: return launch_attention_full<TE, BIAS, 6>(a, B, s);
-    case 8: return launch_attention_full<TE, BIAS, 8>(a, B, s);
-    case 10: return launch_attention_full<TE, BIAS, 10>(a, B, s);
+    case 2: return launch_attention_full<BIAS, 2>(a, B, s);
+    case 4: return launch_attention_full<BIAS, 4>(a, B, s);
+    case 6: return launch_attention_full<BIAS, 6>(a, B, s);
+    case 8: return launch_attention_full<BIAS, 8>(a, B, s);
+    case 10: return launch_attention_full<BIAS, 10>(a, B, s);
     default: return -3;
   }
 }
@@ -937,8 +923,8 @@ int launch_attention(const AttnArgs& a, int B, hipStream_t s) {
   if (a.relb) lds += (size_t)(2 * nkt * AT_K) * 4;
   if (lds > 160 * 1024) return -3;
   if constexpr (BF) {   // fp32 (parity) path keeps the flash kernel: its full-row form spills
-    if (a.T <= 160 && a.relb) return dispatch_full<T, true>(a, B, s);   // <= 10 key blocks: no spills
-    if (a.T <= 160) return dispatch_full<T, false>(a, B, s);
+    if (a.T <= 160 && a.relb) return dispatch_full<true>(a, B, s);   // <= 10 key blocks: no spills
+    if (a.T <= 160) return dispatch_full<false>(a, B, s);
     const int Tk = ((a.T + F2_K - 1) / F2_K) * F2_K;
     const size_t lds2 = 2 * F2_BUF + F2_Q * 4 + (a.relb ? (size_t)2 * Tk * 4 : 0);
     if (lds2 > 160 * 1024) return -3;

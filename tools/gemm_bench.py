@@ -31,4 +31,20 @@ for cfg, (name, (M, N, K, epi)) in [(c, kv) for kv in SHAPES.items() for c in cf
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / n
     res[f"{name}@{cfg}"] = {"ms": round(ms, 4), "tflops": round(2 * M * N * K / ms / 1e9, 1)}
+# vendor library on the same shapes for scale (torch bf16 matmul -> hipBLASLt; plain GEMM only)
+for name, (M, N, K, epi) in SHAPES.items():
+    if name == "qkv":
+        N = 2560
+    a = torch.randn(M, K, device="cuda").bfloat16()
+    b = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    for _ in range(3):
+        a @ b.T
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        a @ b.T
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 20
+    res[f"{name}@torch"] = {"ms": round(ms, 4), "tflops": round(2 * M * N * K / ms / 1e9, 1)}
 print(json.dumps(res))
