@@ -279,13 +279,12 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
       }
       #pragma unroll
       for (int u = 0; u < UNR; ++u) {
-        f32x4 o;
-        #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float x = v[u][e] + bv[u][e];
-          if (gelu) x = gelu_erf(x);
-          o[e] = x + rv[u][e];
+        f32x4 o = v[u] + bv[u];
+        if (gelu) {   // packed-fp32 erf-GELU, bit-identical to the scalar form
+          const f32x2 lo = gelu_erf2(f32x2{o[0], o[1]}), hi = gelu_erf2(f32x2{o[2], o[3]});
+          o = f32x4{lo.x, lo.y, hi.x, hi.y};
         }
+        o += rv[u];
         if (ok[u]) {
           if (g.Cf) *(f32x4*)(g.Cf + off[u]) = o;
           if (g.Ct) {
