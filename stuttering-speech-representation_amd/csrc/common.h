@@ -123,6 +123,7 @@ enum { AMODE_SEG = 0, AMODE_CONV = 1 };
 int launch_gemm_bf16(const GemmArgs& a, int amode, int groups, hipStream_t s);
 int launch_gemm_f32(const GemmArgs& a, int amode, int groups, hipStream_t s);
 
+int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s);   // kernels_gemm8.hip
 template <typename T> inline int launch_gemm(const GemmArgs& a, int amode, int groups, hipStream_t s);
 template <> inline int launch_gemm<bf16>(const GemmArgs& a, int amode, int groups, hipStream_t s) {
   return launch_gemm_bf16(a, amode, groups, s);

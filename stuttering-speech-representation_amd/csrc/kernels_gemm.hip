@@ -331,6 +331,9 @@ int launch_any(const GemmArgs& a, int amode, int groups, hipStream_t s) {
   const int force = fe ? atoi(fe) : 0;
   if (a.N % 128 == 0 && a.M >= 2048 && force == 2) return launch_cfg<T, 256, 128, 4, 2, 3>(a, amode, groups, s);
   if constexpr (sizeof(T) == 2) {
+    // SSE_GEMM_CFG=4: the 8-phase ping-pong 256x256 kernel (kernels_gemm8.hip)
+    if (force == 4 && amode == AMODE_SEG && groups == 1 && a.N % 256 == 0 && a.K % 64 == 0 && a.M >= 4096)
+      return launch_gemm8_bf16(a, s);
     if (a.N % 256 == 0 && a.M >= 4096 && (force == 0 || force == 3))
       return launch_cfg<T, 256, 256, 2, 4, 2>(a, amode, groups, s);
   }

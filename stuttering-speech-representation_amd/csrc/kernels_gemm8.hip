@@ -1,0 +1,289 @@
+// 256x256 bf16 MFMA GEMM with an 8-phase ping-pong schedule (gfx950).
+//
+// Same contract as gemm_body<bf16, 256, 256, ...> in kernels_gemm.hip (SEG-mode A rows, B as
+// [N][K], fused bias / GELU / fp32 residual epilogue), restricted to K % 64 == 0, N % 256 == 0.
+//
+// Why: in the 2-stage loop every K-step ends in vmcnt(0) + barrier, so the block waits for the
+// tile it just requested and all 8 waves issue their LDS reads at the same moment; PMC on the
+// WavLM shapes showed 39-45 % of wave cycles parked (SQ_WAIT_ANY) with the MFMA pipe busy 24-41 %.
+//
+// Schedule (derivation in DESIGN.md "GEMM 8-phase schedule"):
+//  * 8 waves = 2 groups (wm) x 4 (wn).  Wave (wm, wn) owns rows {mi*128 + wm*64 + [0,64)} and
+//    columns {ni*128 + wn*32 + [0,32)} for mi, ni in {0,1}, so each 128-row / 128-column HALF of
+//    the A / B tile is read by all waves in exactly one phase.
+//  * K-tile t (BK = 64) runs 4 phases (mi, ni) = (0,0) (0,1) (1,1) (1,0).  A phase is an
+//    L-section (ds_read fragments, issue one half-tile of LDS-DMA, counted vmcnt), a barrier,
+//    an M-section (16 MFMA 16x16x32 at raised priority) and a barrier.  Group 1 starts one
+//    barrier late, so on every SIMD one wave is in its M-section while the other loads.
+//  * B fragments of ni = 0 stay in registers from phase 0 to phase 3, so per K-tile each half
+//    is read once: A0 and B0 in phase 0, B1 in phase 1, A1 in phase 2.
+//  * Phase k = 4t+p issues: p0 -> B1(t+1), p1 -> A1(t+1), p2 -> A0(t+2), p3 -> B0(t+2) into
+//    buffer (tile & 1).  Every half is issued >= 5 phases before its first read and after the
+//    barrier that follows the last lgkmcnt of its previous occupant; a uniform vmcnt(8) at the
+//    end of each L-section (fewer in the tail) retires what the next phase reads.
+#include <type_traits>
+
+#include "common.h"
+
+namespace {
+
+constexpr int G8_HALF = 128 * 128;            // one half-tile: 128 rows x 128 B (64 bf16 of K)
+constexpr int G8_BUF = 4 * G8_HALF;           // A rows 0-127 | A rows 128-255 | B cols 0-127 | B cols 128-255
+constexpr int G8_OPS = 2 * G8_BUF;            // two K-tiles: 128 KiB
+constexpr int G8_CLD = 256 + 4;               // epilogue fp32 row stride (floats)
+constexpr int G8_EPI = 128 * G8_CLD * 4;      // one 128-row half of the C tile
+constexpr int G8_SMEM = G8_OPS > G8_EPI ? G8_OPS : G8_EPI;
+
+// phase k = 4t + p (k >= -8) -> the (tile, half) whose LDS-DMA it issues
+SSE_DEV void g8_target(int k, int& tile, int& half) {
+  const int t = (k + 8) / 4 - 2, p = (k + 8) & 3;
+  tile = p < 2 ? t + 1 : t + 2;
+  half = p == 0 ? 3 : (p == 1 ? 1 : (p == 2 ? 0 : 2));
+}
+
+SSE_DEV int g8_issued(int k, int nk) {
+  if (k < -6) return 0;
+  int tile, half;
+  g8_target(k, tile, half);
+  return tile < nk ? 1 : 0;
+}
+
+// retire every half-tile issued at phases <= k-4 (2 DMA instructions per half per wave)
+SSE_DEV void g8_wait(int k, int nk) {
+  const int n = g8_issued(k, nk) + g8_issued(k - 1, nk) + g8_issued(k - 2, nk) + g8_issued(k - 3, nk);
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+  }
+}
+
+SSE_DEV void g8_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[G8_SMEM];   // the ONLY shared object
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int q = lane >> 4, r16 = lane & 15;
+  const int M = g.M, N = g.N, K = g.K;
+  const int n_tiles_n = N / 256;
+  int bid = blockIdx.x;
+  {   // XCD-aware bijective remap (as gemm_body)
+    const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
+    bid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
+  }
+  const int m0 = (bid / n_tiles_n) * 256, n0 = (bid % n_tiles_n) * 256;
+  const int nk = K / 64;
+
+  // ---- LDS-DMA sources: buffer descriptors based at the block's first A row / B row; each
+  // lane's byte offset is fixed for the whole K loop, the scalar soffset advances by 128 B.
+  constexpr int NREC = 0x7FFFFFF0;
+  __amdgpu_buffer_rsrc_t a_rsrc, b_rsrc;
+  unsigned a_voff[2][2], b_voff[2][2];
+  {
+    const int mf = m0 < M ? m0 : M - 1;
+    const int seg0 = mf / g.rows_per_seg, rr0 = mf - seg0 * g.rows_per_seg;
+    const long long a_base = (long long)seg0 * g.seg_stride + (long long)rr0 * g.lda;
+    a_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const bf16*)g.A + a_base), (short)0, NREC, 0x00020000);
+    b_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const bf16*)g.B + (long long)n0 * K), (short)0, NREC,
+                                               0x00020000);
+    #pragma unroll
+    for (int h = 0; h < 2; ++h)
+      #pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int row = h * 128 + (wave + 8 * s) * 8 + (lane >> 3);
+        const int ch = (lane & 7) ^ ((row >> 1) & 7);
+        int m = m0 + row;
+        m = m < M ? m : M - 1;
+        const int seg = m / g.rows_per_seg, rr = m - seg * g.rows_per_seg;
+        const long long el = (long long)seg * g.seg_stride + (long long)rr * g.lda + ch * 8;
+        a_voff[h][s] = (unsigned)((el - a_base) * 2);
+        b_voff[h][s] = (unsigned)(((long long)row * K + ch * 8) * 2);
+      }
+  }
+  auto issue = [&](int k) {
+    if (k < -6) return;
+    int tile, half;
+    g8_target(k, tile, half);
+    if (tile >= nk) return;
+    char* dst = smem + (tile & 1) * G8_BUF + half * G8_HALF;
+    const unsigned soff = (unsigned)tile * 128u;
+    if (half < 2) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, LPTR(dst + wave * 1024), 16, a_voff[half][0], soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, LPTR(dst + (wave + 8) * 1024), 16, a_voff[half][1], soff, 0, 0);
+    } else {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, LPTR(dst + wave * 1024), 16, b_voff[half - 2][0], soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, LPTR(dst + (wave + 8) * 1024), 16, b_voff[half - 2][1], soff, 0,
+                                               0);
+    }
+  };
+
+  f32x4 acc[2][2][4][2];
+  #pragma unroll
+  for (int a = 0; a < 2; ++a)
+    #pragma unroll
+    for (int b = 0; b < 2; ++b)
+      #pragma unroll
+      for (int i = 0; i < 4; ++i)
+        #pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[4][2], b0f[2][2], b1f[2][2];
+
+  auto read_a = [&](const char* hb) {
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wm * 64 + i * 16 + r16;
+      #pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        af[i][ks] = *(const bf16x8*)(hb + row * 128 + (((q + 4 * ks) ^ ((row >> 1) & 7)) * 16));
+    }
+  };
+  auto read_b = [&](const char* hb, bf16x8 (&bf)[2][2]) {
+    #pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = wn * 32 + j * 16 + r16;
+      #pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        bf[j][ks] = *(const bf16x8*)(hb + row * 128 + (((q + 4 * ks) ^ ((row >> 1) & 7)) * 16));
+    }
+  };
+  auto mma = [&](f32x4 (&c)[4][2], const bf16x8 (&bf)[2][2]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      #pragma unroll
+      for (int i = 0; i < 4; ++i)
+        #pragma unroll
+        for (int j = 0; j < 2; ++j) c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bf[j][ks], c[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // ---- prologue: phases -6..-1 stage A0(0) B0(0) B1(0) A1(0) A0(1) B0(1)
+  for (int k = -6; k < 0; ++k) issue(k);
+  g8_wait(-1, nk);
+  g8_barrier();
+  if (wm == 1) g8_barrier();   // group 1 runs one barrier behind
+
+  // steady K-tiles (t + 2 < nk): every phase issues a half and waits vmcnt(8) with no
+  // scalar bookkeeping; the last two K-tiles take the counted tail path.
+  auto run_tile = [&](int t, auto steady) {
+    constexpr bool ST = decltype(steady)::value;
+    const char* buf = smem + (t & 1) * G8_BUF;
+    const int k = 4 * t;
+    auto issue_wait = [&](int kk) {
+      if constexpr (ST) {
+        issue(kk);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        issue(kk);
+        g8_wait(kk, nk);
+      }
+    };
+    // phase 0: (mi 0, ni 0) reads A rows 0-127 and B cols 0-127
+    read_a(buf);
+    read_b(buf + 2 * G8_HALF, b0f);
+    issue_wait(k);
+    g8_barrier();
+    mma(acc[0][0], b0f);
+    g8_barrier();
+    // phase 1: (mi 0, ni 1) reads B cols 128-255
+    read_b(buf + 3 * G8_HALF, b1f);
+    issue_wait(k + 1);
+    g8_barrier();
+    mma(acc[0][1], b1f);
+    g8_barrier();
+    // phase 2: (mi 1, ni 1) reads A rows 128-255
+    read_a(buf + G8_HALF);
+    issue_wait(k + 2);
+    g8_barrier();
+    mma(acc[1][1], b1f);
+    g8_barrier();
+    // phase 3: (mi 1, ni 0) no reads
+    issue_wait(k + 3);
+    g8_barrier();
+    mma(acc[1][0], b0f);
+    g8_barrier();
+  };
+  int t = 0;
+  for (; t + 2 < nk; ++t) run_tile(t, std::integral_constant<bool, true>{});
+  for (; t < nk; ++t) run_tile(t, std::integral_constant<bool, false>{});
+  if (wm == 0) g8_barrier();   // balance group 1's extra barrier
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // ---- epilogue: per 128-row half, stage fp32 through LDS, then coalesced 16-B passes -----
+  float* Cs = (float*)smem;
+  constexpr int CH = 128 * 256 / 4;
+  constexpr int UNR = 4;
+  const bool has_bias = g.bias != nullptr, has_res = g.resid != nullptr, gelu = g.act == ACT_GELU;
+  #pragma unroll
+  for (int mi = 0; mi < 2; ++mi) {
+    __syncthreads();
+    #pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+      #pragma unroll
+      for (int i = 0; i < 4; ++i)
+        #pragma unroll
+        for (int j = 0; j < 2; ++j)
+          #pragma unroll
+          for (int r = 0; r < 4; ++r)
+            Cs[(wm * 64 + i * 16 + q * 4 + r) * G8_CLD + ni * 128 + wn * 32 + j * 16 + r16] = acc[mi][ni][i][j][r];
+    __syncthreads();
+    for (int base = threadIdx.x; base < CH; base += 512 * UNR) {
+      f32x4 v[UNR], rv[UNR], bv[UNR];
+      long long off[UNR];
+      bool ok[UNR];
+      #pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int c = base + u * 512;
+        const int row = c >> 6, cc = (c & 63) * 4;
+        const int m = m0 + mi * 128 + row, n = n0 + cc;
+        ok[u] = m < M;
+        off[u] = (long long)(ok[u] ? m : 0) * g.ldc + n;
+        v[u] = *(const f32x4*)(Cs + row * G8_CLD + cc);
+        bv[u] = has_bias ? *(const f32x4*)(g.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+        rv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (has_res) {
+          const long long ro = g.resid_rows ? (long long)((ok[u] ? m : 0) % g.resid_rows) * g.ldc + n : off[u];
+          rv[u] = *(const f32x4*)(g.resid + ro);
+        }
+      }
+      #pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        f32x4 o = v[u] + bv[u];
+        if (gelu) {
+          const f32x2 lo = gelu_erf2(f32x2{o[0], o[1]}), hi = gelu_erf2(f32x2{o[2], o[3]});
+          o = f32x4{lo.x, lo.y, hi.x, hi.y};
+        }
+        o += rv[u];
+        if (ok[u]) {
+          if (g.Cf) *(f32x4*)(g.Cf + off[u]) = o;
+          if (g.Ct) {
+            const bf16x4 ob = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+            *(bf16x4*)((bf16*)g.Ct + off[u]) = ob;
+          }
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+
+int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
+  if (a.M <= 0 || a.N % 256 || a.K % 64 || a.K <= 0) return -3;
+  dim3 grid((unsigned)(((a.M + 255) / 256) * (a.N / 256)));
+  hipLaunchKernelGGL(gemm8_kernel, grid, dim3(512), 0, s, a);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}

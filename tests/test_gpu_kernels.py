@@ -48,10 +48,13 @@ def test_gemm_rejects_bad_shapes():
         gemm(a, b)
 
 
-@pytest.mark.parametrize("M,N,K", [(4099, 512, 768), (8192, 768, 3072), (4100, 2560, 136)])
+@pytest.mark.parametrize("M,N,K", [(4099, 512, 768), (8192, 768, 3072), (4100, 2560, 136), (4133, 768, 64),
+                                   (5000, 256, 128), (6000, 512, 192), (4096, 256, 256)])
 def test_gemm_tile_configs_agree(monkeypatch, M, N, K):
-    """The 256x256 default, the 128x128 tile (SSE_GEMM_CFG=1) and the 256x128 3-stage ring
-    (SSE_GEMM_CFG=2) accumulate every output in the same K order: results are bit-identical."""
+    """The 256x256 default, the 128x128 tile (SSE_GEMM_CFG=1), the 256x128 3-stage ring
+    (SSE_GEMM_CFG=2) and the 8-phase ping-pong kernel (SSE_GEMM_CFG=4) accumulate every output
+    in the same K order: results are bit-identical (K-tile counts 1, 2, 3, 4, 12, 48 cover the
+    8-phase prologue / steady / tail paths)."""
     from ssr_amd.model import gemm
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
@@ -59,10 +62,10 @@ def test_gemm_tile_configs_agree(monkeypatch, M, N, K):
     bias = torch.randn(N, device="cuda", generator=g)
     resid = torch.randn(M, N, device="cuda", generator=g)
     outs = []
-    for cfg in ("0", "1", "2"):
+    for cfg in ("0", "1", "2", "4"):
         monkeypatch.setenv("SSE_GEMM_CFG", cfg)
         outs.append(gemm(a, b, bias, resid, None))
     ref = _ref(a, b, bias, resid, None)
     for o in outs:
         assert ((o - ref).norm() / ref.norm()).item() <= 1e-5
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2]) and torch.equal(outs[0], outs[3])
