@@ -331,10 +331,14 @@ int launch_any(const GemmArgs& a, int amode, int groups, hipStream_t s) {
   const int force = fe ? atoi(fe) : 0;
   if (a.N % 128 == 0 && a.M >= 2048 && force == 2) return launch_cfg<T, 256, 128, 4, 2, 3>(a, amode, groups, s);
   if constexpr (sizeof(T) == 2) {
-    // SSE_GEMM_CFG=4: the 8-phase ping-pong 256x256 kernel (kernels_gemm8.hip)
-    if (force == 4 && amode == AMODE_SEG && groups == 1 && a.N % 256 == 0 && a.K % 64 == 0 && a.M >= 4096)
+    // default for plain / SEG-row bf16 GEMMs with N % 256 == 0, K % 64 == 0: the 8-phase
+    // ping-pong 256x256 kernel (kernels_gemm8.hip; measured vs this file's 256x256 2-stage loop:
+    // qkv 863 vs 760, ffn1 721 vs 653, ffn2 997 vs 880, 4096^3 1353 vs 1192 TF/s).
+    // SSE_GEMM_CFG=3 keeps the 2-stage 256x256 kernel for A/B runs.
+    if ((force == 0 || force == 4) && amode == AMODE_SEG && groups == 1 && a.N % 256 == 0 && a.K % 64 == 0 &&
+        a.M >= 4096)
       return launch_gemm8_bf16(a, s);
-    if (a.N % 256 == 0 && a.M >= 4096 && (force == 0 || force == 3))
+    if (a.N % 256 == 0 && a.M >= 4096 && (force == 0 || force == 3 || force == 4))
       return launch_cfg<T, 256, 256, 2, 4, 2>(a, amode, groups, s);
   }
   if (a.N % 128 == 0) return launch_cfg<T, 128, 128, 2, 2, 2>(a, amode, groups, s);

@@ -51,8 +51,8 @@ def test_gemm_rejects_bad_shapes():
 @pytest.mark.parametrize("M,N,K", [(4099, 512, 768), (8192, 768, 3072), (4100, 2560, 136), (4133, 768, 64),
                                    (5000, 256, 128), (6000, 512, 192), (4096, 256, 256)])
 def test_gemm_tile_configs_agree(monkeypatch, M, N, K):
-    """The 256x256 default, the 128x128 tile (SSE_GEMM_CFG=1), the 256x128 3-stage ring
-    (SSE_GEMM_CFG=2) and the 8-phase ping-pong kernel (SSE_GEMM_CFG=4) accumulate every output
+    """The default (8-phase ping-pong 256x256 where it applies), the 128x128 tile (SSE_GEMM_CFG=1),
+    the 256x128 3-stage ring (SSE_GEMM_CFG=2) and the 2-stage 256x256 kernel (SSE_GEMM_CFG=3) accumulate every output
     in the same K order: results are bit-identical (K-tile counts 1, 2, 3, 4, 12, 48 cover the
     8-phase prologue / steady / tail paths)."""
     from ssr_amd.model import gemm
@@ -62,7 +62,7 @@ def test_gemm_tile_configs_agree(monkeypatch, M, N, K):
     bias = torch.randn(N, device="cuda", generator=g)
     resid = torch.randn(M, N, device="cuda", generator=g)
     outs = []
-    for cfg in ("0", "1", "2", "4"):
+    for cfg in ("0", "1", "2", "3"):
         monkeypatch.setenv("SSE_GEMM_CFG", cfg)
         outs.append(gemm(a, b, bias, resid, None))
     ref = _ref(a, b, bias, resid, None)
