@@ -138,41 +138,45 @@ __global__ __launch_bounds__(256) void conv0_apply_kernel(const float* __restric
   if (norm) { mu = norm[2 * b]; rs = norm[2 * b + 1]; }
   for (int i = threadIdx.x; i < nx; i += blockDim.x) xs[i] = norm ? (xb[i] - mu) * rs : xb[i];
   __syncthreads();
-  // one channel PAIR per thread: both channels read the same sample window, so the 10-tap FMA,
-  // the GroupNorm affine and GELU run as packed fp32 (2 results per VALU op) and the store is 2
-  // adjacent outputs.  C is even (host-checked).
-  for (int c = 2 * threadIdx.x; c < C; c += 2 * blockDim.x) {
-    f32x2 w[K0];
+  // each lane owns 8 adjacent channels (4 packed-fp32 pairs: 4 independent FMA / GELU chains,
+  // one 16-B store per frame); the block's 4 waves split the chunk's frames.  C % 8 == 0.
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int c = lane * 8; c < C; c += 512) {
+    f32x2 w[4][K0], bias[4], sc[4], sh[4];
     #pragma unroll
-    for (int j = 0; j < K0; ++j) w[j] = f32x2{w0[c * K0 + j], w0[(c + 1) * K0 + j]};
-    const f32x2 bias = b0 ? f32x2{b0[c], b0[c + 1]} : f32x2{0.f, 0.f};
-    f32x2 sc = {1.f, 1.f}, sh = {0.f, 0.f};
-    if (!RAW) {
-      const float2 s0v = ss[(long long)b * C + c], s1v = ss[(long long)b * C + c + 1];
-      sc = f32x2{s0v.x, s1v.x};
-      sh = f32x2{s0v.y, s1v.y};
+    for (int p = 0; p < 4; ++p) {
+      const int c0 = c + 2 * p;
+      #pragma unroll
+      for (int j = 0; j < K0; ++j) w[p][j] = f32x2{w0[c0 * K0 + j], w0[(c0 + 1) * K0 + j]};
+      bias[p] = b0 ? f32x2{b0[c0], b0[c0 + 1]} : f32x2{0.f, 0.f};
+      sc[p] = f32x2{1.f, 1.f};
+      sh[p] = f32x2{0.f, 0.f};
+      if (!RAW) {
+        const float2 s0v = ss[(long long)b * C + c0], s1v = ss[(long long)b * C + c0 + 1];
+        sc[p] = f32x2{s0v.x, s1v.x};
+        sh[p] = f32x2{s0v.y, s1v.y};
+      }
     }
     TO* ob = out + ((long long)b * T0 + t0) * C + c;
-    // sliding window: frame t+1 reuses samples 5..9 of frame t, so 5 new LDS reads per frame
-    float win[K0];
-    #pragma unroll
-    for (int j = 0; j < K0; ++j) win[j] = xs[j];
-    for (int t = 0; t < nt; ++t) {
-      f32x2 y = bias;
+    for (int t = wv; t < nt; t += 4) {
+      f32x2 y[4] = {bias[0], bias[1], bias[2], bias[3]};
       #pragma unroll
-      for (int j = 0; j < K0; ++j) y = __builtin_elementwise_fma(w[j], f32x2{win[j], win[j]}, y);
-      if (!RAW) y = gelu_erf2(__builtin_elementwise_fma(y, sc, sh));
-      if constexpr (sizeof(TO) == 2) {
-        const bf16x2 o2 = {(bf16)y.x, (bf16)y.y};
-        *(bf16x2*)(ob + (long long)t * C) = o2;
-      } else {
-        *(f32x2*)((float*)ob + (long long)t * C) = y;
-      }
-      #pragma unroll
-      for (int j = 0; j < K0 - S0; ++j) win[j] = win[j + S0];
-      if (t + 1 < nt) {
+      for (int j = 0; j < K0; ++j) {
+        const float xv = xs[t * S0 + j];
         #pragma unroll
-        for (int j = K0 - S0; j < K0; ++j) win[j] = xs[(t + 1) * S0 + j];
+        for (int p = 0; p < 4; ++p) y[p] = __builtin_elementwise_fma(w[p][j], f32x2{xv, xv}, y[p]);
+      }
+      if (!RAW) {
+        #pragma unroll
+        for (int p = 0; p < 4; ++p) y[p] = gelu_erf2(__builtin_elementwise_fma(y[p], sc[p], sh[p]));
+      }
+      if constexpr (sizeof(TO) == 2) {
+        const bf16x8 o8 = {(bf16)y[0].x, (bf16)y[0].y, (bf16)y[1].x, (bf16)y[1].y,
+                           (bf16)y[2].x, (bf16)y[2].y, (bf16)y[3].x, (bf16)y[3].y};
+        *(bf16x8*)(ob + (long long)t * C) = o8;
+      } else {
+        *(f32x4*)((float*)ob + (long long)t * C) = f32x4{y[0].x, y[0].y, y[1].x, y[1].y};
+        *(f32x4*)((float*)ob + (long long)t * C + 4) = f32x4{y[2].x, y[2].y, y[3].x, y[3].y};
       }
     }
   }
@@ -188,8 +192,8 @@ int launch_conv0_gn(const float* x, int B, int L, const float* norm, const float
   hipLaunchKernelGGL(conv0_moments_kernel, dim3(B), dim3(256), 0, s, x, L, norm, s0, T0, mom);
   hipLaunchKernelGGL(gn_finalize_kernel, dim3((B * C + 255) / 256), dim3(256), 0, s, mom, B, C, T0, w0, b0, gamma,
                      beta, eps, ss);
-  if (C % 2) return -3;
-  dim3 grid((T0 + C0_T - 1) / C0_T, B), block(C / 2 < 256 ? C / 2 : 256);
+  if (C % 8) return -3;
+  dim3 grid((T0 + C0_T - 1) / C0_T, B), block(256);
   hipLaunchKernelGGL((conv0_apply_kernel<TO, false>), grid, block, 0, s, x, L, norm, w0, b0, C, T0, ss, out);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
@@ -199,8 +203,8 @@ template <typename TO>
 int launch_conv0_raw(const float* x, int B, int L, const float* norm, const float* w0, const float* b0, int C,
                      int k0, int s0, int T0, TO* out, hipStream_t s) {
   if (k0 != K0 || s0 != 5) return -3;
-  if (C % 2) return -3;
-  dim3 grid((T0 + C0_T - 1) / C0_T, B), block(C / 2 < 256 ? C / 2 : 256);
+  if (C % 8) return -3;
+  dim3 grid((T0 + C0_T - 1) / C0_T, B), block(256);
   hipLaunchKernelGGL((conv0_apply_kernel<TO, true>), grid, block, 0, s, x, L, norm, w0, b0, C, T0,
                      (const float2*)nullptr, out);
   return hipGetLastError() == hipSuccess ? 0 : -2;
@@ -839,7 +843,7 @@ __global__ __launch_bounds__(640) void attention_full_kernel(AttnArgs a) {
       const int key = kb * 16 + 4 * g + r;
       float v = s[kb][r] * a.scale;
       if (BIAS) v = fmaf(gq, rb[key - qi + (TP - 1)], v);
-      v = key < T ? v : -INFINITY;
+      if (kb * 16 + 16 > T) v = key < T ? v : -INFINITY;   // only the last key block is ragged
       s[kb][r] = v;
       mx = fmaxf(mx, v);
     }
