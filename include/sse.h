@@ -128,6 +128,18 @@ int sse_whisper_embed(sse_model* m, const float* d_wave, int B, int L, const int
 int sse_whisper_decoder_hidden_states(sse_model* m, const float* d_enc, int B, float* d_hs, void* d_ws,
                                       size_t ws_bytes, void* stream);
 
+/* ---- ingest ----
+ * Mono mix: torch.mean(waveform, dim=0) of load_audio (REF/WavLM_embeddings.py:103-105,
+ * REF/whisper_embeddings_large.py:78-96): d_in [B][C][L] -> d_out [B][L]. */
+int sse_mono(const float* d_in, int B, int C, int L, float* d_out, void* stream);
+/* torchaudio.transforms.Resample(orig_freq, new_freq) (default sinc_interp_hann, width 6, rolloff
+ * 0.99) of load_audio (REF/WavLM_embeddings.py:107-110): d_in [B][L] -> d_out [B][Lo],
+ * Lo = sse_resample_length(L, orig, new) = ceil(new*L/orig). */
+int sse_resample_length(int L, int orig_freq, int new_freq);
+size_t sse_resample_workspace_bytes(int B, int L, int orig_freq, int new_freq);
+int sse_resample(const float* d_in, int B, int L, int orig_freq, int new_freq, float* d_out, void* d_ws,
+                 size_t ws_bytes, void* stream);
+
 /* Wav2Vec2FeatureExtractor zero_mean_unit_var_norm on device (feature_extraction_wav2vec2.py:94):
  * d_out[b] = (d_in[b] - mean_b) / sqrt(var_b + 1e-7).  Workspace: 8 * B bytes. */
 int sse_normalize(const float* d_in, int B, int L, float* d_out, void* d_ws, size_t ws_bytes, void* stream);

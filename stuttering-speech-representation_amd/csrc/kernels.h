@@ -39,3 +39,10 @@ int launch_xattn1(const TE* q, const TE* kv, int B, int T, int D, int nh, TE* ou
 int launch_bcast_rows(const float* v, int D, int B, float* out, hipStream_t s);
 template <typename TO>
 int launch_cast(const float* x, long long n, TO* y, hipStream_t s);
+
+// kernels_ingest.hip
+int resample_length(int L, int orig_freq, int new_freq);
+size_t resample_workspace_bytes(int B, int L, int orig_freq, int new_freq);
+int launch_resample(const float* x, int B, int L, int orig_freq, int new_freq, float* y, void* ws, size_t ws_bytes,
+                    hipStream_t s);
+int launch_mono(const float* x, int B, int C, int L, float* y, hipStream_t s);

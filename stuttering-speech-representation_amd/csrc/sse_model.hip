@@ -1030,6 +1030,29 @@ int sse_profile_stop(sse_model* m) {
 
 size_t sse_normalize_workspace_bytes(int B) { return (size_t)B * 8; }
 
+int sse_resample_length(int L, int orig_freq, int new_freq) {
+  if (L <= 0 || orig_freq <= 0 || new_freq <= 0) return SSE_ERR_INVALID;
+  return orig_freq == new_freq ? L : resample_length(L, orig_freq, new_freq);
+}
+
+size_t sse_resample_workspace_bytes(int B, int L, int orig_freq, int new_freq) {
+  if (B <= 0 || L <= 0 || orig_freq <= 0 || new_freq <= 0) return 0;
+  return orig_freq == new_freq ? 256 : resample_workspace_bytes(B, L, orig_freq, new_freq);
+}
+
+int sse_resample(const float* d_in, int B, int L, int orig_freq, int new_freq, float* d_out, void* d_ws,
+                 size_t ws_bytes, void* stream) {
+  if (!d_in || !d_out || !d_ws) return SSE_ERR_INVALID;
+  const int rc = launch_resample(d_in, B, L, orig_freq, new_freq, d_out, d_ws, ws_bytes, (hipStream_t)stream);
+  return rc == -4 ? SSE_ERR_WORKSPACE : (rc == -1 ? SSE_ERR_INVALID : (rc ? SSE_ERR_HIP : SSE_OK));
+}
+
+int sse_mono(const float* d_in, int B, int C, int L, float* d_out, void* stream) {
+  if (!d_in || !d_out) return SSE_ERR_INVALID;
+  const int rc = launch_mono(d_in, B, C, L, d_out, (hipStream_t)stream);
+  return rc == -1 ? SSE_ERR_INVALID : (rc ? SSE_ERR_HIP : SSE_OK);
+}
+
 int sse_gemm(int dtype, const void* d_a, const void* d_b, const float* d_bias, const float* d_resid, float* d_cf,
              void* d_ct, int M, int N, int K, int act, const void* d_zero, void* stream) {
   if (!d_a || !d_b || !d_zero || M <= 0 || N <= 0 || K <= 0 || (!d_cf && !d_ct)) return SSE_ERR_INVALID;

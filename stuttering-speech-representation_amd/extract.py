@@ -71,14 +71,14 @@ def read_wav(path: str) -> tuple[np.ndarray, int]:
     return x[:n * ch].reshape(n, ch).T.copy(), sr
 
 
-def load_audio(file_path, target_sr=16000, max_length=None):
-    """REF/WavLM_embeddings.py:87-125: mono mean, (resample), trim; float32[n] or None."""
+def load_audio(file_path, target_sr=16000, max_length=None, device=None):
+    """REF/WavLM_embeddings.py:87-125: mono mean, resample, trim; float32[n] or None.
+    Mono mixing and resampling run on the GPU (ingest.py); a 16 kHz mono file needs no GPU."""
     try:
         wav, sr = read_wav(file_path)
-        if wav.shape[0] > 1:
-            wav = wav.mean(axis=0, keepdims=True)
-        if sr != target_sr:
-            raise NotImplementedError(f"resampling {sr} -> {target_sr} Hz is SURVEY §8(f) next-3 (ingest)")
+        if wav.shape[0] > 1 or sr != target_sr:
+            from .ingest import to_16k_mono
+            wav = to_16k_mono(wav, sr, target_sr, device).cpu().numpy()[None]
         if max_length is not None:
             m = int(max_length * target_sr)
             if wav.shape[1] > m:
@@ -133,7 +133,7 @@ def extract_embeddings_from_audio_wavlm(audio_array, model, feature_extractor, d
 def extract_wavlm_embeddings(audio_file, model, feature_extractor, device, layer_indices, max_length=None,
                              sample_rate=16000):
     """REF/WavLM_embeddings.py:267-341."""
-    audio = load_audio(audio_file, target_sr=sample_rate, max_length=max_length)
+    audio = load_audio(audio_file, target_sr=sample_rate, max_length=max_length, device=device)
     if audio is None:
         return None
     if audio.shape[-1] > 500000:
@@ -199,7 +199,7 @@ def extract_embeddings_from_audio_whisper(audio_array, model, processor, device,
 
 def extract_whisper_embeddings_fixed(audio_file, model, processor, device, encoder_indices, decoder_indices):
     """REF/whisper_embeddings_large.py:234-299: encoder time-means + 1-token decoder states."""
-    audio = load_audio(audio_file)
+    audio = load_audio(audio_file, device=device)
     if audio is None:
         return None
     if isinstance(model, WhisperModel):

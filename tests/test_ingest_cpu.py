@@ -1,0 +1,128 @@
+"""CPU checks of the ingest row: the resampling oracle's properties
+(torchaudio is absent: parity against torchaudio itself is UNPINNED, see oracle/resample.py)
+and the on-disk embedding format (writer.py) against the reference's reader logic."""
+import math
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+
+
+def test_resample_identity_and_length():
+    from oracle.resample import resample
+    x = np.random.default_rng(0).standard_normal(1000).astype(np.float32)
+    assert np.array_equal(resample(x, 16000, 16000), x)
+    for sr in (8000, 22050, 32000, 44100, 48000):
+        for L in (1, 7, 441, 1000, 44101):
+            y = resample(np.zeros(L, np.float32), sr, 16000)
+            assert y.shape == (math.ceil(16000 * L / sr),)
+
+
+def test_resample_preserves_band_limited_tone():
+    from oracle.resample import resample
+    for sr in (22050, 44100, 48000, 8000):
+        n = sr * 2
+        t = np.arange(n) / sr
+        f = 440.0 if sr > 8000 else 300.0
+        x = (0.5 * np.sin(2 * np.pi * f * t)).astype(np.float32)
+        y = resample(x, sr, 16000)
+        ty = np.arange(y.shape[0]) / 16000
+        ref = 0.5 * np.sin(2 * np.pi * f * ty)
+        mid = slice(200, y.shape[0] - 200)               # away from the zero-padded edges
+        assert np.abs(y[mid] - ref[mid]).max() < 2e-3, sr
+
+
+def test_resample_linear_and_close_to_scipy_polyphase():
+    from oracle.resample import resample
+    from scipy.signal import resample_poly
+    rng = np.random.default_rng(1)
+    a, b = rng.standard_normal((2, 8820)).astype(np.float32)
+    ya, yb, yab = resample(a, 44100, 16000), resample(b, 44100, 16000), resample(a + 2 * b, 44100, 16000)
+    assert np.abs(yab - (ya + 2 * yb)).max() < 1e-5
+    # an independent polyphase design agrees on low-pass content (different filter, same ideal)
+    t = np.arange(44100) / 44100
+    x = (np.sin(2 * np.pi * 1000 * t) + 0.3 * np.sin(2 * np.pi * 3100 * t)).astype(np.float32)
+    y1 = resample(x, 44100, 16000)
+    y2 = resample_poly(x, 160, 441)
+    assert np.abs(y1[300:-300] - y2[300:-300]).max() < 5e-3
+
+
+def test_kernel_rows_are_normalised():
+    from oracle.resample import resample_kernel
+    k, width, orig, new = resample_kernel(44100, 16000)
+    assert (orig, new, width) == (441, 160, 17) and k.shape == (160, 2 * 17 + 441)
+    assert np.allclose(k.sum(axis=1), 1.0, atol=2e-2)    # DC gain ~1 (rolloff 0.99, Hann window)
+
+
+def test_mono_is_channel_mean():
+    from oracle.resample import mono
+    x = np.random.default_rng(2).standard_normal((3, 50)).astype(np.float32)
+    assert np.array_equal(mono(x), ((x[0] + x[1]) + x[2]) / np.float32(3))
+
+
+def _df(n, H, rng):
+    return pd.DataFrame({"filename": [f"f{i}" for i in range(n)], "path": [f"/d/f{i}.wav" for i in range(n)],
+                         "label": rng.integers(0, 2, n), "split": ["train"] * n,
+                         "layer_12": list(rng.standard_normal((n, H)).astype(np.float32)),
+                         "layer_6": list(rng.standard_normal((n, H)).astype(np.float32))})
+
+
+def test_save_embeddings_reference_layout(tmp_path):
+    from ssr_amd.writer import load_split, save_embeddings, write_split
+    rng = np.random.default_rng(3)
+    df = _df(5, 8, rng)
+    save_embeddings(df, str(tmp_path / "a"), split="train", expected_dim=8)
+    d = tmp_path / "a" / "train"
+    assert sorted(os.listdir(d)) == ["embedding_metadata.csv", "layer_12_embeddings.npy", "layer_6_embeddings.npy"]
+    meta = pd.read_csv(d / "embedding_metadata.csv")
+    assert list(meta.columns) == ["filename", "path", "label", "split"]
+    arr = np.load(d / "layer_12_embeddings.npy")
+    assert arr.dtype == np.float32 and arr.shape == (5, 8) and np.array_equal(arr, np.stack(df["layer_12"]))
+    # the reference reader's globbing (REF/model_training_1.py:128-139)
+    m2, emb = load_split(str(tmp_path / "a"), "train")
+    assert sorted(emb) == ["layer_12", "layer_6"] and m2.equals(meta)
+    # the batched writer produces byte-identical files
+    write_split(str(tmp_path / "b"), "train", df[["filename", "path", "label", "split"]],
+                {"layer_12": np.stack(df["layer_12"]), "layer_6": np.stack(df["layer_6"])})
+    for f in os.listdir(d):
+        assert (d / f).read_bytes() == (tmp_path / "b" / "train" / f).read_bytes()
+
+
+def test_whisper_columns_and_split_all(tmp_path):
+    from ssr_amd.writer import save_embeddings
+    df = pd.DataFrame({"filename": ["a", "b"], "encoder_layer_32": [np.ones(4, np.float32)] * 2,
+                       "decoder_layer_30": [np.zeros(4, np.float32)] * 2})
+    save_embeddings(df, str(tmp_path), split="all")
+    assert sorted(os.listdir(tmp_path)) == ["decoder_layer_30_embeddings.npy", "embedding_metadata.csv",
+                                            "encoder_layer_32_embeddings.npy"]
+
+
+def test_shards_merge_in_corpus_order_and_resume(tmp_path):
+    from ssr_amd.writer import ShardWriter, load_split, merge_shards, write_split
+    rng = np.random.default_rng(4)
+    N, H = 23, 6
+    meta = pd.DataFrame({"filename": [f"f{i}" for i in range(N)], "label": rng.integers(0, 3, N)})
+    emb = {"layer_12": rng.standard_normal((N, H)).astype(np.float32)}
+    # two ranks, out-of-order writes, rank 1 "crashes" and re-writes a range after resume
+    w0, w1 = ShardWriter(str(tmp_path), "devel", 0), ShardWriter(str(tmp_path), "devel", 1)
+    for lo, hi, w in ((12, 18, w1), (0, 6, w0), (6, 12, w0), (18, 23, w1)):
+        w.write(lo, meta.iloc[lo:hi], {k: v[lo:hi] for k, v in emb.items()})
+    w1b = ShardWriter(str(tmp_path), "devel", 1)
+    assert sorted(w1b.done()) == [(12, 6), (18, 5)]
+    w1b.write(18, meta.iloc[18:23], {k: v[18:23] for k, v in emb.items()})
+    assert merge_shards(str(tmp_path), "devel", expected_dim=H) == N
+    m, e = load_split(str(tmp_path), "devel")
+    assert np.array_equal(e["layer_12"], emb["layer_12"]) and list(m["filename"]) == list(meta["filename"])
+    write_split(str(tmp_path / "ref"), "devel", meta, emb)
+    assert (tmp_path / "devel" / "layer_12_embeddings.npy").read_bytes() == \
+        (tmp_path / "ref" / "devel" / "layer_12_embeddings.npy").read_bytes()
+
+
+def test_merge_detects_gap(tmp_path):
+    from ssr_amd.writer import ShardWriter, merge_shards
+    w = ShardWriter(str(tmp_path), None, 0)
+    w.write(0, [{"filename": "a"}], {"layer_1": np.zeros((1, 2), np.float32)})
+    w.write(2, [{"filename": "c"}], {"layer_1": np.zeros((1, 2), np.float32)})
+    with pytest.raises(ValueError):
+        merge_shards(str(tmp_path))
