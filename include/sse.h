@@ -140,6 +140,13 @@ size_t sse_resample_workspace_bytes(int B, int L, int orig_freq, int new_freq);
 int sse_resample(const float* d_in, int B, int L, int orig_freq, int new_freq, float* d_out, void* d_ws,
                  size_t ws_bytes, void* stream);
 
+/* Pointwise part of augment_audio (REF/model_training_1.py:167-214), one
+ * clip per row of d_in [B][L]: kind 0 none, 1 noise (x + N(0,1)*factor, N from the counter-hash
+ * Gaussian stream d_stream[b] of `seed`), 2 volume (x*factor), 3 clamp only (after the speed
+ * round trip, done with sse_resample); every kind ends in clamp(-1, 1). */
+int sse_augment(const float* d_in, float* d_out, int B, int L, const int32_t* d_kind, const float* d_factor,
+                const int64_t* d_stream, uint64_t seed, void* stream);
+
 /* Wav2Vec2FeatureExtractor zero_mean_unit_var_norm on device (feature_extraction_wav2vec2.py:94):
  * d_out[b] = (d_in[b] - mean_b) / sqrt(var_b + 1e-7).  Workspace: 8 * B bytes. */
 int sse_normalize(const float* d_in, int B, int L, float* d_out, void* d_ws, size_t ws_bytes, void* stream);

@@ -24,7 +24,7 @@ EXPORTED = ("sse_weight_floats", "sse_model_create", "sse_model_destroy", "sse_o
             "sse_normalize", "sse_normalize_workspace_bytes", "sse_whisper_hidden_states_from_mel",
             "sse_profile_start", "sse_profile_read", "sse_profile_stop", "sse_gemm", "sse_whisper_embed",
             "sse_whisper_decoder_hidden_states", "sse_mono", "sse_resample_length", "sse_resample_workspace_bytes",
-            "sse_resample")
+            "sse_resample", "sse_augment")
 
 
 class SSEError(RuntimeError):
@@ -132,6 +132,8 @@ def lib() -> ctypes.CDLL:
     L.sse_resample_workspace_bytes.restype = sz
     L.sse_resample.argtypes = [vp, i32, i32, i32, i32, vp, vp, sz, vp]
     L.sse_resample.restype = i32
+    L.sse_augment.argtypes = [vp, vp, i32, i32, vp, vp, vp, ctypes.c_uint64, vp]
+    L.sse_augment.restype = i32
     L.sse_strerror.argtypes = [i32]
     L.sse_strerror.restype = ctypes.c_char_p
     L.sse_rel_bucket.argtypes = [i32, i32, i32]

@@ -46,3 +46,5 @@ size_t resample_workspace_bytes(int B, int L, int orig_freq, int new_freq);
 int launch_resample(const float* x, int B, int L, int orig_freq, int new_freq, float* y, void* ws, size_t ws_bytes,
                     hipStream_t s);
 int launch_mono(const float* x, int B, int C, int L, float* y, hipStream_t s);
+int launch_augment(const float* x, float* y, int B, int L, const int* kind, const float* factor,
+                   const long long* stream, uint64_t seed, hipStream_t s);

@@ -131,3 +131,45 @@ int launch_mono(const float* x, int B, int C, int L, float* y, hipStream_t s) {
   hipLaunchKernelGGL(mono_kernel, dim3((L + 255) / 256, B), dim3(256), 0, s, x, C, L, y);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// ---------------------------------------------------------------------------------------
+// Pointwise augmentation of augment_audio (REF/model_training_1.py:167-214): per clip
+//   kind 0 none, 1 noise: x + (float)N(0,1) * factor, 2 volume: x * factor, 3 clamp only;
+// then torch.clamp(-1, 1).  N(0,1) is the build's counter-hash Gaussian (synth.gaussian: splitmix64
+// uniforms, Box-Muller in fp64) on stream 2*s / 2*s+1, so the oracle can restate it exactly.
+namespace {
+SSE_DEV uint64_t smix(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+SSE_DEV uint64_t sbase(uint64_t seed, uint64_t stream) {
+  return smix(seed * 0x100000001B3ull + stream * 0x9E3779B1ull + 0x632BE59BD9B4E019ull);
+}
+SSE_DEV double u01(uint64_t base, uint64_t i) { return (double)(smix(i + base) >> 11) * (1.0 / 9007199254740992.0); }
+
+__global__ void augment_kernel(const float* __restrict__ x, float* __restrict__ y, int L, const int* __restrict__ kind,
+                               const float* __restrict__ factor, const long long* __restrict__ stream, uint64_t seed) {
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= L) return;
+  const int k = kind[b];
+  float v = x[(long long)b * L + i];
+  if (k == 1) {
+    const uint64_t s = (uint64_t)stream[b];
+    const double g = sqrt(-2.0 * log1p(-u01(sbase(seed, 2 * s), i))) * cos(2.0 * M_PI * u01(sbase(seed, 2 * s + 1), i));
+    v = v + (float)g * factor[b];
+  } else if (k == 2) {
+    v = v * factor[b];
+  }
+  y[(long long)b * L + i] = fminf(fmaxf(v, -1.0f), 1.0f);
+}
+}  // namespace
+
+int launch_augment(const float* x, float* y, int B, int L, const int* kind, const float* factor,
+                   const long long* stream, uint64_t seed, hipStream_t s) {
+  if (B <= 0 || L <= 0) return -1;
+  hipLaunchKernelGGL(augment_kernel, dim3((L + 255) / 256, B), dim3(256), 0, s, x, y, L, kind, factor, stream, seed);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}

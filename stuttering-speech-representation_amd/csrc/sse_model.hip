@@ -1047,6 +1047,14 @@ int sse_resample(const float* d_in, int B, int L, int orig_freq, int new_freq, f
   return rc == -4 ? SSE_ERR_WORKSPACE : (rc == -1 ? SSE_ERR_INVALID : (rc ? SSE_ERR_HIP : SSE_OK));
 }
 
+int sse_augment(const float* d_in, float* d_out, int B, int L, const int32_t* d_kind, const float* d_factor,
+                const int64_t* d_stream, uint64_t seed, void* stream) {
+  if (!d_in || !d_out || !d_kind || !d_factor || !d_stream) return SSE_ERR_INVALID;
+  const int rc = launch_augment(d_in, d_out, B, L, (const int*)d_kind, d_factor, (const long long*)d_stream, seed,
+                                (hipStream_t)stream);
+  return rc == -1 ? SSE_ERR_INVALID : (rc ? SSE_ERR_HIP : SSE_OK);
+}
+
 int sse_mono(const float* d_in, int B, int C, int L, float* d_out, void* stream) {
   if (!d_in || !d_out) return SSE_ERR_INVALID;
   const int rc = launch_mono(d_in, B, C, L, d_out, (hipStream_t)stream);

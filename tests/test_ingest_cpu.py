@@ -126,3 +126,62 @@ def test_merge_detects_gap(tmp_path):
     w.write(2, [{"filename": "c"}], {"layer_1": np.zeros((1, 2), np.float32)})
     with pytest.raises(ValueError):
         merge_shards(str(tmp_path))
+
+
+def _ref_draws(rng, n, variant):
+    """The random calls of the reference's augment_audio, restated line by line
+    (REF/model_training_1.py:179-200; REF/model_training_01.py:153-181)."""
+    out = []
+    for _ in range(n):
+        if variant == "1":
+            t = rng.choice(['speed', 'noise', 'volume', 'none'])
+            if t == 'speed':
+                f = rng.uniform(0.95, 1.05)
+                out.append((t, f, int(16000 * f)))
+            elif t == 'noise':
+                out.append((t, rng.uniform(0.001, 0.005), 0))
+            elif t == 'volume':
+                out.append((t, rng.uniform(0.9, 1.1), 0))
+            else:
+                out.append((t, 1.0, 0))
+        else:
+            t = rng.choice(['speed', 'noise', 'pitch', 'volume'])
+            if t == 'speed':
+                f = rng.uniform(0.9, 1.1)
+                out.append((t, f, int(16000 * f)))
+            elif t == 'noise':
+                out.append((t, rng.uniform(0.005, 0.02), 0))
+            elif t == 'pitch':
+                out.append((t, float(rng.randint(-2, 2)), 0))
+            else:
+                out.append((t, rng.uniform(0.8, 1.2), 0))
+    return out
+
+
+@pytest.mark.parametrize("variant", ["1", "01"])
+def test_augmentation_draws_follow_reference_rng_order(variant):
+    import random
+    from ssr_amd.augment import draw
+    ref = _ref_draws(random.Random(123), 200, variant)
+    rng = random.Random(123)
+    got = []
+    for _ in range(200):
+        s = draw(rng, variant)
+        got.append((s.kind, float(s.n_steps) if s.kind == "pitch" else s.factor, s.new_sr))
+    assert got == ref
+    assert {k for k, _, _ in got} == set(["speed", "noise", "volume", "none"] if variant == "1"
+                                         else ["speed", "noise", "pitch", "volume"])
+
+
+def test_augment_oracle_ops():
+    from oracle.augment import augment
+    from ssr_amd import synth
+    x = synth.synth_clips(1, 16000, seed=9)[0] * 8          # exceeds +-1 -> clamp matters
+    assert np.abs(augment(x, "none")).max() <= 1.0
+    v = augment(x, "volume", 0.5)
+    assert np.array_equal(v, np.clip(x * np.float32(0.5), -1, 1))
+    z = np.zeros(200000, np.float32)
+    n = augment(z, "noise", 0.004, seed=1, stream=3)
+    assert abs(n.std() - 0.004) < 1e-4 and abs(n.mean()) < 5e-5
+    s = augment(synth.synth_clips(1, 48000, seed=2)[0], "speed", new_sr=int(16000 * 0.97))
+    assert s.shape == (48000,)
