@@ -55,7 +55,7 @@ def test_apply_data_augmentation_matches_sequential(tmp_path):
     for i in range(5):
         p = str(tmp_path / f"f{i}.wav")
         write_wav(p, synth.synth_clips(1, 16000 + 160 * i, seed=50 + i)[0], fmt="float")
-        rows.append({"filename": f"f{i}", "path": p, "label": "rare" if i < 3 else "common"})
+        rows.append({"filename": f"f{i}", "path": p, "label": "rare" if i < 2 else "common"})
     meta = pd.DataFrame(rows)
     model = WavLMModel.from_state_dict(C.WAVLM_BASE, synth.synth_wavlm_state_dict(C.WAVLM_BASE), "cuda:0", "fp32")
     fe = Wav2Vec2FeatureExtractor(do_normalize=False, device="cuda:0")
@@ -64,12 +64,12 @@ def test_apply_data_augmentation_matches_sequential(tmp_path):
     cache = {}
     m2, e2 = apply_data_augmentation(meta, emb, model, fe, "cuda:0", names, "wavlm", augmentation_factor=3,
                                      minority_threshold=3, rng=random.Random(5), seed=9, cache=cache)
-    assert len(m2) == 5 + 9 and e2["layer_12"].shape == (14, 768)
+    assert len(m2) == 5 + 6 and e2["layer_12"].shape == (11, 768)     # class "rare" (2 < 3) x 3
     assert list(m2["filename"][5:8]) == ["f0_aug_0", "f0_aug_1", "f0_aug_2"] and m2["augmented"][5:].all()
     # restate the reference loop batch-1: same draws, oracle augmentation, single-clip embed
     rng = random.Random(5)
     j = 0
-    for i in range(3):
+    for i in range(2):
         clip = synth.synth_clips(1, 16000 + 160 * i, seed=50 + i)[0]
         for a in range(3):
             sp = draw(rng)
@@ -82,4 +82,4 @@ def test_apply_data_augmentation_matches_sequential(tmp_path):
     emb6 = {"layer_6": rng_np.standard_normal((5, 768)).astype(np.float32)}
     m3, e3 = apply_data_augmentation(meta, emb6, model, fe, "cuda:0", names, "wavlm", augmentation_factor=3,
                                      minority_threshold=3, rng=random.Random(999), seed=9, cache=cache)
-    assert e3["layer_6"].shape == (14, 768) and m3["filename"].equals(m2["filename"])
+    assert e3["layer_6"].shape == (11, 768) and m3["filename"].equals(m2["filename"])
