@@ -13,7 +13,9 @@ import os
 from .config import KIND_WAVLM, WavLMSpec, WhisperSpec
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsse.so")
+# SSE_LIB_PATH: load another build of the same ABI (A/B timing of two builds on one box,
+# tools/ab_bench.sh); unset in tests and in the product path.
+LIB_PATH = os.environ.get("SSE_LIB_PATH") or os.path.join(_HERE, "libsse.so")
 
 SSE_DTYPE_F32 = 0
 SSE_DTYPE_BF16 = 1
