@@ -115,7 +115,21 @@ struct GemmArgs {
   int ldc;
   int act;
   const void* zero;     // >= 64 zero bytes of device memory
+  // resid' = LayerNorm(resid) applied in the epilogue from per-row (mean, rstd) and per-column
+  // (w, b): the residual stream then never has to be written normalised in fp32 (post-LN path)
+  const float2* rstats;
+  const float* rln_w;
+  const float* rln_b;
 };
+
+// LayerNorm affine of one 4-column group, the exact expression of layernorm_kernel
+SSE_DEV f32x4 ln_apply4(f32x4 v, float2 st, const float* w, const float* b, int n) {
+  const f32x4 wv = *(const f32x4*)(w + n), bv = *(const f32x4*)(b + n);
+  f32x4 o;
+  #pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = fmaf((v[e] - st.x) * st.y, wv[e], bv[e]);
+  return o;
+}
 
 enum { AMODE_SEG = 0, AMODE_CONV = 1 };
 

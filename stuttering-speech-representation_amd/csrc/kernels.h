@@ -16,9 +16,10 @@ int launch_conv0_raw(const float* x, int B, int L, const float* norm, const floa
 
 template <typename TI, typename TO>
 int launch_layernorm(const TI* in, const float* w, const float* b, int rows, int H, float eps, int act,
-                     float* out_f, TO* out_t, hipStream_t s);
+                     float* out_f, TO* out_t, hipStream_t s, float2* stats = nullptr);
 
-int launch_pool_mean(const float* x, int B, int T, int H, float* out, long long out_stride, hipStream_t s);
+int launch_pool_mean(const float* x, int B, int T, int H, float* out, long long out_stride, hipStream_t s,
+                     const float2* st = nullptr, const float* w = nullptr, const float* b = nullptr);
 
 struct AttnArgs {
   const void* qkv;       // [B*T][ldq]  (q | k | v | WavLM gate projection | pad), element type T

@@ -275,6 +275,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
         if (has_res) {
           const long long ro = g.resid_rows ? (long long)((ok[u] ? m : 0) % g.resid_rows) * g.ldc + col0 + n : off[u];
           rv[u] = *(const f32x4*)(g.resid + ro);
+          if (g.rstats) rv[u] = ln_apply4(rv[u], g.rstats[ok[u] ? m : 0], g.rln_w, g.rln_b, col0 + n);
         }
       }
       #pragma unroll

@@ -240,33 +240,48 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
           for (int r = 0; r < 4; ++r)
             Cs[(wm * 64 + i * 16 + q * 4 + r) * G8_CLD + ni * 128 + wn * 32 + j * 16 + r16] = acc[mi][ni][i][j][r];
     __syncthreads();
+    // chunk c = base + u*512 has column group (c & 63), fixed per thread: the column operands
+    // (bias, LayerNorm w/b of the residual) are loaded once, only rows vary
+    const int cc = (threadIdx.x & 63) * 4, n = n0 + cc;
+    const f32x4 bv = has_bias ? *(const f32x4*)(g.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 lw = f32x4{1.f, 1.f, 1.f, 1.f}, lb = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (g.rstats) {
+      lw = *(const f32x4*)(g.rln_w + n);
+      lb = *(const f32x4*)(g.rln_b + n);
+    }
     for (int base = threadIdx.x; base < CH; base += 512 * UNR) {
-      f32x4 v[UNR], rv[UNR], bv[UNR];
+      f32x4 v[UNR], rv[UNR];
+      float2 st[UNR];
       long long off[UNR];
       bool ok[UNR];
       #pragma unroll
       for (int u = 0; u < UNR; ++u) {
-        const int c = base + u * 512;
-        const int row = c >> 6, cc = (c & 63) * 4;
-        const int m = m0 + mi * 128 + row, n = n0 + cc;
+        const int row = (base + u * 512) >> 6;
+        const int m = m0 + mi * 128 + row;
         ok[u] = m < M;
         off[u] = (long long)(ok[u] ? m : 0) * g.ldc + n;
         v[u] = *(const f32x4*)(Cs + row * G8_CLD + cc);
-        bv[u] = has_bias ? *(const f32x4*)(g.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
         rv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        st[u] = make_float2(0.f, 1.f);
         if (has_res) {
           const long long ro = g.resid_rows ? (long long)((ok[u] ? m : 0) % g.resid_rows) * g.ldc + n : off[u];
           rv[u] = *(const f32x4*)(g.resid + ro);
+          if (g.rstats) st[u] = g.rstats[ok[u] ? m : 0];
         }
       }
       #pragma unroll
       for (int u = 0; u < UNR; ++u) {
-        f32x4 o = v[u] + bv[u];
+        f32x4 o = v[u] + bv;
         if (gelu) {
           const f32x2 lo = gelu_erf2(f32x2{o[0], o[1]}), hi = gelu_erf2(f32x2{o[2], o[3]});
           o = f32x4{lo.x, lo.y, hi.x, hi.y};
         }
-        o += rv[u];
+        f32x4 r = rv[u];
+        if (g.rstats) {   // LayerNorm of the residual, the exact expression of layernorm_kernel
+          #pragma unroll
+          for (int e = 0; e < 4; ++e) r[e] = fmaf((r[e] - st[u].x) * st[u].y, lw[e], lb[e]);
+        }
+        o += r;
         if (ok[u]) {
           if (g.Cf) *(f32x4*)(g.Cf + off[u]) = o;
           if (g.Ct) {

@@ -234,7 +234,7 @@ template <typename TI, typename TO>
 __global__ __launch_bounds__(256) void layernorm_kernel(const TI* __restrict__ in, const float* __restrict__ w,
                                                         const float* __restrict__ bta, int rows, int H,
                                                         float eps, int act, float* __restrict__ out_f,
-                                                        TO* __restrict__ out_t) {
+                                                        TO* __restrict__ out_t, float2* __restrict__ stats) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int lane = threadIdx.x & 63;
@@ -261,6 +261,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TI* __restrict__ i
         q = fmaf(d, d, q);
       }
   const float rstd = 1.0f / sqrtf(wave_sum(q) / H + eps);
+  if (stats && lane == 0) stats[row] = make_float2(mean, rstd);
   #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int g = lane + 64 * i;
@@ -270,7 +271,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TI* __restrict__ i
       f32x4 o;
       #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        float y = (v[i][e] - mean) * rstd * wv[e] + bv[e];
+        float y = fmaf((v[i][e] - mean) * rstd, wv[e], bv[e]);   // = ln_apply4 (common.h)
         o[e] = act == ACT_GELU ? gelu_erf(y) : y;
       }
       const long long off = (long long)row * H + c;
@@ -289,33 +290,51 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TI* __restrict__ i
 
 template <typename TI, typename TO>
 int launch_layernorm(const TI* in, const float* w, const float* b, int rows, int H, float eps, int act,
-                     float* out_f, TO* out_t, hipStream_t s) {
+                     float* out_f, TO* out_t, hipStream_t s, float2* stats) {
   if (H % 4 || H > 2048) return -3;
   hipLaunchKernelGGL((layernorm_kernel<TI, TO>), dim3((rows + 3) / 4), dim3(256), 0, s, in, w, b, rows, H, eps,
-                     act, out_f, out_t);
+                     act, out_f, out_t, stats);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 template int launch_layernorm<float, float>(const float*, const float*, const float*, int, int, float, int,
-                                            float*, float*, hipStream_t);
+                                            float*, float*, hipStream_t, float2*);
 template int launch_layernorm<float, bf16>(const float*, const float*, const float*, int, int, float, int,
-                                           float*, bf16*, hipStream_t);
+                                           float*, bf16*, hipStream_t, float2*);
 template int launch_layernorm<bf16, bf16>(const bf16*, const float*, const float*, int, int, float, int, float*,
-                                          bf16*, hipStream_t);
+                                          bf16*, hipStream_t, float2*);
 
 // ---------------------------------------------------------------------------------------
 // K8/K12: out[b*out_stride + n] = mean_t x[b][t][n]  (torch.mean(hs, dim=1), fp64 accumulation).
+// Block = 64 columns x 4 waves; wave w sums frames t = w, w+4, ... (fp64), LDS combine.  With
+// stats, each element is first normalised exactly as layernorm_kernel would have written it.
 __global__ __launch_bounds__(256) void pool_mean_kernel(const float* __restrict__ x, int T, int H,
-                                                        float* __restrict__ out, long long out_stride) {
-  const int n = blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
-  if (n >= H) return;
-  const float* xb = x + (long long)b * T * H + n;
+                                                        float* __restrict__ out, long long out_stride,
+                                                        const float2* __restrict__ st, const float* __restrict__ w,
+                                                        const float* __restrict__ bb) {
+  __shared__ double part[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + lane, b = blockIdx.y;
   double s = 0.0;
-  for (int t = 0; t < T; ++t) s += xb[(long long)t * H];
-  out[b * out_stride + n] = (float)(s / T);
+  if (n < H) {
+    const float* xb = x + (long long)b * T * H + n;
+    const float wn = st ? w[n] : 1.f, bn = st ? bb[n] : 0.f;
+    for (int t = wv; t < T; t += 4) {
+      float v = xb[(long long)t * H];
+      if (st) {
+        const float2 q = st[(long long)b * T + t];
+        v = fmaf((v - q.x) * q.y, wn, bn);
+      }
+      s += v;
+    }
+  }
+  part[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && n < H) out[b * out_stride + n] = (float)((part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]) / T);
 }
 
-int launch_pool_mean(const float* x, int B, int T, int H, float* out, long long out_stride, hipStream_t s) {
-  hipLaunchKernelGGL(pool_mean_kernel, dim3((H + 255) / 256, B), dim3(256), 0, s, x, T, H, out, out_stride);
+int launch_pool_mean(const float* x, int B, int T, int H, float* out, long long out_stride, hipStream_t s,
+                     const float2* st, const float* w, const float* b) {
+  hipLaunchKernelGGL(pool_mean_kernel, dim3((H + 63) / 64, B), dim3(256), 0, s, x, T, H, out, out_stride, st, w, b);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

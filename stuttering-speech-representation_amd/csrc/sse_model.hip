@@ -421,7 +421,7 @@ int wavlm_frames(const sse_cfg& c, int L, int* Ts) {
 }
 
 struct WavlmWs {
-  size_t zero, norm, part, ss, bufA, bufB, x, xt, xb, qkv, ctx, ff, hf;
+  size_t zero, norm, part, ss, bufA, bufB, x, xt, xb, qkv, ctx, ff, hf, st1, st2;
 };
 
 WavlmWs wavlm_plan(const sse_model* m, int B, int L, Plan& p) {
@@ -451,6 +451,8 @@ WavlmWs wavlm_plan(const sse_model* m, int B, int L, Plan& p) {
   w.ctx = p.add(M * H * es);
   w.ff = p.add(M * (size_t)c.ffn * es);
   w.hf = c.stable_layer_norm ? p.add(M * H * 4) : 0;
+  w.st1 = p.add(M * 8);        // per-row LayerNorm (mean, rstd): post-LN bf16 path
+  w.st2 = p.add(M * 8);
   return w;
 }
 
@@ -509,6 +511,16 @@ struct Sink {
       if (hipMemcpyAsync(hs + (size_t)idx * B * T * H, x, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
         return SSE_ERR_HIP;
     }
+    return 0;
+  }
+  // hidden state = LayerNorm(x) with per-row stats st already computed (x itself un-normalised)
+  int emit_ln(int idx, const float* x, const float2* st, const float* w, const float* b, float eps) const {
+    for (int i = 0; i < n_ids; ++i)
+      if (ids[i] == idx)
+        RC(launch_pool_mean(x, B, T, H, pooled + (size_t)i * H, (long long)n_ids * H, s, st, w, b));
+    if (hs)
+      RC((launch_layernorm<float, float>(x, w, b, B * T, H, eps, ACT_NONE, hs + (size_t)idx * B * T * H,
+                                         (float*)nullptr, s)));
     return 0;
   }
 };
@@ -593,6 +605,13 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
   T* ctx = (T*)(ws + w.ctx);
   T* ff = (T*)(ws + w.ff);
   float* hf = c.stable_layer_norm ? (float*)(ws + w.hf) : nullptr;
+  // bf16 post-LN: LayerNorm outputs are never written in fp32; the residual-adding GEMMs and
+  // the embedding pool re-normalise on the fly from per-row (mean, rstd) (bit-identical values).
+  // SSE_NO_LNFOLD=1 restores the materialised flow (A/B and equality tests).
+  const char* nlf = getenv("SSE_NO_LNFOLD");
+  const bool lnfold = sizeof(T) == 2 && !c.stable_layer_norm && !(nlf && nlf[0] == '1');
+  float2* st1 = (float2*)(ws + w.st1);
+  float2* st2 = (float2*)(ws + w.st2);
   for (int l = 0; l < c.layers; ++l) {
     const LayerW& Lw = m->layers[l];
     if (c.stable_layer_norm)
@@ -612,8 +631,14 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     g = GemmArgs{};
     g.A = ctx; g.B = m->ptr(Lw.o_w); g.M = M; g.N = H; g.K = H; g.rows_per_seg = M; g.lda = H;
     g.bias = m->ptr<float>(Lw.o_b); g.resid = x; g.Cf = x; g.ldc = H; g.zero = zero;
+    if (lnfold && l > 0) {   // x holds the previous layer's un-normalised sum: LN2 applied here
+      g.rstats = st2; g.rln_w = m->ptr<float>(m->layers[l - 1].ln2_w); g.rln_b = m->ptr<float>(m->layers[l - 1].ln2_b);
+    }
     RC(prof(m, s, "gemm:oproj", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
-    if (!c.stable_layer_norm) {
+    if (lnfold) {
+      RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, ACT_NONE,
+                                     nullptr, xb, s, st1)));
+    } else if (!c.stable_layer_norm) {
       RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, ACT_NONE, x,
                                      xb, s)));
     } else {
@@ -627,7 +652,14 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     g = GemmArgs{};
     g.A = ff; g.B = m->ptr(Lw.f2_w); g.M = M; g.N = H; g.K = F; g.rows_per_seg = M; g.lda = F;
     g.bias = m->ptr<float>(Lw.f2_b); g.resid = x; g.Cf = x; g.ldc = H; g.zero = zero;
+    if (lnfold) { g.rstats = st1; g.rln_w = m->ptr<float>(Lw.ln1_w); g.rln_b = m->ptr<float>(Lw.ln1_b); }
     RC(prof(m, s, "gemm:ffn2", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    if (lnfold) {
+      RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, H, eps, ACT_NONE,
+                                     nullptr, xb, s, st2)));
+      RC(sink.emit_ln(l + 1, x, st2, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), eps));
+      continue;
+    }
     if (!c.stable_layer_norm) {
       RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, H, eps, ACT_NONE, x,
                                      xb, s)));

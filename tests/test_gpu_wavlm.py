@@ -135,3 +135,22 @@ def test_wavlm_large_matches_reference(dtype, tol):
     rel = _rel(got, g["emb"])
     print(dtype, "wavlm-large rel", rel.max())
     assert rel.max() <= tol and _cos(got, g["emb"]).min() >= BF16_COS
+
+
+def test_bf16_lnfold_bit_identical(monkeypatch, wavlm_sd):
+    """The bf16 post-LN path never writes LayerNorm outputs in fp32: the residual GEMMs and the
+    pool re-normalise from per-row (mean, rstd).  It must reproduce the materialised flow
+    (SSE_NO_LNFOLD=1) bit for bit, pooled embeddings and every hidden state."""
+    from ssr_amd import config as C, synth
+    from ssr_amd.model import SSEModel
+    m = SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype="bf16")
+    w = torch.from_numpy(synth.synth_clips(6, 48000, seed=21)).cuda()
+    idx = list(range(13))
+    a = m.embed(w, idx).clone()
+    ha = [h.clone() for h in m.hidden_states(w[:2])]
+    monkeypatch.setenv("SSE_NO_LNFOLD", "1")
+    b = m.embed(w, idx)
+    hb = m.hidden_states(w[:2])
+    assert torch.equal(a, b)
+    for x, y in zip(ha, hb):
+        assert torch.equal(x, y)
