@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 typedef __bf16 bf16;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -63,6 +64,28 @@ SSE_DEV f32x2 gelu_erf2(f32x2 x) {
   return f32x2{x.x >= 0.f ? pos.x : h.x, x.y >= 0.f ? pos.y : h.y};
 }
 
+// GELU for the bf16 path (its result is rounded to bf16, relative step 2^-8): gelu(x) = x * Phi(x)
+// with Phi(x) = 1 / (1 + 2^(x * P(min(x^2, 25)))), P a degree-6 minimax fit of
+// -log2(e) * logit(Phi(x)) / x on |x| <= 5 (tools/fit_gelu.py).  Odd in the exponent, so
+// branch-free on both tails.  Error against the exact erf-GELU (fp32 evaluation, 4M points on
+// [-12, 12]): absolute <= 7.3e-7, relative <= 4.8e-5 wherever |gelu| > 1e-3 — 80x below the bf16
+// rounding step.  Cost per pair: 9 packed VALU + 2 v_exp + 2 v_rcp, against 17 packed VALU +
+// 2 v_exp + 2 v_rcp + compare/select for gelu_erf2.  The fp32 path keeps gelu_erf.
+SSE_DEV f32x2 gelu_sig2(f32x2 x) {
+  f32x2 s = x * x;
+  s = f32x2{fminf(s.x, 25.f), fminf(s.y, 25.f)};
+  f32x2 p = {-5.244055156e-09f, -5.244055156e-09f};
+  p = __builtin_elementwise_fma(p, s, f32x2{3.856162590e-07f, 3.856162590e-07f});
+  p = __builtin_elementwise_fma(p, s, f32x2{-1.144617894e-05f, -1.144617894e-05f});
+  p = __builtin_elementwise_fma(p, s, f32x2{1.592489983e-04f, 1.592489983e-04f});
+  p = __builtin_elementwise_fma(p, s, f32x2{9.618200986e-05f, 9.618200986e-05f});
+  p = __builtin_elementwise_fma(p, s, f32x2{-1.048389829e-01f, -1.048389829e-01f});
+  p = __builtin_elementwise_fma(p, s, f32x2{-2.302207293e+00f, -2.302207293e+00f});
+  const f32x2 u = x * p;
+  const f32x2 d = f32x2{__builtin_amdgcn_exp2f(u.x), __builtin_amdgcn_exp2f(u.y)} + 1.0f;
+  return x * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+
 template <typename T> SSE_DEV T from_f32(float v);
 template <> SSE_DEV float from_f32<float>(float v) { return v; }
 template <> SSE_DEV bf16 from_f32<bf16>(float v) { return (bf16)v; }
@@ -86,7 +109,14 @@ SSE_DEV double wave_sum_d(double v) {
 }
 
 // Epilogue activation codes.
-enum { ACT_NONE = 0, ACT_GELU = 1 };
+// ACT_GELU_FAST: gelu_sig2, used by the bf16 path only (host picks it, see gelu_act<T>()).
+enum { ACT_NONE = 0, ACT_GELU = 1, ACT_GELU_FAST = 2 };
+
+// SSE_GELU_EXACT=1 keeps the erf form on the bf16 path too (A/B runs, equality tests).
+inline bool gelu_exact_env() {
+  static const bool exact = [] { const char* e = getenv("SSE_GELU_EXACT"); return e && e[0] == '1'; }();
+  return exact;
+}
 
 // ---------------------------------------------------------------------------------------
 // GEMM descriptor.  C[m][n] = sum_k A(m, k) * Bt[n][k]  (+bias[n]) (act) (+resid[m][n]).

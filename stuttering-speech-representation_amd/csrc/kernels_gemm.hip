@@ -243,7 +243,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
   constexpr int CH = EPI_ROWS * BN / 4;       // 16-B chunks per epilogue chunk
   constexpr int UNR = 4;
   const int col0 = grp * N;
-  const bool has_bias = g.bias != nullptr, has_res = g.resid != nullptr, gelu = g.act == ACT_GELU;
+  const bool has_bias = g.bias != nullptr, has_res = g.resid != nullptr, gelu = g.act == ACT_GELU, gelu_fast = g.act == ACT_GELU_FAST;
   #pragma unroll
   for (int half = 0; half < BM / EPI_ROWS; ++half) {
     __syncthreads();                          // operand stages (or the previous chunk) fully consumed
@@ -283,6 +283,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
         f32x4 o = v[u] + bv[u];
         if (gelu) {   // packed-fp32 erf-GELU, bit-identical to the scalar form
           const f32x2 lo = gelu_erf2(f32x2{o[0], o[1]}), hi = gelu_erf2(f32x2{o[2], o[3]});
+          o = f32x4{lo.x, lo.y, hi.x, hi.y};
+        }
+        if (gelu_fast) {
+          const f32x2 lo = gelu_sig2(f32x2{o[0], o[1]}), hi = gelu_sig2(f32x2{o[2], o[3]});
           o = f32x4{lo.x, lo.y, hi.x, hi.y};
         }
         o += rv[u];

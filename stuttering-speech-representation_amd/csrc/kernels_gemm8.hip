@@ -226,7 +226,7 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
   float* Cs = (float*)smem;
   constexpr int CH = 128 * 256 / 4;
   constexpr int UNR = 4;
-  const bool has_bias = g.bias != nullptr, has_res = g.resid != nullptr, gelu = g.act == ACT_GELU;
+  const bool has_bias = g.bias != nullptr, has_res = g.resid != nullptr, gelu = g.act == ACT_GELU, gelu_fast = g.act == ACT_GELU_FAST;
   #pragma unroll
   for (int mi = 0; mi < 2; ++mi) {
     __syncthreads();
@@ -274,6 +274,10 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
         f32x4 o = v[u] + bv;
         if (gelu) {
           const f32x2 lo = gelu_erf2(f32x2{o[0], o[1]}), hi = gelu_erf2(f32x2{o[2], o[3]});
+          o = f32x4{lo.x, lo.y, hi.x, hi.y};
+        }
+        if (gelu_fast) {
+          const f32x2 lo = gelu_sig2(f32x2{o[0], o[1]}), hi = gelu_sig2(f32x2{o[2], o[3]});
           o = f32x4{lo.x, lo.y, hi.x, hi.y};
         }
         f32x4 r = rv[u];

@@ -121,7 +121,7 @@ __global__ void gn_finalize_kernel(const double* __restrict__ mom, int B, int C,
   ss[i] = make_float2(sc, beta[c] - (float)mean * sc);
 }
 
-template <typename TO, bool RAW>
+template <typename TO, bool RAW, bool FAST>
 __global__ __launch_bounds__(256) void conv0_apply_kernel(const float* __restrict__ x, int L,
                                                           const float* __restrict__ norm,
                                                           const float* __restrict__ w0, const float* __restrict__ b0,
@@ -168,7 +168,10 @@ __global__ __launch_bounds__(256) void conv0_apply_kernel(const float* __restric
       }
       if (!RAW) {
         #pragma unroll
-        for (int p = 0; p < 4; ++p) y[p] = gelu_erf2(__builtin_elementwise_fma(y[p], sc[p], sh[p]));
+        for (int p = 0; p < 4; ++p) {
+          const f32x2 z = __builtin_elementwise_fma(y[p], sc[p], sh[p]);
+          y[p] = FAST ? gelu_sig2(z) : gelu_erf2(z);
+        }
       }
       if constexpr (sizeof(TO) == 2) {
         const bf16x8 o8 = {(bf16)y[0].x, (bf16)y[0].y, (bf16)y[1].x, (bf16)y[1].y,
@@ -194,7 +197,10 @@ int launch_conv0_gn(const float* x, int B, int L, const float* norm, const float
                      beta, eps, ss);
   if (C % 8) return -3;
   dim3 grid((T0 + C0_T - 1) / C0_T, B), block(256);
-  hipLaunchKernelGGL((conv0_apply_kernel<TO, false>), grid, block, 0, s, x, L, norm, w0, b0, C, T0, ss, out);
+  if (sizeof(TO) == 2 && !gelu_exact_env())   // bf16 output: gelu_sig2 (common.h)
+    hipLaunchKernelGGL((conv0_apply_kernel<TO, false, true>), grid, block, 0, s, x, L, norm, w0, b0, C, T0, ss, out);
+  else
+    hipLaunchKernelGGL((conv0_apply_kernel<TO, false, false>), grid, block, 0, s, x, L, norm, w0, b0, C, T0, ss, out);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -205,7 +211,7 @@ int launch_conv0_raw(const float* x, int B, int L, const float* norm, const floa
   if (k0 != K0 || s0 != 5) return -3;
   if (C % 8) return -3;
   dim3 grid((T0 + C0_T - 1) / C0_T, B), block(256);
-  hipLaunchKernelGGL((conv0_apply_kernel<TO, true>), grid, block, 0, s, x, L, norm, w0, b0, C, T0,
+  hipLaunchKernelGGL((conv0_apply_kernel<TO, true, false>), grid, block, 0, s, x, L, norm, w0, b0, C, T0,
                      (const float2*)nullptr, out);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

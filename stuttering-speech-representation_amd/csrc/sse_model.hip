@@ -525,6 +525,17 @@ struct Sink {
   }
 };
 
+// GELU of a GEMM epilogue whose output is rounded to the element type: the bf16 path uses the
+// cheaper gelu_sig2 (error 80x below the bf16 step, common.h); fp32 keeps the exact erf form.
+template <typename T>
+int gelu_rounded_act() {
+  if constexpr (sizeof(T) == 2) {
+    return gelu_exact_env() ? ACT_GELU : ACT_GELU_FAST;
+  } else {
+    return ACT_GELU;
+  }
+}
+
 template <typename T>
 int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sink, char* ws, hipStream_t s) {
   const sse_cfg& c = m->cfg;
@@ -566,7 +577,7 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     g.M = B * Ts[i]; g.N = co; g.K = k * cin;
     g.rows_per_seg = Ts[i]; g.seg_stride = (long long)Ts[i - 1] * cin; g.lda = (long long)st * cin;
     g.bias = m->conv_b[i] ? m->ptr<float>(m->conv_b[i]) : nullptr;
-    g.Ct = bufs[i & 1]; g.ldc = co; g.act = c.feat_norm_layer ? ACT_NONE : ACT_GELU; g.zero = zero;
+    g.Ct = bufs[i & 1]; g.ldc = co; g.act = c.feat_norm_layer ? ACT_NONE : gelu_rounded_act<T>(); g.zero = zero;
     RC(prof(m, s, "gemm:conv", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     if (c.feat_norm_layer)
       RC((launch_layernorm<T, T>(bufs[i & 1], m->ptr<float>(m->conv_ln_w[i]), m->ptr<float>(m->conv_ln_b[i]),
@@ -647,7 +658,7 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     }
     g = GemmArgs{};
     g.A = xb; g.B = m->ptr(Lw.f1_w); g.M = M; g.N = F; g.K = H; g.rows_per_seg = M; g.lda = H;
-    g.bias = m->ptr<float>(Lw.f1_b); g.Ct = ff; g.ldc = F; g.act = ACT_GELU; g.zero = zero;
+    g.bias = m->ptr<float>(Lw.f1_b); g.Ct = ff; g.ldc = F; g.act = gelu_rounded_act<T>(); g.zero = zero;
     RC(prof(m, s, "gemm:ffn1", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     g = GemmArgs{};
     g.A = ff; g.B = m->ptr(Lw.f2_w); g.M = M; g.N = H; g.K = F; g.rows_per_seg = M; g.lda = F;
@@ -725,7 +736,7 @@ int whisper_decoder(sse_model* m, const T* enc, int B, const Sink& sink, char* w
     // feed-forward
     RC((launch_layernorm<float, T>(x, m->ptr<float>(W.ln3_w), m->ptr<float>(W.ln3_b), B, D, eps, ACT_NONE, nullptr,
                                    xb, s)));
-    RC(lin("dec_gemm:fc1", xb, W.f1_w, W.f1_b, Fd, D, nullptr, nullptr, ff, ACT_GELU));
+    RC(lin("dec_gemm:fc1", xb, W.f1_w, W.f1_b, Fd, D, nullptr, nullptr, ff, gelu_rounded_act<T>()));
     RC(lin("dec_gemm:fc2", ff, W.f2_w, W.f2_b, D, Fd, x, x, nullptr, ACT_NONE));
     if (l + 1 < c.decoder_layers) RC(sink.emit(l + 1, x));
   }
@@ -759,7 +770,7 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
     GemmArgs g{};   // conv1: k3 pad1, 80 -> D, GELU
     g.A = mel; g.B = m->ptr(m->c1_w); g.M = B * T2; g.N = D; g.K = 3 * nm;
     g.rows_per_seg = T2; g.T_in = T2; g.stride = 1; g.pad = 1; g.cin = nm; g.ld_in = nm;
-    g.bias = m->ptr<float>(m->c1_b); g.Ct = h1; g.ldc = D; g.act = ACT_GELU; g.zero = zero;
+    g.bias = m->ptr<float>(m->c1_b); g.Ct = h1; g.ldc = D; g.act = gelu_rounded_act<T>(); g.zero = zero;
     RC(prof(m, s, "gemm_conv:conv1", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_CONV, 1, s); }));
     g = GemmArgs{};   // conv2: k3 s2 pad1, GELU, + embed_positions
     g.A = h1; g.B = m->ptr(m->c2_w); g.M = M; g.N = D; g.K = 3 * D;
@@ -791,7 +802,7 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
                                    xb, s)));
     g = GemmArgs{};
     g.A = xb; g.B = m->ptr(Lw.f1_w); g.M = M; g.N = F; g.K = D; g.rows_per_seg = M; g.lda = D;
-    g.bias = m->ptr<float>(Lw.f1_b); g.Ct = ff; g.ldc = F; g.act = ACT_GELU; g.zero = zero;
+    g.bias = m->ptr<float>(Lw.f1_b); g.Ct = ff; g.ldc = F; g.act = gelu_rounded_act<T>(); g.zero = zero;
     RC(prof(m, s, "gemm:ffn1", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     g = GemmArgs{};
     g.A = ff; g.B = m->ptr(Lw.f2_w); g.M = M; g.N = D; g.K = F; g.rows_per_seg = M; g.lda = F;

@@ -270,7 +270,8 @@ _ZERO = {}
 def gemm(a: torch.Tensor, b: torch.Tensor, bias=None, resid=None, act: str | None = None,
          out_dtype=torch.float32) -> torch.Tensor:
     """The path's MFMA GEMM on its own: a [M, K] @ b[N, K]^T (+bias) (gelu) (+resid).
-    a, b both bf16 (bf16 MFMA) or both fp32 (exact-f32 MFMA)."""
+    a, b both bf16 (bf16 MFMA) or both fp32 (exact-f32 MFMA).  act: None | "gelu" (erf form) |
+    "gelu_fast" (the bf16 path's gelu_sig2 epilogue, common.h)."""
     if a.dtype != b.dtype or a.dtype not in (torch.bfloat16, torch.float32):
         raise TypeError("a and b must both be bf16 or both fp32")
     M, K = a.shape
@@ -287,7 +288,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, bias=None, resid=None, act: str | Non
     res_p = resid.contiguous().data_ptr() if resid is not None else None
     _lib.check(_lib.lib().sse_gemm(dt, a.data_ptr(), b.data_ptr(), bias_p, res_p,
                                    cf.data_ptr() if cf is not None else None,
-                                   ct.data_ptr() if ct is not None else None, M, N, K, 1 if act == "gelu" else 0,
+                                   ct.data_ptr() if ct is not None else None, M, N, K, {None: 0, "gelu": 1, "gelu_fast": 2}[act],
                                    z.data_ptr(), ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
                "sse_gemm")
     return cf if cf is not None else ct
