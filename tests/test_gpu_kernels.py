@@ -105,3 +105,47 @@ def test_fast_gelu_pointwise():
     assert err.max().item() <= 1e-6, err.max().item()
     m = ref.abs() > 1e-3
     assert (err[m] / ref[m].abs()).max().item() <= 1e-4
+
+
+@pytest.mark.parametrize("M,N,K", [(16421, 1024, 64), (16421, 1024, 128), (16421, 768, 192), (16384, 1024, 256),
+                                   (16421, 1024, 768), (9000, 2560, 768), (300, 512, 512)])
+@pytest.mark.parametrize("epi", ["plain", "bias_gelu_fast", "bias_f32_and_bf16"])
+def test_gemm_persistent_agrees(monkeypatch, M, N, K, epi):
+    """The persistent 8-phase kernel (default for GEMMs without a residual: blocks walk several
+    tiles, the next tile's prologue is issued before this tile's stores, which stay in flight)
+    against the non-persistent kernel (SSE_GEMM_PERSIST=0) and the 2-stage kernel
+    (SSE_GEMM_CFG=3): bit-identical.  Tile counts above the CU count, ragged M, K-tile counts
+    1, 2, 3, 4, 12 and every output combination."""
+    from ssr_amd.model import gemm
+    from ssr_amd import _lib
+    import ctypes
+    g = torch.Generator(device="cuda").manual_seed(M + N + 7 * K)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    b = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    bias = torch.randn(N, device="cuda", generator=g) if epi != "plain" else None
+    act = "gelu_fast" if epi == "bias_gelu_fast" else None
+
+    def run():
+        if epi != "bias_f32_and_bf16":
+            return (gemm(a, b, bias, None, act, out_dtype=torch.bfloat16),)
+        cf = torch.empty(M, N, device="cuda")
+        ct = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        z = torch.zeros(64, device="cuda")
+        _lib.check(_lib.lib().sse_gemm(_lib.SSE_DTYPE_BF16, a.data_ptr(), b.data_ptr(), bias.data_ptr(), None,
+                                       cf.data_ptr(), ct.data_ptr(), M, N, K, 0, z.data_ptr(),
+                                       ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "sse_gemm")
+        return cf, ct
+
+    outs = []
+    for env in ({}, {"SSE_GEMM_PERSIST": "0"}, {"SSE_GEMM_CFG": "3"}):
+        for k in ("SSE_GEMM_PERSIST", "SSE_GEMM_CFG"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        outs.append(run())
+        torch.cuda.synchronize()
+    ref = _ref(a, b, bias, None, "gelu" if act else None)
+    assert ((outs[0][0].float() - ref).norm() / ref.norm()).item() <= 5e-3
+    for o in outs[1:]:
+        for x, y in zip(outs[0], o):
+            assert torch.equal(x, y)
