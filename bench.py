@@ -84,6 +84,27 @@ def cpu_baseline(model_name: str, n: int, seconds: float):
                       f"(numpy fp32, {threads} BLAS threads, host {os.cpu_count()} CPUs), {dt:.1f} s"}
 
 
+# rocprofv3 PMC traffic per kernel (tools/pmc_traffic.sh: FETCH_SIZE x2 + WRITE_SIZE per launch),
+# measured on the same workload; kernel symbols of each bench tag prefix
+TRAFFIC_FILE = {("wavlm-base", "bf16"): "profiles/r1_pmc_traffic_wavlm_base_bf16.json"}
+TAG_SYMBOLS = {"gemm": ("gemm8_kernel", "gemm8p_kernel"), "attn": ("attention_",), "conv0_gn": ("conv0_apply",)}
+
+
+def pmc_traffic(model_name, dtype, kernel, launch_counts):
+    """Launch-weighted mean HBM bytes per launch of the kernels behind a bench tag, or None."""
+    path = TRAFFIC_FILE.get((model_name, dtype))
+    if not path or not os.path.exists(os.path.join(ROOT, path)):
+        return None, None
+    with open(os.path.join(ROOT, path)) as fh:
+        ks = json.load(fh)["kernels"]
+    pats = TAG_SYMBOLS.get(kernel, (kernel,))
+    sel = [v for k, v in ks.items() if any(p in k for p in pats)]
+    n = sum(v["launches"] for v in sel)
+    if not n:
+        return None, path
+    return sum(v["hbm_bytes_per_launch"] * v["launches"] for v in sel) / n, path
+
+
 def roofline(records, dtype):
     """Dominant kernel over the timed region: the kernel symbol (tag prefix) with most time."""
     by_kernel = {}
@@ -110,7 +131,7 @@ def roofline(records, dtype):
              for k, v in sorted(by_role.items())}
     return {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": None,
-            "flop_per_launch": fl / n, "mean_launch_ms": round(ms / n, 4), "launches": n,
+            "alg_bytes_per_launch": by / n, "flop_per_launch": fl / n, "mean_launch_ms": round(ms / n, 4), "launches": n,
             "device_ms_per_step_sum": None, "breakdown": breakdown, "roles": roles}
 
 
@@ -187,6 +208,10 @@ def main():
         if records:
             rf = roofline(records, a.dtype)
             rf["device_ms_per_step_sum"] = round(sum(r[1] for r in records) / a.steps, 3)
+            tr, src = pmc_traffic(spec.name, a.dtype, rf["kernel"], None)
+            if tr is not None:
+                rf["traffic"] = round(tr)
+                rf["traffic_source"] = src + " (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE, bytes per launch)"
             res["roofline"] = rf
         res["model_flops_frac"] = round(value / world * FLOP_PER_CLIP[a.model] / 1e12 / PEAK_TFLOPS[a.dtype], 4)
         ncpu = a.cpu_sample if a.cpu_sample is not None else (48 if wavlm else 2)   # ~10-30 s of CPU work

@@ -409,6 +409,24 @@ int prof(sse_model* m, hipStream_t s, const char* tag, double flops, double byte
 
 inline double gflops(const GemmArgs& g, int groups = 1) { return 2.0 * g.M * (double)g.N * g.K * groups; }
 
+// Algorithmic HBM bytes of one GEMM launch: every operand element read once, every output written
+// once.  A counts unique elements: strided-conv SEG rows overlap (a segment spans seg_stride),
+// CONV-mode rows read a [T_in][ld_in] segment per clip.
+template <typename T>
+double gbytes(const GemmArgs& g, int amode = AMODE_SEG, int groups = 1) {
+  const double e = sizeof(T);
+  const double segs = g.rows_per_seg > 0 ? (double)((g.M + g.rows_per_seg - 1) / g.rows_per_seg) : 1.0;
+  double a;
+  if (amode == AMODE_CONV) a = segs * g.T_in * (double)g.ld_in * e;
+  else if (g.lda != g.K) a = segs * (double)g.seg_stride * e;
+  else a = (double)g.M * g.K * e;
+  const double mn = (double)g.M * g.N * groups;
+  const double b = (double)g.N * g.K * groups * e;
+  const double c = mn * ((g.Cf ? 4.0 : 0.0) + (g.Ct ? e : 0.0));
+  const double r = g.resid ? (g.resid_rows ? (double)g.resid_rows * g.N * groups * 4.0 : mn * 4.0) : 0.0;
+  return a + b + c + r;
+}
+
 int wavlm_frames(const sse_cfg& c, int L, int* Ts) {
   int t = L;
   for (int i = 0; i < c.n_conv; ++i) {
@@ -578,7 +596,7 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     g.rows_per_seg = Ts[i]; g.seg_stride = (long long)Ts[i - 1] * cin; g.lda = (long long)st * cin;
     g.bias = m->conv_b[i] ? m->ptr<float>(m->conv_b[i]) : nullptr;
     g.Ct = bufs[i & 1]; g.ldc = co; g.act = c.feat_norm_layer ? ACT_NONE : gelu_rounded_act<T>(); g.zero = zero;
-    RC(prof(m, s, "gemm:conv", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    RC(prof(m, s, "gemm:conv", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     if (c.feat_norm_layer)
       RC((launch_layernorm<T, T>(bufs[i & 1], m->ptr<float>(m->conv_ln_w[i]), m->ptr<float>(m->conv_ln_b[i]),
                                  B * Ts[i], co, 1e-5f, ACT_GELU, nullptr, bufs[i & 1], s)));
@@ -596,7 +614,7 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     g.A = xb; g.B = m->ptr(m->fp_w); g.M = M; g.N = H; g.K = C;
     g.rows_per_seg = M; g.seg_stride = 0; g.lda = C;
     g.bias = m->ptr<float>(m->fp_b); g.Cf = x; g.Ct = xt; g.ldc = H; g.act = ACT_NONE; g.zero = zero;
-    RC(prof(m, s, "gemm:proj", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    RC(prof(m, s, "gemm:proj", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
   }
   // ---- positional conv embedding: x = x + gelu(conv(x) + b) ----
   {
@@ -605,7 +623,7 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     g.A = xt; g.B = m->ptr(m->pos_w); g.M = M; g.N = cg; g.K = K * cg;
     g.rows_per_seg = Tf; g.T_in = Tf; g.stride = 1; g.pad = K / 2; g.cin = cg; g.ld_in = H;
     g.bias = m->ptr<float>(m->pos_b); g.resid = x; g.Cf = x; g.ldc = H; g.act = ACT_GELU; g.zero = zero;
-    RC(prof(m, s, "gemm_conv:posconv", gflops(g, G), 0, [&] { return launch_gemm<T>(g, AMODE_CONV, G, s); }));
+    RC(prof(m, s, "gemm_conv:posconv", gflops(g, G), gbytes<T>(g, AMODE_CONV, G), [&] { return launch_gemm<T>(g, AMODE_CONV, G, s); }));
   }
   if (!c.stable_layer_norm)
     RC((launch_layernorm<float, T>(x, m->ptr<float>(m->enc_ln_w), m->ptr<float>(m->enc_ln_b), M, H, eps, ACT_NONE,
@@ -632,20 +650,21 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     g.A = xb; g.B = m->ptr(Lw.qkv_w); g.M = M; g.N = m->ldq; g.K = H;
     g.rows_per_seg = M; g.lda = H; g.bias = m->ptr<float>(Lw.qkv_b); g.Ct = qkv; g.ldc = m->ldq; g.zero = zero;
     // algorithmic FLOPs count the 3H + 8*heads useful columns, not the zero pad to ldq
-    RC(prof(m, s, "gemm:qkv", 2.0 * M * (3.0 * H + 8.0 * nh) * H, 0,
+    RC(prof(m, s, "gemm:qkv", 2.0 * M * (3.0 * H + 8.0 * nh) * H, gbytes<T>(g),
             [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     AttnArgs a{};
     a.qkv = qkv; a.out = ctx; a.T = Tf; a.H = H; a.nh = nh; a.ldq = m->ldq; a.scale = 0.125f;
     a.gconst = m->ptr<float>(Lw.g_const); a.relb = m->ptr<float>(m->relb); a.maxd = MAXD;
     if (Tf > MAXD) return SSE_ERR_UNSUPPORTED;
-    RC(prof(m, s, "attn", 4.0 * B * (double)Tf * Tf * H, 0, [&] { return launch_attention<T>(a, B, s); }));
+    RC(prof(m, s, "attn", 4.0 * B * (double)Tf * Tf * H, (double)B * Tf * (4.0 * H + 8.0 * nh) * sizeof(T),
+            [&] { return launch_attention<T>(a, B, s); }));
     g = GemmArgs{};
     g.A = ctx; g.B = m->ptr(Lw.o_w); g.M = M; g.N = H; g.K = H; g.rows_per_seg = M; g.lda = H;
     g.bias = m->ptr<float>(Lw.o_b); g.resid = x; g.Cf = x; g.ldc = H; g.zero = zero;
     if (lnfold && l > 0) {   // x holds the previous layer's un-normalised sum: LN2 applied here
       g.rstats = st2; g.rln_w = m->ptr<float>(m->layers[l - 1].ln2_w); g.rln_b = m->ptr<float>(m->layers[l - 1].ln2_b);
     }
-    RC(prof(m, s, "gemm:oproj", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    RC(prof(m, s, "gemm:oproj", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     if (lnfold) {
       RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, ACT_NONE,
                                      nullptr, xb, s, st1)));
@@ -659,12 +678,12 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     g = GemmArgs{};
     g.A = xb; g.B = m->ptr(Lw.f1_w); g.M = M; g.N = F; g.K = H; g.rows_per_seg = M; g.lda = H;
     g.bias = m->ptr<float>(Lw.f1_b); g.Ct = ff; g.ldc = F; g.act = gelu_rounded_act<T>(); g.zero = zero;
-    RC(prof(m, s, "gemm:ffn1", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    RC(prof(m, s, "gemm:ffn1", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     g = GemmArgs{};
     g.A = ff; g.B = m->ptr(Lw.f2_w); g.M = M; g.N = H; g.K = F; g.rows_per_seg = M; g.lda = F;
     g.bias = m->ptr<float>(Lw.f2_b); g.resid = x; g.Cf = x; g.ldc = H; g.zero = zero;
     if (lnfold) { g.rstats = st1; g.rln_w = m->ptr<float>(Lw.ln1_w); g.rln_b = m->ptr<float>(Lw.ln1_b); }
-    RC(prof(m, s, "gemm:ffn2", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    RC(prof(m, s, "gemm:ffn2", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     if (lnfold) {
       RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, H, eps, ACT_NONE,
                                      nullptr, xb, s, st2)));
@@ -711,7 +730,7 @@ int whisper_decoder(sse_model* m, const T* enc, int B, const Sink& sink, char* w
     GemmArgs g{};
     g.A = A; g.B = m->ptr(wo); g.M = B; g.N = N; g.K = K; g.rows_per_seg = B; g.lda = K;
     g.bias = m->ptr<float>(bo); g.resid = resid; g.Cf = Cf; g.Ct = Ct; g.ldc = N; g.act = act; g.zero = zero;
-    return prof(m, s, tag, gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); });
+    return prof(m, s, tag, gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); });
   };
   for (int l = 0; l < c.decoder_layers; ++l) {
     const DecLayerW& W = m->dec[l];
@@ -728,7 +747,7 @@ int whisper_decoder(sse_model* m, const T* enc, int B, const Sink& sink, char* w
       GemmArgs g{};
       g.A = enc; g.B = m->ptr(W.kv_w); g.M = B * Tq; g.N = 2 * D; g.K = D; g.rows_per_seg = B * Tq; g.lda = D;
       g.bias = m->ptr<float>(W.kv_b); g.Ct = kv; g.ldc = 2 * D; g.zero = zero;
-      RC(prof(m, s, "gemm:dec_kv", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+      RC(prof(m, s, "gemm:dec_kv", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     }
     RC(prof(m, s, "dec_xattn", 4.0 * B * (double)Tq * D, (double)B * Tq * 2 * D * sizeof(T),
             [&] { return launch_xattn1<T>(q, kv, B, Tq, D, nh, ctx, s); }));
@@ -771,13 +790,13 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
     g.A = mel; g.B = m->ptr(m->c1_w); g.M = B * T2; g.N = D; g.K = 3 * nm;
     g.rows_per_seg = T2; g.T_in = T2; g.stride = 1; g.pad = 1; g.cin = nm; g.ld_in = nm;
     g.bias = m->ptr<float>(m->c1_b); g.Ct = h1; g.ldc = D; g.act = gelu_rounded_act<T>(); g.zero = zero;
-    RC(prof(m, s, "gemm_conv:conv1", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_CONV, 1, s); }));
+    RC(prof(m, s, "gemm_conv:conv1", gflops(g), gbytes<T>(g, AMODE_CONV), [&] { return launch_gemm<T>(g, AMODE_CONV, 1, s); }));
     g = GemmArgs{};   // conv2: k3 s2 pad1, GELU, + embed_positions
     g.A = h1; g.B = m->ptr(m->c2_w); g.M = M; g.N = D; g.K = 3 * D;
     g.rows_per_seg = Tq; g.T_in = T2; g.stride = 2; g.pad = 1; g.cin = D; g.ld_in = D;
     g.bias = m->ptr<float>(m->c2_b); g.resid = m->ptr<float>(m->positions); g.resid_rows = Tq;
     g.Cf = x; g.ldc = D; g.act = ACT_GELU; g.zero = zero;
-    RC(prof(m, s, "gemm_conv:conv2", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_CONV, 1, s); }));
+    RC(prof(m, s, "gemm_conv:conv2", gflops(g), gbytes<T>(g, AMODE_CONV), [&] { return launch_gemm<T>(g, AMODE_CONV, 1, s); }));
   }
   RC(sink.emit(0, x));
   T* qkv = (T*)(ws + w.qkv);
@@ -790,24 +809,25 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
     GemmArgs g{};
     g.A = xb; g.B = m->ptr(Lw.qkv_w); g.M = M; g.N = 3 * D; g.K = D; g.rows_per_seg = M; g.lda = D;
     g.bias = m->ptr<float>(Lw.qkv_b); g.Ct = qkv; g.ldc = 3 * D; g.zero = zero;
-    RC(prof(m, s, "gemm:qkv", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    RC(prof(m, s, "gemm:qkv", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     AttnArgs a{};
     a.qkv = qkv; a.out = ctx; a.T = Tq; a.H = D; a.nh = nh; a.ldq = m->ldq; a.scale = 1.0f;
-    RC(prof(m, s, "attn", 4.0 * B * (double)Tq * Tq * D, 0, [&] { return launch_attention<T>(a, B, s); }));
+    RC(prof(m, s, "attn", 4.0 * B * (double)Tq * Tq * D, (double)B * Tq * 4.0 * D * sizeof(T),
+            [&] { return launch_attention<T>(a, B, s); }));
     g = GemmArgs{};
     g.A = ctx; g.B = m->ptr(Lw.o_w); g.M = M; g.N = D; g.K = D; g.rows_per_seg = M; g.lda = D;
     g.bias = m->ptr<float>(Lw.o_b); g.resid = x; g.Cf = x; g.ldc = D; g.zero = zero;
-    RC(prof(m, s, "gemm:oproj", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    RC(prof(m, s, "gemm:oproj", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, D, eps, ACT_NONE, nullptr,
                                    xb, s)));
     g = GemmArgs{};
     g.A = xb; g.B = m->ptr(Lw.f1_w); g.M = M; g.N = F; g.K = D; g.rows_per_seg = M; g.lda = D;
     g.bias = m->ptr<float>(Lw.f1_b); g.Ct = ff; g.ldc = F; g.act = gelu_rounded_act<T>(); g.zero = zero;
-    RC(prof(m, s, "gemm:ffn1", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    RC(prof(m, s, "gemm:ffn1", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     g = GemmArgs{};
     g.A = ff; g.B = m->ptr(Lw.f2_w); g.M = M; g.N = D; g.K = F; g.rows_per_seg = M; g.lda = F;
     g.bias = m->ptr<float>(Lw.f2_b); g.resid = x; g.Cf = x; g.ldc = D; g.zero = zero;
-    RC(prof(m, s, "gemm:ffn2", gflops(g), 0, [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    RC(prof(m, s, "gemm:ffn2", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     if (l + 1 < c.layers) RC(sink.emit(l + 1, x));
   }
   // hidden_states[-1] is the post-LN last_hidden_state (HF/utils/output_capturing.py:268-279)

@@ -26,8 +26,8 @@ def per_kernel(d, counter):
 
 def main():
     out, js = sys.argv[1], sys.argv[2]
-    fetch = per_kernel(os.path.join(out, "fetch"), "FETCH_SIZE")
-    write = per_kernel(os.path.join(out, "write"), "WRITE_SIZE")
+    fetch = per_kernel(out, "FETCH_SIZE")
+    write = per_kernel(out, "WRITE_SIZE")
     kernels = {}
     for k in sorted(set(fetch) | set(write)):
         nf, f = fetch.get(k, (0, 0.0))
@@ -36,8 +36,8 @@ def main():
         kernels[k] = {"launches": n, "fetch_bytes_per_launch": 2 * 1024 * f / max(nf, 1),
                       "write_bytes_per_launch": 1024 * w / max(nw, 1)}
         kernels[k]["hbm_bytes_per_launch"] = kernels[k]["fetch_bytes_per_launch"] + kernels[k]["write_bytes_per_launch"]
-    res = {"note": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE, separate passes over bench.py "
-                   + " ".join(sys.argv[3:]) + " --no-profile; FETCH_SIZE x2 (gfx950), KiB -> bytes",
+    res = {"note": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE (separate passes) over bench.py "
+                   + " ".join(sys.argv[3:]) + "; FETCH_SIZE x2 (gfx950 correction), KiB -> bytes",
            "kernels": kernels}
     with open(js, "w") as fh:
         json.dump(res, fh, indent=1)
