@@ -12,9 +12,12 @@ Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 the driver us
 torch.distributed.run (one rank per GPU, RANK/LOCAL_RANK/WORLD_SIZE from the env).
 
 The JSON line carries:
-  roofline      dominant kernel (most device time in the timed region): algorithmic FLOPs
-                per launch / its mean launch time, both from HIP events recorded around every
-                launch on the launch stream inside the timed region (sse_profile_*).
+  value         clips/s over K steps timed without instrumentation.
+  roofline      dominant kernel (most device time): algorithmic FLOPs per launch / its mean
+                launch time, both from HIP events recorded around every launch on the launch
+                stream (sse_profile_*) during a second timed region of the same K steps
+                (profiled_ms_per_step: that region's step time, events included); traffic from
+                the committed rocprofv3 PMC summary of the same workload.
   cpu_baseline  the numpy oracle ("port") on this host's cores, a bounded sample of clips
                 (rank 0, N = 1 only).
 """
@@ -171,21 +174,33 @@ def main():
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
+
+    def timed(profile):
+        """K steps between barriers + device syncs; with profile, HIP events around every launch."""
+        if profile:
+            model.profile_start(max_launches=200 * max(a.steps, 1))
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        recs = []
+        if profile:
+            recs = model.profile_read()
+            model.profile_stop()
+        return el, recs
+
+    # value: an unperturbed timed region (per-launch event records add ~0.5 ms/step of launch
+    # gaps); roofline: a second timed region of the same K steps with the events
+    elapsed, _ = timed(False)
+    records, prof_elapsed = [], None
     if not a.no_profile:
-        model.profile_start(max_launches=200 * max(a.steps, 1))
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    records = model.profile_read() if not a.no_profile else []
-    if not a.no_profile:
-        model.profile_stop()
+        prof_elapsed, records = timed(True)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if dist is not None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -208,6 +223,7 @@ def main():
         if records:
             rf = roofline(records, a.dtype)
             rf["device_ms_per_step_sum"] = round(sum(r[1] for r in records) / a.steps, 3)
+            rf["profiled_ms_per_step"] = round(1e3 * prof_elapsed / a.steps, 3)
             tr, src = pmc_traffic(spec.name, a.dtype, rf["kernel"], None)
             if tr is not None:
                 rf["traffic"] = round(tr)
