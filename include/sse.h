@@ -34,7 +34,9 @@ extern "C" {
 #endif
 
 enum sse_kind { SSE_KIND_WAVLM = 0, SSE_KIND_WHISPER = 1 };
-enum sse_dtype { SSE_DTYPE_F32 = 0, SSE_DTYPE_BF16 = 1 };
+/* SSE_DTYPE_FP8 (Whisper): bf16 activations, the encoder layers' QKV / fc1 / fc2 GEMMs in MX-fp8
+ * (OCP e4m3 operands, one E8M0 scale per 32 K-elements, BASELINE configs[4] "fp8 MFMA encoder"). */
+enum sse_dtype { SSE_DTYPE_F32 = 0, SSE_DTYPE_BF16 = 1, SSE_DTYPE_FP8 = 2 };
 enum sse_err {
   SSE_OK = 0,
   SSE_ERR_INVALID = -1,      /* bad argument / null pointer / bad layer index         */
@@ -168,7 +170,24 @@ int sse_profile_stop(sse_model* m);
 int sse_gemm(int dtype, const void* d_a, const void* d_b, const float* d_bias, const float* d_resid, float* d_cf,
              void* d_ct, int M, int N, int K, int act, const void* d_zero, void* stream);
 
+/* MX-fp8 operands (SSE_DTYPE_FP8): e4m3 bytes [R][K] (K % 128 == 0) plus E8M0 scales, one per 32
+ * consecutive K elements, in the tiled layout the GEMM stages (role 0: A operand / activations,
+ * role 1: B operand / weights [N][K]); sse_mx_scale_bytes(R, K) bytes.  Quantisation: block
+ * exponent E = the smallest with max|x| <= 448 * 2^E, q = RNE_e4m3(x * 2^-E). */
+size_t sse_mx_scale_bytes(int R, int K);
+/* byte offset of the scale of (row r, block b = k / 32) in the role's layout */
+long long sse_mx_scale_offset(int role, int r, int b, int K);
+int sse_mx_quantize(const float* d_x, int R, int K, int role, uint8_t* d_q, uint8_t* d_scale, void* stream);
+/* C[M][N] = dequant(A)[M][K] . dequant(B)[N][K]^T (+bias) (GELU: act 1 erf, 2 bf16-path form)
+ * (+resid fp32) -> d_cf fp32, or d_ct bf16, or (d_c_scale != NULL) d_ct MX-fp8 in the A layout of
+ * a GEMM with K = N.  M > 0, N % 256 == 0, K % 128 == 0. */
+int sse_gemm_mx(const uint8_t* d_a, const uint8_t* d_a_scale, const uint8_t* d_b, const uint8_t* d_b_scale,
+                const float* d_bias, const float* d_resid, float* d_cf, void* d_ct, uint8_t* d_c_scale, int M, int N,
+                int K, int act, void* stream);
+
 /* Host-only helpers (no device work; usable without a GPU). */
+/* The quantiser above on the host (what sse_model_create applies to the weights). */
+int sse_mx_quantize_host(const float* x, int R, int K, int role, uint8_t* q, uint8_t* scale);
 const char* sse_strerror(int err);
 /* WavLM relative-position bucket of distance d = key - query (HF _relative_positions_bucket). */
 int sse_rel_bucket(int d, int num_buckets, int max_distance);

@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get("SSE_LIB_PATH") or os.path.join(_HERE, "libsse.so")
 
 SSE_DTYPE_F32 = 0
 SSE_DTYPE_BF16 = 1
+SSE_DTYPE_FP8 = 2   # bf16 activations + MX-fp8 encoder-layer GEMMs (Whisper)
 
 EXPORTED = ("sse_weight_floats", "sse_model_create", "sse_model_destroy", "sse_output_frames",
             "sse_workspace_bytes", "sse_logmel_workspace_bytes", "sse_logmel", "sse_embed",
@@ -26,7 +27,8 @@ EXPORTED = ("sse_weight_floats", "sse_model_create", "sse_model_destroy", "sse_o
             "sse_normalize", "sse_normalize_workspace_bytes", "sse_whisper_hidden_states_from_mel",
             "sse_profile_start", "sse_profile_read", "sse_profile_stop", "sse_gemm", "sse_whisper_embed",
             "sse_whisper_decoder_hidden_states", "sse_mono", "sse_resample_length", "sse_resample_workspace_bytes",
-            "sse_resample", "sse_augment")
+            "sse_resample", "sse_augment", "sse_mx_scale_bytes", "sse_mx_scale_offset", "sse_mx_quantize",
+            "sse_mx_quantize_host", "sse_gemm_mx")
 
 
 class SSEError(RuntimeError):
@@ -136,6 +138,16 @@ def lib() -> ctypes.CDLL:
     L.sse_resample.restype = i32
     L.sse_augment.argtypes = [vp, vp, i32, i32, vp, vp, vp, ctypes.c_uint64, vp]
     L.sse_augment.restype = i32
+    L.sse_mx_scale_bytes.argtypes = [i32, i32]
+    L.sse_mx_scale_bytes.restype = sz
+    L.sse_mx_scale_offset.argtypes = [i32, i32, i32, i32]
+    L.sse_mx_scale_offset.restype = ctypes.c_longlong
+    L.sse_mx_quantize.argtypes = [vp, i32, i32, i32, vp, vp, vp]
+    L.sse_mx_quantize.restype = i32
+    L.sse_mx_quantize_host.argtypes = [vp, i32, i32, i32, vp, vp]
+    L.sse_mx_quantize_host.restype = i32
+    L.sse_gemm_mx.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp]
+    L.sse_gemm_mx.restype = i32
     L.sse_strerror.argtypes = [i32]
     L.sse_strerror.restype = ctypes.c_char_p
     L.sse_rel_bucket.argtypes = [i32, i32, i32]

@@ -150,7 +150,48 @@ struct GemmArgs {
   const float2* rstats;
   const float* rln_w;
   const float* rln_b;
+  // MX-fp8 operands (launch_gemm8_mx): A / B are e4m3 bytes, one E8M0 scale per 32 consecutive K
+  // elements in the tile layouts of mx_a_scale_off / mx_b_scale_off.  c_scale != null: Ct is e4m3
+  // with its scales written in the A layout of a following GEMM whose K is this GEMM's N.
+  const unsigned char* a_scale;
+  const unsigned char* b_scale;
+  unsigned char* c_scale;
 };
+
+// ---- MX-fp8 scale layouts (both operands: K-tiles of 128, one E8M0 byte per 32-element block) ----
+// The 8-phase MX GEMM stages, per 256-row (column) tile and K-tile, one 1 KiB scale block by
+// LDS-DMA; inside it the bytes are ordered so that each lane's MFMA scales are one dword:
+//   A rows   m = mi*128 + wm*64 + i*16 + r16 : [mi][wm][q][r16][i]   (q = block within the K-tile)
+//   B cols   n = ni*128 + wn*32 + j*16 + r16 : [wn][q][r16][ni][j]
+__host__ __device__ inline long long mx_a_scale_off(long long m, int blk, int kt) {
+  return ((m >> 8) * kt + (blk >> 2)) * 1024 + ((((m >> 6) & 3) * 4 + (blk & 3)) * 16 + (m & 15)) * 4 + ((m >> 4) & 3);
+}
+__host__ __device__ inline long long mx_b_scale_off(long long n, int blk, int kt) {
+  return ((n >> 8) * kt + (blk >> 2)) * 1024 + ((((n >> 5) & 3) * 4 + (blk & 3)) * 16 + (n & 15)) * 4 +
+         ((n >> 7) & 1) * 2 + ((n >> 4) & 1);
+}
+// bytes of a scale tensor for R rows (columns) and K elements
+__host__ __device__ inline long long mx_scale_bytes(long long R, int K) { return ((R + 255) / 256) * (K / 128) * 1024; }
+
+// E8M0 exponent of a 32-element block with max |x| = amax: the smallest E with amax <= 448 * 2^E
+// (448 = e4m3 max), clamped to [-127, 127]; returns the biased byte E + 127.
+__host__ __device__ inline int mx_scale_exp(float amax) {
+  union { float f; unsigned u; } v;
+  v.f = amax;
+  const int be = (int)((v.u >> 23) & 255);
+  if (be == 0) return 0;                       // zero / denormal block: 2^-127
+  int E = be - 127 - ((v.u & 0x7FFFFF) <= 0x600000 ? 8 : 7);
+  E = E < -127 ? -127 : (E > 127 ? 127 : E);
+  return E + 127;
+}
+// 2^-(b - 127) as float (b in [0, 254]); exact (2^127 .. 2^-127, the last a denormal)
+__host__ __device__ inline float mx_inv_scale(int b) {
+  union { float f; unsigned u; } v;
+  const int e = 127 - (b - 127);               // biased exponent of 2^(127 - b)
+  if (e >= 1) { v.u = (unsigned)e << 23; return v.f; }
+  v.u = 0x00400000u;                           // 2^-127
+  return v.f;
+}
 
 // LayerNorm affine of one 4-column group, the exact expression of layernorm_kernel
 SSE_DEV f32x4 ln_apply4(f32x4 v, float2 st, const float* w, const float* b, int n) {
@@ -168,6 +209,7 @@ int launch_gemm_bf16(const GemmArgs& a, int amode, int groups, hipStream_t s);
 int launch_gemm_f32(const GemmArgs& a, int amode, int groups, hipStream_t s);
 
 int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s);   // kernels_gemm8.hip
+int launch_gemm8_mx(const GemmArgs& a, hipStream_t s);     // kernels_gemm8.hip (MX-fp8 operands)
 template <typename T> inline int launch_gemm(const GemmArgs& a, int amode, int groups, hipStream_t s);
 template <> inline int launch_gemm<bf16>(const GemmArgs& a, int amode, int groups, hipStream_t s) {
   return launch_gemm_bf16(a, amode, groups, s);

@@ -18,6 +18,11 @@ template <typename TI, typename TO>
 int launch_layernorm(const TI* in, const float* w, const float* b, int rows, int H, float eps, int act,
                      float* out_f, TO* out_t, hipStream_t s, float2* stats = nullptr);
 
+// MX-fp8 (e4m3 + E8M0 per 32 K-elements) GEMM operands, layouts in common.h
+int launch_layernorm_mx(const float* in, const float* w, const float* b, int rows, int H, float eps,
+                        unsigned char* q, unsigned char* scale, hipStream_t s);
+int launch_mx_quantize(const float* x, int R, int K, int role, unsigned char* q, unsigned char* scale, hipStream_t s);
+
 int launch_pool_mean(const float* x, int B, int T, int H, float* out, long long out_stride, hipStream_t s,
                      const float2* st = nullptr, const float* w = nullptr, const float* b = nullptr);
 

@@ -21,6 +21,15 @@
 //    buffer (tile & 1).  Every half is issued >= 5 phases before its first read and after the
 //    barrier that follows the last lgkmcnt of its previous occupant; a uniform vmcnt(8) at the
 //    end of each L-section (fewer in the tail) retires what the next phase reads.
+//
+// MX = true: MX-fp8 operands (OCP e4m3 + E8M0 per 32 K-elements, v_mfma_scale_f32_16x16x128_f8f6f4,
+// 2x the bf16 MFMA rate).  A K-tile is still 128 B per row (128 elements), the LDS image and the
+// fragment reads are byte-identical to the bf16 kernel's: the MX instruction takes lane group q's
+// K elements from chunks q and q+4 of the row (k in [16q, 16q+16) u [64+16q, 64+16q+16), probed on
+// gfx950, tools/probe_mx2.hip) and block b's scale of row r from lane r + 16b.  Per K-tile the
+// 256 A-row and 256 B-column scales (2 KiB, layouts mx_a_scale_off / mx_b_scale_off) are one extra
+// dword LDS-DMA per wave, issued with A0 (phase p = 2) into a 4-deep ring (tile & 3), so the same
+// WAR / RAW argument holds; that phase counts 3 vector-memory ops instead of 2.
 #include <string.h>
 
 #include <type_traits>
@@ -34,7 +43,13 @@ constexpr int G8_BUF = 4 * G8_HALF;           // A rows 0-127 | A rows 128-255 |
 constexpr int G8_OPS = 2 * G8_BUF;            // two K-tiles: 128 KiB
 constexpr int G8_CLD = 256 + 4;               // epilogue fp32 row stride (floats)
 constexpr int G8_EPI = 128 * G8_CLD * 4;      // one 128-row half of the C tile
+constexpr int G8_SC = 2048;                   // MX: one K-tile's scales (A 1 KiB | B 1 KiB)
+constexpr int G8_OPS_MX = G8_OPS + 4 * G8_SC; // MX: operands + 4-deep scale ring
 constexpr int G8_SMEM = G8_OPS > G8_EPI ? G8_OPS : G8_EPI;
+constexpr int G8_SMEM_MX = G8_OPS_MX > G8_EPI ? G8_OPS_MX : G8_EPI;
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 // phase k = 4t + p (k >= -8) -> the (tile, half) whose LDS-DMA it issues
 SSE_DEV void g8_target(int k, int& tile, int& half) {
@@ -43,24 +58,54 @@ SSE_DEV void g8_target(int k, int& tile, int& half) {
   half = p == 0 ? 3 : (p == 1 ? 1 : (p == 2 ? 0 : 2));
 }
 
-SSE_DEV int g8_issued(int k, int nk) {
+// vector-memory ops (per wave) issued at phase k: 2 LDS-DMA per half-tile, +1 scale DMA (MX) at
+// the phase that issues A0 (p = 2)
+template <bool MX>
+SSE_DEV int g8_ops(int k, int nk) {
   if (k < -6) return 0;
   int tile, half;
   g8_target(k, tile, half);
-  return tile < nk ? 1 : 0;
+  if (tile >= nk) return 0;
+  return MX && half == 0 ? 3 : 2;
 }
 
-// retire every half-tile issued at phases <= k-4 (2 DMA instructions per half per wave)
-SSE_DEV void g8_wait(int k, int nk) {
-  const int n = g8_issued(k, nk) + g8_issued(k - 1, nk) + g8_issued(k - 2, nk) + g8_issued(k - 3, nk);
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-  }
+template <bool MX>
+SSE_DEV int g8_count(int k, int nk) {   // ops issued at phases k-3 .. k (the wait at the end of L(k))
+  return g8_ops<MX>(k, nk) + g8_ops<MX>(k - 1, nk) + g8_ops<MX>(k - 2, nk) + g8_ops<MX>(k - 3, nk);
 }
+
+// s_waitcnt vmcnt(n), n in [0, 63] (6-bit field; larger n waits for everything).  The bf16 kernels
+// only ever wait for even counts (2 ops per phase, even store counts): a 32-way switch.
+template <bool MX>
+SSE_DEV void g8_vmcnt_dyn(int n) {
+#define G8_VM(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+#define G8_VE(N) case N / 2: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+  if constexpr (MX) {
+    switch (n) {
+      G8_VM(1) G8_VM(2) G8_VM(3) G8_VM(4) G8_VM(5) G8_VM(6) G8_VM(7) G8_VM(8) G8_VM(9) G8_VM(10) G8_VM(11)
+      G8_VM(12) G8_VM(13) G8_VM(14) G8_VM(15) G8_VM(16) G8_VM(17) G8_VM(18) G8_VM(19) G8_VM(20) G8_VM(21)
+      G8_VM(22) G8_VM(23) G8_VM(24) G8_VM(25) G8_VM(26) G8_VM(27) G8_VM(28) G8_VM(29) G8_VM(30) G8_VM(31)
+      G8_VM(32) G8_VM(33) G8_VM(34) G8_VM(35) G8_VM(36) G8_VM(37) G8_VM(38) G8_VM(39) G8_VM(40) G8_VM(41)
+      G8_VM(42) G8_VM(43) G8_VM(44) G8_VM(45) G8_VM(46) G8_VM(47) G8_VM(48) G8_VM(49) G8_VM(50) G8_VM(51)
+      G8_VM(52) G8_VM(53) G8_VM(54) G8_VM(55) G8_VM(56) G8_VM(57) G8_VM(58) G8_VM(59) G8_VM(60) G8_VM(61)
+      G8_VM(62) G8_VM(63)
+      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+  } else {
+    switch (n >> 1) {
+      G8_VE(2) G8_VE(4) G8_VE(6) G8_VE(8) G8_VE(10) G8_VE(12) G8_VE(14) G8_VE(16) G8_VE(18) G8_VE(20) G8_VE(22)
+      G8_VE(24) G8_VE(26) G8_VE(28) G8_VE(30) G8_VE(32) G8_VE(34) G8_VE(36) G8_VE(38) G8_VE(40) G8_VE(42)
+      G8_VE(44) G8_VE(46) G8_VE(48) G8_VE(50) G8_VE(52) G8_VE(54) G8_VE(56) G8_VE(58) G8_VE(60) G8_VE(62)
+      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+  }
+#undef G8_VM
+#undef G8_VE
+}
+
+// retire every op issued at phases <= k-4
+template <bool MX>
+SSE_DEV void g8_wait(int k, int nk) { g8_vmcnt_dyn<MX>(g8_count<MX>(k, nk)); }
 
 // epilogue memory ops; NT = non-temporal (streaming: C tiles and residual rows are touched once
 // and should not evict the A / B operand lines from L2)
@@ -81,17 +126,35 @@ SSE_DEV void g8_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+template <int OA, int OB>
+SSE_DEV f32x4 g8_mx(i32x8 a, i32x8 b, f32x4 c, int sa, int sb) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, OA, sa, OB, sb);
+}
+template <int I, int N, typename F>
+SSE_DEV void g8_sfor(F&& f) {   // f(integral_constant<int, I>) for I .. N-1, compile-time indices
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    g8_sfor<I + 1, N>(f);
+  }
+}
+
+// two 16-B fragments (chunks q and q+4 of the K-tile row) as one 32-byte MX operand
+SSE_DEV i32x8 g8_cat(bf16x8 lo, bf16x8 hi) {
+  const i32x4 a = __builtin_bit_cast(i32x4, lo), b = __builtin_bit_cast(i32x4, hi);
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
 // DBG = 1 (SSE_GEMM_DEBUG=skip_epi, timing experiments only): no epilogue, a checksum keeps the MFMAs live.
-template <bool RES>
+template <bool RES, bool Q8 = false>
 SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, int n0, int wm, int wn,
                                 int q, int r16);
 
 // TR = true: the MFMAs compute C^T blocks (the B fragment is the MFMA's A operand), so every
 // lane ends up holding 4 consecutive output columns of one row and the epilogue stores straight
 // from registers (see g8_epilogue_direct).  TR = false: C blocks, LDS-staged epilogue.
-template <int DBG, bool TR, bool NT>
+template <int DBG, bool TR, bool NT, bool MX = false>
 __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[G8_SMEM];   // the ONLY shared object
+  __shared__ __attribute__((aligned(16))) char smem[MX ? G8_SMEM_MX : G8_SMEM];   // the ONLY shared object
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 2, wn = wave & 3;
@@ -104,20 +167,27 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
     bid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
   }
   const int m0 = (bid / n_tiles_n) * 256, n0 = (bid % n_tiles_n) * 256;
-  const int nk = K / 64;
+  constexpr int ES = MX ? 1 : 2;   // operand element bytes; a K-tile is 128 B per row either way
+  const int nk = K / (128 / ES);
 
   // ---- LDS-DMA sources: buffer descriptors based at the block's first A row / B row; each
   // lane's byte offset is fixed for the whole K loop, the scalar soffset advances by 128 B.
   constexpr int NREC = 0x7FFFFFF0;
-  __amdgpu_buffer_rsrc_t a_rsrc, b_rsrc;
-  unsigned a_voff[2][2], b_voff[2][2];
+  __amdgpu_buffer_rsrc_t a_rsrc, b_rsrc, s_rsrc;
+  unsigned a_voff[2][2], b_voff[2][2], s_voff = 0;
   {
     const int mf = m0 < M ? m0 : M - 1;
     const int seg0 = mf / g.rows_per_seg, rr0 = mf - seg0 * g.rows_per_seg;
-    const long long a_base = (long long)seg0 * g.seg_stride + (long long)rr0 * g.lda;
-    a_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const bf16*)g.A + a_base), (short)0, NREC, 0x00020000);
-    b_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const bf16*)g.B + (long long)n0 * K), (short)0, NREC,
+    const long long a_base = ((long long)seg0 * g.seg_stride + (long long)rr0 * g.lda) * ES;   // bytes
+    a_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)g.A + a_base), (short)0, NREC, 0x00020000);
+    b_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)g.B + (long long)n0 * K * ES), (short)0, NREC,
                                                0x00020000);
+    if constexpr (MX) {   // this tile's scale blocks; waves 0-3 stage A's 1 KiB, waves 4-7 B's
+      const unsigned char* sb = wave < 4 ? g.a_scale + (long long)(m0 >> 8) * nk * 1024
+                                         : g.b_scale + (long long)(n0 >> 8) * nk * 1024;
+      s_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)sb, (short)0, NREC, 0x00020000);
+      s_voff = (unsigned)((wave & 3) * 256 + lane * 4);
+    }
     #pragma unroll
     for (int h = 0; h < 2; ++h)
       #pragma unroll
@@ -127,9 +197,9 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
         int m = m0 + row;
         m = m < M ? m : M - 1;
         const int seg = m / g.rows_per_seg, rr = m - seg * g.rows_per_seg;
-        const long long el = (long long)seg * g.seg_stride + (long long)rr * g.lda + ch * 8;
-        a_voff[h][s] = (unsigned)((el - a_base) * 2);
-        b_voff[h][s] = (unsigned)(((long long)row * K + ch * 8) * 2);
+        const long long el = ((long long)seg * g.seg_stride + (long long)rr * g.lda) * ES + ch * 16;
+        a_voff[h][s] = (unsigned)(el - a_base);
+        b_voff[h][s] = (unsigned)((long long)row * K * ES + ch * 16);
       }
   }
   auto issue = [&](int k) {
@@ -139,6 +209,11 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
     if (tile >= nk) return;
     char* dst = smem + (tile & 1) * G8_BUF + half * G8_HALF;
     const unsigned soff = (unsigned)tile * 128u;
+    if constexpr (MX) {
+      if (half == 0)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(s_rsrc, LPTR(smem + G8_OPS + (tile & 3) * G8_SC + wave * 256), 4,
+                                                 s_voff, (unsigned)tile * 1024u, 0, 0);
+    }
     if (half < 2) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, LPTR(dst + wave * 1024), 16, a_voff[half][0], soff, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, LPTR(dst + (wave + 8) * 1024), 16, a_voff[half][1], soff, 0, 0);
@@ -159,44 +234,78 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
         #pragma unroll
         for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 af[4][2], b0f[2][2], b1f[2][2];
+  int sa = 0, sb = 0;   // MX: this lane's A scales (rows i = 0..3 of the current mi), B scales (ni, j)
+  auto read_sa = [&](int t, int mi) {
+    if constexpr (MX) sa = *(const int*)(smem + G8_OPS + (t & 3) * G8_SC + (((mi * 2 + wm) * 4 + q) * 16 + r16) * 4);
+  };
+  auto read_sb = [&](int t) {
+    if constexpr (MX) sb = *(const int*)(smem + G8_OPS + (t & 3) * G8_SC + 1024 + ((wn * 4 + q) * 16 + r16) * 4);
+  };
 
+  // MX: the same two 16-B reads per fragment, landing in one 8-dword operand tuple
+  i32x8 afx[4], b0x[2], b1x[2];
+  auto rd32 = [&](const char* hb, int row) {
+    const i32x4 lo = *(const i32x4*)(hb + row * 128 + ((q ^ ((row >> 1) & 7)) * 16));
+    const i32x4 hi = *(const i32x4*)(hb + row * 128 + (((q + 4) ^ ((row >> 1) & 7)) * 16));
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
   auto read_a = [&](const char* hb) {
     #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = wm * 64 + i * 16 + r16;
-      #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        af[i][ks] = *(const bf16x8*)(hb + row * 128 + (((q + 4 * ks) ^ ((row >> 1) & 7)) * 16));
+      if constexpr (MX) {
+        afx[i] = rd32(hb, row);
+      } else {
+        #pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          af[i][ks] = *(const bf16x8*)(hb + row * 128 + (((q + 4 * ks) ^ ((row >> 1) & 7)) * 16));
+      }
     }
   };
-  auto read_b = [&](const char* hb, bf16x8 (&bf)[2][2]) {
+  auto read_b = [&](const char* hb, bf16x8 (&bf)[2][2], i32x8 (&bx)[2]) {
     #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int row = wn * 32 + j * 16 + r16;
-      #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        bf[j][ks] = *(const bf16x8*)(hb + row * 128 + (((q + 4 * ks) ^ ((row >> 1) & 7)) * 16));
+      if constexpr (MX) {
+        bx[j] = rd32(hb, row);
+      } else {
+        #pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          bf[j][ks] = *(const bf16x8*)(hb + row * 128 + (((q + 4 * ks) ^ ((row >> 1) & 7)) * 16));
+      }
     }
   };
-  auto mma = [&](f32x4 (&c)[4][2], const bf16x8 (&bf)[2][2]) {
+  auto mma = [&](f32x4 (&c)[4][2], const bf16x8 (&bf)[2][2], const i32x8 (&bx)[2], auto ni_c) {
+    constexpr int NI = decltype(ni_c)::value;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
-    #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    if constexpr (MX) {
+      g8_sfor<0, 4>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        g8_sfor<0, 2>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          if constexpr (TR) c[i][j] = g8_mx<NI * 2 + j, i>(bx[j], afx[i], c[i][j], sb, sa);
+          else c[i][j] = g8_mx<i, NI * 2 + j>(afx[i], bx[j], c[i][j], sa, sb);
+        });
+      });
+    } else {
       #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int ks = 0; ks < 2; ++ks)
         #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          c[i][j] = TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][ks], af[i][ks], c[i][j], 0, 0, 0)
-                       : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bf[j][ks], c[i][j], 0, 0, 0);
+        for (int i = 0; i < 4; ++i)
+          #pragma unroll
+          for (int j = 0; j < 2; ++j)
+            c[i][j] = TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][ks], af[i][ks], c[i][j], 0, 0, 0)
+                         : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bf[j][ks], c[i][j], 0, 0, 0);
+    }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   };
 
   // ---- prologue: phases -6..-1 stage A0(0) B0(0) B1(0) A1(0) A0(1) B0(1)
   for (int k = -6; k < 0; ++k) issue(k);
-  g8_wait(-1, nk);
+  g8_wait<MX>(-1, nk);
   g8_barrier();
   if (wm == 1) g8_barrier();   // group 1 runs one barrier behind
 
@@ -209,35 +318,41 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
     auto issue_wait = [&](int kk) {
       if constexpr (ST) {
         issue(kk);
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        if constexpr (MX) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       } else {
         issue(kk);
-        g8_wait(kk, nk);
+        g8_wait<MX>(kk, nk);
       }
     };
+    const std::integral_constant<int, 0> ni0;
+    const std::integral_constant<int, 1> ni1;
     // phase 0: (mi 0, ni 0) reads A rows 0-127 and B cols 0-127
     read_a(buf);
-    read_b(buf + 2 * G8_HALF, b0f);
+    read_b(buf + 2 * G8_HALF, b0f, b0x);
+    read_sa(t, 0);
+    read_sb(t);
     issue_wait(k);
     g8_barrier();
-    mma(acc[0][0], b0f);
+    mma(acc[0][0], b0f, b0x, ni0);
     g8_barrier();
     // phase 1: (mi 0, ni 1) reads B cols 128-255
-    read_b(buf + 3 * G8_HALF, b1f);
+    read_b(buf + 3 * G8_HALF, b1f, b1x);
     issue_wait(k + 1);
     g8_barrier();
-    mma(acc[0][1], b1f);
+    mma(acc[0][1], b1f, b1x, ni1);
     g8_barrier();
     // phase 2: (mi 1, ni 1) reads A rows 128-255
     read_a(buf + G8_HALF);
+    read_sa(t, 1);
     issue_wait(k + 2);
     g8_barrier();
-    mma(acc[1][1], b1f);
+    mma(acc[1][1], b1f, b1x, ni1);
     g8_barrier();
     // phase 3: (mi 1, ni 0) no reads
     issue_wait(k + 3);
     g8_barrier();
-    mma(acc[1][0], b0f);
+    mma(acc[1][0], b0f, b0x, ni0);
     g8_barrier();
   };
   int t = 0;
@@ -329,6 +444,25 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
           for (int e = 0; e < 4; ++e) r[e] = fmaf((r[e] - st[u].x) * st[u].y, lw[e], lb[e]);
         }
         o += r;
+        if (MX && g.c_scale) {
+          // MX-fp8 out: the wave holds one row's 256 columns, 8 lanes = one 32-column block
+          float a = fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3])));
+          a = fmaxf(a, __shfl_xor(a, 1, 64));
+          a = fmaxf(a, __shfl_xor(a, 2, 64));
+          a = fmaxf(a, __shfl_xor(a, 4, 64));
+          const int e = mx_scale_exp(a);
+          const float inv = mx_inv_scale(e);
+          int x = __builtin_amdgcn_cvt_pk_fp8_f32(o[0] * inv, o[1] * inv, 0, false);
+          x = __builtin_amdgcn_cvt_pk_fp8_f32(o[2] * inv, o[3] * inv, x, true);
+          if (ok[u]) {
+            *(int*)((unsigned char*)g.Ct + off[u]) = x;
+            if ((threadIdx.x & 7) == 0) {
+              const int m = m0 + mi * 128 + ((base + u * 512) >> 6);
+              g.c_scale[mx_a_scale_off(m, n >> 5, g.N >> 7)] = (unsigned char)e;
+            }
+          }
+          continue;
+        }
         if (ok[u]) {
           if (g.Cf) g8_st<NT>((f32x4*)(g.Cf + off[u]), o);
           if (g.Ct) {
@@ -352,48 +486,6 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
 // retire in issue order) and the stores drain under the first K-tile's MFMAs.  From K-tile 1
 // on, waits target loads issued after the stores and the plain counts apply.
 // ======================================================================================
-SSE_DEV void g8_vmcnt_dyn(int n) {   // n even, 0..62 (vmcnt is 6 bits)
-  switch (n >> 1) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
-    case 11: asm volatile("s_waitcnt vmcnt(22)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
-    case 13: asm volatile("s_waitcnt vmcnt(26)" ::: "memory"); break;
-    case 14: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
-    case 15: asm volatile("s_waitcnt vmcnt(30)" ::: "memory"); break;
-    case 16: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
-    case 17: asm volatile("s_waitcnt vmcnt(34)" ::: "memory"); break;
-    case 18: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
-    case 19: asm volatile("s_waitcnt vmcnt(38)" ::: "memory"); break;
-    case 20: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
-    case 21: asm volatile("s_waitcnt vmcnt(42)" ::: "memory"); break;
-    case 22: asm volatile("s_waitcnt vmcnt(44)" ::: "memory"); break;
-    case 23: asm volatile("s_waitcnt vmcnt(46)" ::: "memory"); break;
-    case 24: asm volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
-    case 25: asm volatile("s_waitcnt vmcnt(50)" ::: "memory"); break;
-    case 26: asm volatile("s_waitcnt vmcnt(52)" ::: "memory"); break;
-    case 27: asm volatile("s_waitcnt vmcnt(54)" ::: "memory"); break;
-    case 28: asm volatile("s_waitcnt vmcnt(56)" ::: "memory"); break;
-    case 29: asm volatile("s_waitcnt vmcnt(58)" ::: "memory"); break;
-    case 30: asm volatile("s_waitcnt vmcnt(60)" ::: "memory"); break;
-    case 31: asm volatile("s_waitcnt vmcnt(62)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
-}
-
-SSE_DEV int g8_count(int k, int nk) {   // vmcnt of g8_wait(k, nk)
-  return 2 * (g8_issued(k, nk) + g8_issued(k - 1, nk) + g8_issued(k - 2, nk) + g8_issued(k - 3, nk));
-}
-
 // tile of block b in round r (-1: idle), XCD-aware bijective remap within the round
 SSE_DEV int g8p_tile(int b, int r, int G, int n_tiles) {
   const int base = r * G;
@@ -411,7 +503,8 @@ SSE_DEV int g8p_tile(int b, int r, int G, int n_tiles) {
 // finished in place in acc, then the residual of mi = 1 is loaded into the same registers, THEN
 // the mi = 0 stores go out.
 // RES = false compiles the residual out (the caller guarantees g.resid == nullptr).
-template <bool RES>
+// Q8 = true: Ct is MX-fp8 (e4m3 + g.c_scale, see store_half_q8).
+template <bool RES, bool Q8>
 SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, int n0, int wm, int wn,
                                 int q, int r16) {
   const bool has_bias = g.bias != nullptr, has_res = RES && g.resid != nullptr, ln = RES && g.rstats != nullptr;
@@ -502,46 +595,93 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
       }
     }
   };
+  // MX-fp8 out (the next GEMM's A operand): the 32 columns n0 + ni*128 + wn*32 + [0, 32) of a row
+  // are one MX block, held by the row's four q lanes (j = 0, 1 each).  amax over the 8 values and
+  // across q (xor 16, 32), E8M0 exponent mx_scale_exp, e4m3 = RNE(x * 2^-E) (v_cvt_pk_fp8_f32),
+  // the same lane-pair exchange as the bf16 path (8 consecutive bytes per lane).  The four lanes of
+  // a row hold the same exponents; lane q stores the scale dword (i = 0..3) of (mi, ni) = (q>>1, q&1).
+  unsigned scw[2][2] = {{0u, 0u}, {0u, 0u}};
+  auto store_half_q8 = [&](int mi) {
+    unsigned char* C8 = (unsigned char*)g.Ct;
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + mi * 128 + wm * 64 + i * 16 + r16;
+      const bool ok = m < g.M;
+      const long long row = (long long)(ok ? m : 0) * g.ldc;
+      #pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const f32x4 o0 = acc[mi][ni][i][0], o1 = acc[mi][ni][i][1];
+        float a = fmaxf(fmaxf(fmaxf(fabsf(o0[0]), fabsf(o0[1])), fmaxf(fabsf(o0[2]), fabsf(o0[3]))),
+                        fmaxf(fmaxf(fabsf(o1[0]), fabsf(o1[1])), fmaxf(fabsf(o1[2]), fabsf(o1[3]))));
+        a = fmaxf(a, __shfl_xor(a, 16, 64));
+        a = fmaxf(a, __shfl_xor(a, 32, 64));
+        const int e = mx_scale_exp(a);
+        const float inv = mx_inv_scale(e);
+        int x0 = __builtin_amdgcn_cvt_pk_fp8_f32(o0[0] * inv, o0[1] * inv, 0, false);
+        x0 = __builtin_amdgcn_cvt_pk_fp8_f32(o0[2] * inv, o0[3] * inv, x0, true);
+        int x1 = __builtin_amdgcn_cvt_pk_fp8_f32(o1[0] * inv, o1[1] * inv, 0, false);
+        x1 = __builtin_amdgcn_cvt_pk_fp8_f32(o1[2] * inv, o1[3] * inv, x1, true);
+        const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)x0, (unsigned)x1, false, false);
+        if (ok) *(uint2*)(C8 + row + n0 + ni * 128 + wn * 32 + (q & 1) * 16 + (q >> 1) * 8) = make_uint2(sw[0], sw[1]);
+        scw[mi][ni] |= (unsigned)e << (8 * i);
+      }
+    }
+  };
   load_half(0);
   finish_half(0);
   load_half(1);
-  store_half(0);
+  if constexpr (Q8) store_half_q8(0); else store_half(0);
   finish_half(1);
-  store_half(1);
+  if constexpr (Q8) {
+    store_half_q8(1);
+    const int mi = q >> 1, ni = q & 1;
+    const unsigned v = mi ? (ni ? scw[1][1] : scw[1][0]) : (ni ? scw[0][1] : scw[0][0]);
+    const long long m = m0 + mi * 128 + wm * 64 + r16;
+    *(unsigned*)(g.c_scale + mx_a_scale_off(m, (n0 + ni * 128 + wn * 32) >> 5, g.N >> 7)) = v;
+  } else {
+    store_half(1);
+  }
 }
 
 // RES = false only: residual GEMMs keep the non-persistent LDS-staged kernel (their epilogue
 // would need the residual tile in registers next to the accumulators).
-template <bool RES>
+template <bool RES, bool MX = false, bool Q8 = false>
 __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
-  __shared__ __attribute__((aligned(16))) char smem[G8_OPS];   // the ONLY shared object
+  __shared__ __attribute__((aligned(16))) char smem[MX ? G8_OPS_MX : G8_OPS];   // the ONLY shared object
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   const int q = lane >> 4, r16 = lane & 15;
   const int M = g.M, K = g.K;
   const int n_tiles_n = g.N / 256;
-  const int nk = K / 64;
+  constexpr int ES = MX ? 1 : 2;
+  const int nk = K / (128 / ES);
   const int G = gridDim.x, b = blockIdx.x;
   // stores per wave of one full tile (the count the next tile's first K-tile may leave in
   // flight); under-counting is safe, so it is capped to keep 2n + S within vmcnt's 6 bits
-  const int s_full = min(32 * (g.Cf ? 1 : 0) + 16 * (g.Ct ? 1 : 0), 54);
+  const int s_full = min(32 * (g.Cf ? 1 : 0) + 16 * (g.Ct ? 1 : 0), 54);   // 54 + 9 <= 63
 
   int round = 0;
   int tile = g8p_tile(b, 0, G, n_tiles);
   if (tile < 0) return;
 
   constexpr int NREC = 0x7FFFFFF0;
-  __amdgpu_buffer_rsrc_t a_rsrc, b_rsrc;
-  unsigned a_voff[2][2], b_voff[2][2];
+  __amdgpu_buffer_rsrc_t a_rsrc, b_rsrc, s_rsrc;
+  unsigned a_voff[2][2], b_voff[2][2], s_voff = 0;
   auto setup = [&](int tl) {
     const int m0 = (tl / n_tiles_n) * 256, n0 = (tl % n_tiles_n) * 256;
     const int mf = m0 < M ? m0 : M - 1;
     const int seg0 = mf / g.rows_per_seg, rr0 = mf - seg0 * g.rows_per_seg;
-    const long long a_base = (long long)seg0 * g.seg_stride + (long long)rr0 * g.lda;
-    a_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const bf16*)g.A + a_base), (short)0, NREC, 0x00020000);
-    b_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const bf16*)g.B + (long long)n0 * K), (short)0, NREC,
+    const long long a_base = ((long long)seg0 * g.seg_stride + (long long)rr0 * g.lda) * ES;   // bytes
+    a_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)g.A + a_base), (short)0, NREC, 0x00020000);
+    b_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)g.B + (long long)n0 * K * ES), (short)0, NREC,
                                                0x00020000);
+    if constexpr (MX) {   // this tile's scale blocks; waves 0-3 stage A's 1 KiB, waves 4-7 B's
+      const unsigned char* sb = wave < 4 ? g.a_scale + (long long)(m0 >> 8) * nk * 1024
+                                         : g.b_scale + (long long)(n0 >> 8) * nk * 1024;
+      s_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)sb, (short)0, NREC, 0x00020000);
+      s_voff = (unsigned)((wave & 3) * 256 + lane * 4);
+    }
     #pragma unroll
     for (int h = 0; h < 2; ++h)
       #pragma unroll
@@ -551,9 +691,9 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
         int m = m0 + row;
         m = m < M ? m : M - 1;
         const int seg = m / g.rows_per_seg, rr = m - seg * g.rows_per_seg;
-        const long long el = (long long)seg * g.seg_stride + (long long)rr * g.lda + ch * 8;
-        a_voff[h][s] = (unsigned)((el - a_base) * 2);
-        b_voff[h][s] = (unsigned)(((long long)row * K + ch * 8) * 2);
+        const long long el = ((long long)seg * g.seg_stride + (long long)rr * g.lda) * ES + ch * 16;
+        a_voff[h][s] = (unsigned)(el - a_base);
+        b_voff[h][s] = (unsigned)((long long)row * K * ES + ch * 16);
       }
   };
   auto issue = [&](int k) {
@@ -563,6 +703,11 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
     if (tl >= nk) return;
     char* dst = smem + (tl & 1) * G8_BUF + half * G8_HALF;
     const unsigned soff = (unsigned)tl * 128u;
+    if constexpr (MX) {
+      if (half == 0)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(s_rsrc, LPTR(smem + G8_OPS + (tl & 3) * G8_SC + wave * 256), 4,
+                                                 s_voff, (unsigned)tl * 1024u, 0, 0);
+    }
     if (half < 2) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, LPTR(dst + wave * 1024), 16, a_voff[half][0], soff, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, LPTR(dst + (wave + 8) * 1024), 16, a_voff[half][1], soff, 0, 0);
@@ -575,34 +720,67 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
 
   f32x4 acc[2][2][4][2];
   bf16x8 af[4][2], b0f[2][2], b1f[2][2];
+  int sa = 0, sb = 0;
+  auto read_sa = [&](int t, int mi) {
+    if constexpr (MX) sa = *(const int*)(smem + G8_OPS + (t & 3) * G8_SC + (((mi * 2 + wm) * 4 + q) * 16 + r16) * 4);
+  };
+  auto read_sb = [&](int t) {
+    if constexpr (MX) sb = *(const int*)(smem + G8_OPS + (t & 3) * G8_SC + 1024 + ((wn * 4 + q) * 16 + r16) * 4);
+  };
+  // MX: the same two 16-B reads per fragment, landing in one 8-dword operand tuple
+  i32x8 afx[4], b0x[2], b1x[2];
+  auto rd32 = [&](const char* hb, int row) {
+    const i32x4 lo = *(const i32x4*)(hb + row * 128 + ((q ^ ((row >> 1) & 7)) * 16));
+    const i32x4 hi = *(const i32x4*)(hb + row * 128 + (((q + 4) ^ ((row >> 1) & 7)) * 16));
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
   auto read_a = [&](const char* hb) {
     #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = wm * 64 + i * 16 + r16;
-      #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        af[i][ks] = *(const bf16x8*)(hb + row * 128 + (((q + 4 * ks) ^ ((row >> 1) & 7)) * 16));
+      if constexpr (MX) {
+        afx[i] = rd32(hb, row);
+      } else {
+        #pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          af[i][ks] = *(const bf16x8*)(hb + row * 128 + (((q + 4 * ks) ^ ((row >> 1) & 7)) * 16));
+      }
     }
   };
-  auto read_b = [&](const char* hb, bf16x8 (&bf)[2][2]) {
+  auto read_b = [&](const char* hb, bf16x8 (&bf)[2][2], i32x8 (&bx)[2]) {
     #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int row = wn * 32 + j * 16 + r16;
-      #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        bf[j][ks] = *(const bf16x8*)(hb + row * 128 + (((q + 4 * ks) ^ ((row >> 1) & 7)) * 16));
+      if constexpr (MX) {
+        bx[j] = rd32(hb, row);
+      } else {
+        #pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          bf[j][ks] = *(const bf16x8*)(hb + row * 128 + (((q + 4 * ks) ^ ((row >> 1) & 7)) * 16));
+      }
     }
   };
-  auto mma = [&](f32x4 (&c)[4][2], const bf16x8 (&bf)[2][2]) {
+  auto mma = [&](f32x4 (&c)[4][2], const bf16x8 (&bf)[2][2], const i32x8 (&bx)[2], auto ni_c) {
+    constexpr int NI = decltype(ni_c)::value;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
-    #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    if constexpr (MX) {
+      g8_sfor<0, 4>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        g8_sfor<0, 2>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          c[i][j] = g8_mx<NI * 2 + j, i>(bx[j], afx[i], c[i][j], sb, sa);
+        });
+      });
+    } else {
       #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int ks = 0; ks < 2; ++ks)
         #pragma unroll
-        for (int j = 0; j < 2; ++j) c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][ks], af[i][ks], c[i][j], 0, 0, 0);
+        for (int i = 0; i < 4; ++i)
+          #pragma unroll
+          for (int j = 0; j < 2; ++j) c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][ks], af[i][ks], c[i][j], 0, 0, 0);
+    }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -620,7 +798,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
         for (int i = 0; i < 4; ++i)
           #pragma unroll
           for (int j = 0; j < 2; ++j) acc[a][c][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    g8_vmcnt_dyn(g8_count(-1, nk) + S);
+    g8_vmcnt_dyn<MX>(g8_count<MX>(-1, nk) + S);
     g8_barrier();
     if (wm == 1) g8_barrier();   // group 1 runs one barrier behind
 
@@ -633,32 +811,38 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
       auto issue_wait = [&](int kk) {
         issue(kk);
         if constexpr (FI) {
-          g8_vmcnt_dyn(g8_count(kk, nk) + S);
+          g8_vmcnt_dyn<MX>(g8_count<MX>(kk, nk) + S);
         } else if constexpr (ST) {
-          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          if constexpr (MX) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         } else {
-          g8_wait(kk, nk);
+          g8_wait<MX>(kk, nk);
         }
       };
+      const std::integral_constant<int, 0> ni0;
+      const std::integral_constant<int, 1> ni1;
       read_a(buf);
-      read_b(buf + 2 * G8_HALF, b0f);
+      read_b(buf + 2 * G8_HALF, b0f, b0x);
+      read_sa(t, 0);
+      read_sb(t);
       issue_wait(k);
       g8_barrier();
-      mma(acc[0][0], b0f);
+      mma(acc[0][0], b0f, b0x, ni0);
       g8_barrier();
-      read_b(buf + 3 * G8_HALF, b1f);
+      read_b(buf + 3 * G8_HALF, b1f, b1x);
       issue_wait(k + 1);
       g8_barrier();
-      mma(acc[0][1], b1f);
+      mma(acc[0][1], b1f, b1x, ni1);
       g8_barrier();
       read_a(buf + G8_HALF);
+      read_sa(t, 1);
       issue_wait(k + 2);
       g8_barrier();
-      mma(acc[1][1], b1f);
+      mma(acc[1][1], b1f, b1x, ni1);
       g8_barrier();
       issue_wait(k + 3);
       g8_barrier();
-      mma(acc[1][0], b0f);
+      mma(acc[1][0], b0f, b0x, ni0);
       g8_barrier();
     };
     run_tile(0, std::integral_constant<bool, false>{}, std::integral_constant<bool, true>{});
@@ -673,7 +857,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
       setup(next);
       for (int k = -6; k < 0; ++k) issue(k);
     }
-    g8_epilogue_direct<RES>(g, acc, m0, n0, wm, wn, q, r16);
+    g8_epilogue_direct<RES, Q8>(g, acc, m0, n0, wm, wn, q, r16);
     if (next < 0) break;
     S = m0 + 256 <= M ? s_full : 0;
     tile = next;
@@ -709,5 +893,18 @@ int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
     const int G = n_tiles < cus[dev] ? n_tiles : cus[dev];
     hipLaunchKernelGGL(gemm8p_kernel<false>, dim3(G), dim3(512), 0, s, a, n_tiles);
   }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// MX-fp8 operands (K % 128 == 0, N % 256 == 0, plain row-major A with lda == K); output fp32 (Cf,
+// optional residual), bf16 (Ct) or MX-fp8 (Ct + c_scale, A layout of a GEMM with K = N).
+int launch_gemm8_mx(const GemmArgs& a, hipStream_t s) {
+  if (a.M <= 0 || a.N % 256 || a.K % 128 || a.K <= 0 || !a.a_scale || !a.b_scale) return -3;
+  if (a.rows_per_seg != a.M || a.lda != a.K) return -3;
+  if (a.c_scale && (a.Cf || !a.Ct)) return -3;
+  dim3 grid((unsigned)(((a.M + 255) / 256) * (a.N / 256)));
+  // LDS-staged epilogue for every MX shape: the persistent direct-epilogue kernel exceeds 256
+  // VGPRs with the MX operand tuples and would spill inside the counted-vmcnt main loop
+  hipLaunchKernelGGL((gemm8_kernel<0, false, false, true>), grid, dim3(512), 0, s, a);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

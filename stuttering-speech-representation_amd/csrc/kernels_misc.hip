@@ -236,6 +236,22 @@ template <> SSE_DEV f32x4 load4<bf16>(const bf16* p) {
   return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
 }
 
+// MX-fp8 quantisation of 4 consecutive values (columns c..c+3 of row `row`, K = H) held by a lane
+// whose 7 neighbours (lane ^ 1, 2, 4) hold the rest of the 32-column block: amax, E8M0 exponent
+// (mx_scale_exp), e4m3 = RNE(x * 2^-E), one dword store; lane % 8 == 0 stores the scale byte.
+SSE_DEV void mx_quant4(f32x4 o, unsigned char* dst, unsigned char* scale, long long row, int c, int K, int lane) {
+  float a = fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3])));
+  a = fmaxf(a, __shfl_xor(a, 1, 64));
+  a = fmaxf(a, __shfl_xor(a, 2, 64));
+  a = fmaxf(a, __shfl_xor(a, 4, 64));
+  const int e = mx_scale_exp(a);
+  const float inv = mx_inv_scale(e);
+  int x = __builtin_amdgcn_cvt_pk_fp8_f32(o[0] * inv, o[1] * inv, 0, false);
+  x = __builtin_amdgcn_cvt_pk_fp8_f32(o[2] * inv, o[3] * inv, x, true);
+  *(int*)dst = x;
+  if ((lane & 7) == 0) scale[mx_a_scale_off(row, c >> 5, K >> 7)] = (unsigned char)e;
+}
+
 template <typename TI, typename TO>
 __global__ __launch_bounds__(256) void layernorm_kernel(const TI* __restrict__ in, const float* __restrict__ w,
                                                         const float* __restrict__ bta, int rows, int H,
@@ -267,7 +283,8 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TI* __restrict__ i
         q = fmaf(d, d, q);
       }
   const float rstd = 1.0f / sqrtf(wave_sum(q) / H + eps);
-  if (stats && lane == 0) stats[row] = make_float2(mean, rstd);
+  if constexpr (sizeof(TO) != 1)
+    if (stats && lane == 0) stats[row] = make_float2(mean, rstd);
   #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int g = lane + 64 * i;
@@ -282,7 +299,11 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TI* __restrict__ i
       }
       const long long off = (long long)row * H + c;
       if (out_f) *(f32x4*)(out_f + off) = o;
-      if (out_t) {
+      if constexpr (sizeof(TO) == 1) {
+        // MX-fp8 GEMM operand (A layout): 8 lanes = one 32-column block (H % 32 == 0, so a block's
+        // lanes are active together); out_t is e4m3 bytes, stats carries the scale tensor
+        mx_quant4(o, (unsigned char*)out_t + off, (unsigned char*)stats, row, c, H, lane);
+      } else if (out_t) {
         if constexpr (sizeof(TO) == 2) {
           bf16x4 ob = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
           *(bf16x4*)(out_t + off) = ob;
@@ -308,6 +329,52 @@ template int launch_layernorm<float, bf16>(const float*, const float*, const flo
                                            float*, bf16*, hipStream_t, float2*);
 template int launch_layernorm<bf16, bf16>(const bf16*, const float*, const float*, int, int, float, int, float*,
                                           bf16*, hipStream_t, float2*);
+
+int launch_layernorm_mx(const float* in, const float* w, const float* b, int rows, int H, float eps,
+                        unsigned char* q, unsigned char* scale, hipStream_t s) {
+  if (H % 128 || H > 2048) return -3;
+  hipLaunchKernelGGL((layernorm_kernel<float, unsigned char>), dim3((rows + 3) / 4), dim3(256), 0, s, in, w, b, rows,
+                     H, eps, (int)ACT_NONE, (float*)nullptr, q, (float2*)scale);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// ---------------------------------------------------------------------------------------
+// MX-fp8 quantisation of a row-major fp32 [R][K] tensor (K % 128 == 0) into e4m3 bytes [R][K]
+// and E8M0 scales in the GEMM's A layout (role 0) or B layout (role 1).  One wave per (row,
+// 256-column segment), 4 values per lane.
+__global__ __launch_bounds__(256) void mx_quantize_kernel(const float* __restrict__ x, int R, int K, int role,
+                                                          unsigned char* __restrict__ q,
+                                                          unsigned char* __restrict__ scale) {
+  const int segs = (K + 255) / 256;
+  const long long wid = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wid >= (long long)R * segs) return;
+  const int lane = threadIdx.x & 63;
+  const long long row = wid / segs;
+  const int c = (int)(wid % segs) * 256 + lane * 4;
+  if (c >= K) return;   // whole 8-lane blocks leave together (K % 32 == 0)
+  const f32x4 o = *(const f32x4*)(x + row * K + c);
+  if (role == 0) {
+    mx_quant4(o, q + row * K + c, scale, row, c, K, lane);
+  } else {
+    float a = fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3])));
+    a = fmaxf(a, __shfl_xor(a, 1, 64));
+    a = fmaxf(a, __shfl_xor(a, 2, 64));
+    a = fmaxf(a, __shfl_xor(a, 4, 64));
+    const int e = mx_scale_exp(a);
+    const float inv = mx_inv_scale(e);
+    int v = __builtin_amdgcn_cvt_pk_fp8_f32(o[0] * inv, o[1] * inv, 0, false);
+    v = __builtin_amdgcn_cvt_pk_fp8_f32(o[2] * inv, o[3] * inv, v, true);
+    *(int*)(q + row * K + c) = v;
+    if ((lane & 7) == 0) scale[mx_b_scale_off(row, c >> 5, K >> 7)] = (unsigned char)e;
+  }
+}
+
+int launch_mx_quantize(const float* x, int R, int K, int role, unsigned char* q, unsigned char* scale, hipStream_t s) {
+  if (R <= 0 || K <= 0 || K % 128) return -3;
+  const long long waves = (long long)R * ((K + 255) / 256);
+  hipLaunchKernelGGL(mx_quantize_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, x, R, K, role, q, scale);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
 
 // ---------------------------------------------------------------------------------------
 // K8/K12: out[b*out_stride + n] = mean_t x[b][t][n]  (torch.mean(hs, dim=1), fp64 accumulation).

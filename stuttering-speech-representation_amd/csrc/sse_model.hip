@@ -40,6 +40,42 @@ inline uint16_t f2bf_bits(float f) {
   return (uint16_t)(u >> 16);
 }
 
+// OCP e4m3 (e4m3fn) of |y| <= 448 with round-to-nearest-even: what v_cvt_pk_fp8_f32 produces
+// (checked exhaustively against nearest-even search, tools/probe_mx.hip).  Bit-level on the fp32.
+uint8_t f32_to_e4m3(float y) {
+  uint32_t u;
+  std::memcpy(&u, &y, 4);
+  const uint8_t sign = (uint8_t)((u >> 24) & 0x80);
+  u &= 0x7FFFFFFFu;
+  if (u >= 0x43E00000u) return sign | 0x7E;                  // >= 448: saturate (never reached by mx)
+  if (u < 0x3C800000u) {                                      // < 2^-6: subnormal m * 2^-9, m in [0, 8]
+    float a;
+    std::memcpy(&a, &u, 4);
+    const float m = std::nearbyint(a * 512.0f);               // exact scaling, ties to even
+    return sign | (uint8_t)m;                                 // m == 8 is the first normal (0x08)
+  }
+  uint32_t keep = u >> 20;                                    // float exponent | top 3 mantissa bits
+  const uint32_t rem = u & 0xFFFFFu;
+  if (rem > 0x80000u || (rem == 0x80000u && (keep & 1))) ++keep;   // carry rolls into the exponent
+  const int e = (int)(keep >> 3) - 127 + 7;
+  return sign | (uint8_t)((e << 3) | (keep & 7));
+}
+
+// MX quantisation of row-major x [R][K] (K % 128 == 0): e4m3 bytes + E8M0 scales (role 0: A layout,
+// 1: B layout), the same arithmetic as mx_quant4 (kernels_misc.hip)
+void mx_quantize_rows(const float* x, int R, int K, int role, uint8_t* q, uint8_t* scale) {
+  for (int r = 0; r < R; ++r)
+    for (int b = 0; b < K / 32; ++b) {
+      const float* v = x + (size_t)r * K + b * 32;
+      float amax = 0.f;
+      for (int i = 0; i < 32; ++i) amax = std::fmax(amax, std::fabs(v[i]));
+      const int e = mx_scale_exp(amax);
+      const float inv = mx_inv_scale(e);
+      for (int i = 0; i < 32; ++i) q[(size_t)r * K + b * 32 + i] = f32_to_e4m3(v[i] * inv);
+      scale[role ? mx_b_scale_off(r, b, K / 128) : mx_a_scale_off(r, b, K / 128)] = (uint8_t)e;
+    }
+}
+
 int rel_bucket(int d, int num_buckets, int max_distance) {
   // HF WavLMAttention._relative_positions_bucket (modeling_wavlm.py:246-271), float32 path
   const int nb = num_buckets / 2;
@@ -87,11 +123,20 @@ struct Arena {
     for (size_t i = 0; i < v.size(); ++i) h[i] = f2bf_bits(v[i]);
     return put(h.data(), h.size() * 2);
   }
+  // MX-fp8 weight [N][K] (B layout): e4m3 bytes at the returned offset, scales at *scale_off
+  size_t put_mx(const std::vector<float>& v, int N, int K, size_t* scale_off) {
+    std::vector<uint8_t> q((size_t)N * K), sc((size_t)mx_scale_bytes(N, K), 0x7F);
+    mx_quantize_rows(v.data(), N, K, 1, q.data(), sc.data());
+    const size_t o = put(q.data(), q.size());
+    *scale_off = put(sc.data(), sc.size());
+    return o;
+  }
 };
 
 struct LayerW {
   size_t qkv_w, qkv_b, o_w, o_b, ln1_w, ln1_b, f1_w, f1_b, f2_w, f2_b, ln2_w, ln2_b;
   size_t g_const, g_w, g_b;   // WavLM gate
+  size_t qkv_q, qkv_s, f1_q, f1_s, f2_q, f2_s;   // SSE_DTYPE_FP8: MX-fp8 copies (e4m3 + scales)
 };
 
 // Whisper decoder layer for the 1-token pass (HF/models/whisper/modeling_whisper.py:448-506)
@@ -129,7 +174,8 @@ struct sse_model {
   } prof;
 
   template <typename X = void> const X* ptr(size_t off) const { return (const X*)(dmem + off); }
-  bool bf() const { return dtype == SSE_DTYPE_BF16; }
+  bool bf() const { return dtype == SSE_DTYPE_BF16 || dtype == SSE_DTYPE_FP8; }   // bf16 activations
+  bool mx() const { return dtype == SSE_DTYPE_FP8; }   // MX-fp8 encoder-layer GEMMs (Whisper)
 };
 
 namespace {
@@ -306,6 +352,11 @@ int build_whisper(sse_model* m, Blob& bl, Arena& ar) {
     L.qkv_w = ar.put_elem(qkv, BF);
     L.qkv_b = ar.put_f32(qkvb.data(), 3 * D);
     m->ldq = 3 * D;
+    if (m->mx()) {
+      L.qkv_q = ar.put_mx(qkv, 3 * D, D, &L.qkv_s);
+      L.f1_q = ar.put_mx(std::vector<float>(f1w, f1w + (size_t)F * D), F, D, &L.f1_s);
+      L.f2_q = ar.put_mx(std::vector<float>(f2w, f2w + (size_t)D * F), D, F, &L.f2_s);
+    }
     L.o_w = ar.put_elem(std::vector<float>(ow, ow + (size_t)D * D), BF);
     L.o_b = ar.put_f32(ob, D);
     L.ln1_w = ar.put_f32(l1w, D);
@@ -802,14 +853,40 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
   T* qkv = (T*)(ws + w.qkv);
   T* ctx = (T*)(ws + w.ctx);
   T* ff = (T*)(ws + w.ff);
+  // SSE_DTYPE_FP8: LayerNorm writes the MX-fp8 operand (e4m3 + scales) into xb's space, fc1 writes
+  // MX-fp8 into ff's space; QKV / fc1 / fc2 run on the MX GEMM (kernels_gemm8.hip)
+  const bool mx = m->mx();
+  unsigned char* xq = (unsigned char*)(ws + w.xb);
+  unsigned char* xq_s = xq + (size_t)M * D;
+  unsigned char* fq = (unsigned char*)(ws + w.ff);
+  unsigned char* fq_s = fq + (size_t)M * F;
+  auto mx_gemm = [&](const char* tag, const unsigned char* A, const unsigned char* As, size_t wq, size_t wsc, size_t bo,
+                     int N, int K, const float* resid, float* Cf, void* Ct, unsigned char* Cs, int act) {
+    GemmArgs g{};
+    g.A = A; g.a_scale = As; g.B = m->ptr(wq); g.b_scale = m->ptr<unsigned char>(wsc);
+    g.M = M; g.N = N; g.K = K; g.rows_per_seg = M; g.lda = K;
+    g.bias = m->ptr<float>(bo); g.resid = resid; g.Cf = Cf; g.Ct = Ct; g.c_scale = Cs; g.ldc = N; g.act = act;
+    g.zero = zero;
+    const double bytes = (double)M * K + (double)N * K + (M + (double)N) * K / 32.0 +
+                         (double)M * N * (Cf ? 4.0 : 0.0) + (double)M * N * (resid ? 4.0 : 0.0) +
+                         (Ct ? (double)M * N * (Cs ? 1.0 + 1.0 / 32 : 2.0) : 0.0);
+    return prof(m, s, tag, gflops(g), bytes, [&] { return launch_gemm8_mx(g, s); });
+  };
   for (int l = 0; l < c.layers; ++l) {
     const LayerW& Lw = m->layers[l];
-    RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, D, eps, ACT_NONE, nullptr,
-                                   xb, s)));
+    if (mx) {
+      RC(launch_layernorm_mx(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, D, eps, xq, xq_s, s));
+      RC(mx_gemm("gemm_mx:qkv", xq, xq_s, Lw.qkv_q, Lw.qkv_s, Lw.qkv_b, 3 * D, D, nullptr, nullptr, qkv, nullptr,
+                 ACT_NONE));
+    } else {
+      RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, D, eps, ACT_NONE, nullptr,
+                                     xb, s)));
+      GemmArgs g{};
+      g.A = xb; g.B = m->ptr(Lw.qkv_w); g.M = M; g.N = 3 * D; g.K = D; g.rows_per_seg = M; g.lda = D;
+      g.bias = m->ptr<float>(Lw.qkv_b); g.Ct = qkv; g.ldc = 3 * D; g.zero = zero;
+      RC(prof(m, s, "gemm:qkv", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    }
     GemmArgs g{};
-    g.A = xb; g.B = m->ptr(Lw.qkv_w); g.M = M; g.N = 3 * D; g.K = D; g.rows_per_seg = M; g.lda = D;
-    g.bias = m->ptr<float>(Lw.qkv_b); g.Ct = qkv; g.ldc = 3 * D; g.zero = zero;
-    RC(prof(m, s, "gemm:qkv", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     AttnArgs a{};
     a.qkv = qkv; a.out = ctx; a.T = Tq; a.H = D; a.nh = nh; a.ldq = m->ldq; a.scale = 1.0f;
     RC(prof(m, s, "attn", 4.0 * B * (double)Tq * Tq * D, (double)B * Tq * 4.0 * D * sizeof(T),
@@ -818,6 +895,14 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
     g.A = ctx; g.B = m->ptr(Lw.o_w); g.M = M; g.N = D; g.K = D; g.rows_per_seg = M; g.lda = D;
     g.bias = m->ptr<float>(Lw.o_b); g.resid = x; g.Cf = x; g.ldc = D; g.zero = zero;
     RC(prof(m, s, "gemm:oproj", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    if (mx) {
+      RC(launch_layernorm_mx(x, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, D, eps, xq, xq_s, s));
+      RC(mx_gemm("gemm_mx:ffn1", xq, xq_s, Lw.f1_q, Lw.f1_s, Lw.f1_b, F, D, nullptr, nullptr, fq, fq_s,
+                 gelu_rounded_act<T>()));
+      RC(mx_gemm("gemm_mx:ffn2", fq, fq_s, Lw.f2_q, Lw.f2_s, Lw.f2_b, D, F, x, x, nullptr, nullptr, ACT_NONE));
+      if (l + 1 < c.layers) RC(sink.emit(l + 1, x));
+      continue;
+    }
     RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, D, eps, ACT_NONE, nullptr,
                                    xb, s)));
     g = GemmArgs{};
@@ -913,8 +998,12 @@ size_t sse_weight_floats(const sse_cfg* cfg) {
 
 int sse_model_create(const sse_cfg* cfg, const float* host_weights, size_t nbytes, int device, int dtype,
                      sse_model** out) {
-  if (!out || !host_weights || !cfg_valid(cfg) || (dtype != SSE_DTYPE_F32 && dtype != SSE_DTYPE_BF16))
+  if (!out || !host_weights || !cfg_valid(cfg) ||
+      (dtype != SSE_DTYPE_F32 && dtype != SSE_DTYPE_BF16 && dtype != SSE_DTYPE_FP8))
     return SSE_ERR_INVALID;
+  // MX-fp8 GEMMs: N % 256 and K % 128 for QKV (3D x D), fc1 (F x D), fc2 (D x F)
+  if (dtype == SSE_DTYPE_FP8 && (cfg->kind != SSE_KIND_WHISPER || cfg->hidden % 256 || cfg->ffn % 256))
+    return SSE_ERR_UNSUPPORTED;
   *out = nullptr;
   const size_t need = sse_weight_floats(cfg);
   if (need == 0 || nbytes != need * 4) return SSE_ERR_WEIGHTS;
@@ -1132,6 +1221,41 @@ int sse_gemm(int dtype, const void* d_a, const void* d_b, const float* d_bias, c
   g.bias = d_bias; g.resid = d_resid; g.Cf = d_cf; g.Ct = d_ct; g.ldc = N; g.act = act; g.zero = d_zero;
   return dtype == SSE_DTYPE_BF16 ? launch_gemm_bf16(g, AMODE_SEG, 1, (hipStream_t)stream)
                                  : launch_gemm_f32(g, AMODE_SEG, 1, (hipStream_t)stream);
+}
+
+size_t sse_mx_scale_bytes(int R, int K) {
+  if (R <= 0 || K <= 0 || K % 128) return 0;
+  return (size_t)mx_scale_bytes(R, K);
+}
+
+long long sse_mx_scale_offset(int role, int r, int b, int K) {
+  if (r < 0 || b < 0 || K <= 0 || K % 128 || b >= K / 32) return -1;
+  return role ? mx_b_scale_off(r, b, K / 128) : mx_a_scale_off(r, b, K / 128);
+}
+
+int sse_mx_quantize(const float* d_x, int R, int K, int role, uint8_t* d_q, uint8_t* d_scale, void* stream) {
+  if (!d_x || !d_q || !d_scale || R <= 0 || K <= 0 || K % 128 || (role != 0 && role != 1)) return SSE_ERR_INVALID;
+  return launch_mx_quantize(d_x, R, K, role, d_q, d_scale, (hipStream_t)stream) ? SSE_ERR_HIP : SSE_OK;
+}
+
+int sse_mx_quantize_host(const float* x, int R, int K, int role, uint8_t* q, uint8_t* scale) {
+  if (!x || !q || !scale || R <= 0 || K <= 0 || K % 128 || (role != 0 && role != 1)) return SSE_ERR_INVALID;
+  mx_quantize_rows(x, R, K, role, q, scale);
+  return SSE_OK;
+}
+
+int sse_gemm_mx(const uint8_t* d_a, const uint8_t* d_a_scale, const uint8_t* d_b, const uint8_t* d_b_scale,
+                const float* d_bias, const float* d_resid, float* d_cf, void* d_ct, uint8_t* d_c_scale, int M, int N,
+                int K, int act, void* stream) {
+  if (!d_a || !d_a_scale || !d_b || !d_b_scale || M <= 0 || N <= 0 || K <= 0 || (!d_cf && !d_ct)) return SSE_ERR_INVALID;
+  if (N % 256 || K % 128) return SSE_ERR_UNSUPPORTED;
+  if (d_c_scale && (d_cf || !d_ct || d_resid)) return SSE_ERR_INVALID;
+  if (d_resid && d_ct) return SSE_ERR_UNSUPPORTED;
+  GemmArgs g{};
+  g.A = d_a; g.a_scale = d_a_scale; g.B = d_b; g.b_scale = d_b_scale; g.M = M; g.N = N; g.K = K;
+  g.rows_per_seg = M; g.lda = K; g.bias = d_bias; g.resid = d_resid; g.Cf = d_cf; g.Ct = d_ct; g.c_scale = d_c_scale;
+  g.ldc = N; g.act = act;
+  return launch_gemm8_mx(g, (hipStream_t)stream) ? SSE_ERR_HIP : SSE_OK;
 }
 
 int sse_normalize(const float* d_in, int B, int L, float* d_out, void* d_ws, size_t ws_bytes, void* stream) {

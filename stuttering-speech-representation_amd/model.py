@@ -19,7 +19,8 @@ from . import _lib
 from .config import WavLMSpec, WhisperSpec, param_specs
 
 DTYPES = {"fp32": _lib.SSE_DTYPE_F32, "float32": _lib.SSE_DTYPE_F32, "f32": _lib.SSE_DTYPE_F32,
-          "bf16": _lib.SSE_DTYPE_BF16, "bfloat16": _lib.SSE_DTYPE_BF16}
+          "bf16": _lib.SSE_DTYPE_BF16, "bfloat16": _lib.SSE_DTYPE_BF16,
+          "fp8": _lib.SSE_DTYPE_FP8, "mxfp8": _lib.SSE_DTYPE_FP8}
 
 
 def _as_numpy(v) -> np.ndarray:
@@ -60,7 +61,8 @@ def pack_weights(spec, state_dict: dict) -> np.ndarray:
 
 
 class SSEModel:
-    """One model on one GPU.  ``dtype``: "bf16" (throughput path) or "fp32" (parity path)."""
+    """One model on one GPU.  ``dtype``: "bf16" (throughput path), "fp32" (parity path) or "fp8"
+    (Whisper only: bf16 activations, MX-fp8 QKV / fc1 / fc2 GEMMs, BASELINE configs[4])."""
 
     def __init__(self, spec, state_dict: dict, device="cuda:0", dtype: str = "bf16", do_normalize: bool = False):
         if not isinstance(spec, (WavLMSpec, WhisperSpec)):
@@ -292,3 +294,59 @@ def gemm(a: torch.Tensor, b: torch.Tensor, bias=None, resid=None, act: str | Non
                                    z.data_ptr(), ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
                "sse_gemm")
     return cf if cf is not None else ct
+
+
+def mx_scale_bytes(R: int, K: int) -> int:
+    return int(_lib.lib().sse_mx_scale_bytes(R, K))
+
+
+def mx_quantize(x: torch.Tensor, role: int = 0) -> tuple[torch.Tensor, torch.Tensor]:
+    """MX-fp8 quantisation on the GPU: fp32 x [R, K] (K % 128 == 0) -> (e4m3 bytes uint8 [R, K],
+    E8M0 scales uint8 in the GEMM's role-0 (A) / role-1 (B) tile layout)."""
+    x = x.contiguous()
+    R, K = x.shape
+    q = torch.empty((R, K), dtype=torch.uint8, device=x.device)
+    sc = torch.empty(mx_scale_bytes(R, K), dtype=torch.uint8, device=x.device)
+    _lib.check(_lib.lib().sse_mx_quantize(x.data_ptr(), R, K, role, q.data_ptr(), sc.data_ptr(),
+                                          ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)),
+               "sse_mx_quantize")
+    return q, sc
+
+
+def mx_quantize_host(x: np.ndarray, role: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    """The host quantiser libsse.so applies to weights at sse_model_create (no GPU needed)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    R, K = x.shape
+    q = np.empty((R, K), dtype=np.uint8)
+    sc = np.empty(mx_scale_bytes(R, K), dtype=np.uint8)
+    _lib.check(_lib.lib().sse_mx_quantize_host(x.ctypes.data, R, K, role, q.ctypes.data, sc.ctypes.data),
+               "sse_mx_quantize_host")
+    return q, sc
+
+
+def gemm_mx(a_q: torch.Tensor, a_s: torch.Tensor, b_q: torch.Tensor, b_s: torch.Tensor, bias=None, resid=None,
+            act: str | None = None, out: str = "fp32"):
+    """MX-fp8 GEMM: dequant(a) [M, K] @ dequant(b)[N, K]^T (+bias) (gelu) (+resid).  out: "fp32",
+    "bf16" or "fp8" (returns (e4m3 [M, N], scales in the A layout of a GEMM with K = N))."""
+    M, K = a_q.shape
+    N = b_q.shape[0]
+    dev = a_q.device
+    cf = torch.empty((M, N), dtype=torch.float32, device=dev) if out == "fp32" else None
+    ct = None
+    cs = None
+    if out == "bf16":
+        ct = torch.empty((M, N), dtype=torch.bfloat16, device=dev)
+    elif out == "fp8":
+        ct = torch.empty((M, N), dtype=torch.uint8, device=dev)
+        cs = torch.empty(mx_scale_bytes(M, N), dtype=torch.uint8, device=dev)
+    bias_p = bias.contiguous().data_ptr() if bias is not None else None
+    res_p = resid.contiguous().data_ptr() if resid is not None else None
+    _lib.check(_lib.lib().sse_gemm_mx(a_q.data_ptr(), a_s.data_ptr(), b_q.data_ptr(), b_s.data_ptr(), bias_p, res_p,
+                                      cf.data_ptr() if cf is not None else None,
+                                      ct.data_ptr() if ct is not None else None,
+                                      cs.data_ptr() if cs is not None else None, M, N, K,
+                                      {None: 0, "gelu": 1, "gelu_fast": 2}[act],
+                                      ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "sse_gemm_mx")
+    if out == "fp32":
+        return cf
+    return (ct, cs) if out == "fp8" else ct
