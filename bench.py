@@ -42,7 +42,7 @@ from ssr_amd.model import SSEModel  # noqa: E402
 
 # Algorithmic FLOPs per clip: 2 x MACs of every GEMM/conv + QK^T, AV.
 FLOP_PER_CLIP = {"wavlm-base": 42.39e9, "whisper-large-v2": 2272.67e9}
-PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}          # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
+PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3, "fp8": 5000.0}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -52,9 +52,11 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="wavlm-base", choices=["wavlm-base", "whisper-large-v2"])
-    ap.add_argument("--batch", type=int, default=None, help="clips per rank per step (default 256 / 64)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="clips per rank per step (default 256 WavLM / 64 Whisper bf16 / 128 Whisper fp8)")
     ap.add_argument("--seconds", type=float, default=None, help="clip length (default 3 s / 30 s)")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"],
+                    help="fp8: Whisper only, MX-fp8 QKV / fc1 / fc2 GEMMs (BASELINE configs[4])")
     ap.add_argument("--cpu-sample", type=int, default=None, help="clips for the CPU baseline (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-launch event timing")
     return ap.parse_args()
@@ -121,7 +123,8 @@ def roofline(records, dtype):
     total = sum(v[0] for v in by_kernel.values())
     name, (ms, fl, by, n) = max(by_kernel.items(), key=lambda kv: kv[1][0])
     achieved = fl / (ms * 1e-3) / 1e12
-    peak = PEAK_TFLOPS[dtype]
+    # the MX-fp8 GEMM is priced at the dense fp8 peak, every other kernel at the bf16 (fp32) one
+    peak = PEAK_TFLOPS["fp8"] if name == "gemm_mx" else PEAK_TFLOPS["fp32" if dtype == "fp32" else "bf16"]
     breakdown = {k: {"ms": round(v[0], 3), "launches": v[3], "share": round(v[0] / total, 4),
                      "tflops": round(v[1] / max(v[0], 1e-9) / 1e9, 1)} for k, v in sorted(by_kernel.items())}
     by_role = {}
@@ -155,7 +158,9 @@ def main():
 
     wavlm = a.model == "wavlm-base"
     spec = C.WAVLM_BASE if wavlm else C.WHISPER_LARGE_V2
-    B = a.batch or (256 if wavlm else 64)
+    if a.dtype == "fp8" and wavlm:
+        raise SystemExit("--dtype fp8 is the Whisper encoder mode (BASELINE configs[4])")
+    B = a.batch or (256 if wavlm else (128 if a.dtype == "fp8" else 64))
     secs = a.seconds or (3.0 if wavlm else 30.0)
     L = int(16000 * secs)
     sd = synth.synth_state_dict(spec)
