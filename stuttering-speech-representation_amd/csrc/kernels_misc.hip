@@ -735,20 +735,25 @@ __global__ __launch_bounds__(256) void attention_flash2_kernel(AttnArgs a) {
     for (int ks = 0; ks < 2; ++ks) qf[qq][ks] = v ? *(const bf16x8*)(qrow + ks * 32 + g * 8) : bf16x8{};
   }
   f32x4 o[2][4];
-  float m_run[2], l_run[2];
+  float m_run[2];
+  f32x2 l_run[2];
   #pragma unroll
   for (int qq = 0; qq < 2; ++qq) {
     m_run[qq] = -INFINITY;
-    l_run[qq] = 0.f;
+    l_run[qq] = f32x2{0.f, 0.f};
     #pragma unroll
     for (int i = 0; i < 4; ++i) o[qq][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   const float LOG2E = 1.4426950408889634f;
+  const float sl2 = a.scale * LOG2E;
 
   load_tile(0);
   store_tile(0);
   __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
+  // one K/V tile; LAST: the ragged final tile (keys >= T masked), a separate instantiation so the
+  // steady tiles carry no mask selects
+  auto tile_step = [&](int kt, auto last_c) {
+    constexpr bool last = decltype(last_c)::value;
     const int cur = kt & 1;
     if (kt + 1 < nkt) load_tile(kt + 1);           // in flight during this tile's MFMAs
     const char* Ks = smem + cur * F2_BUF;
@@ -766,39 +771,60 @@ __global__ __launch_bounds__(256) void attention_flash2_kernel(AttnArgs a) {
         sc[qq][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf[qq][1], acc, 0, 0, 0);
       }
     }
+    // online softmax in the log2 domain: v = s * scale * log2(e) (+ gate * log2(e) * bias), p = 2^(v - m)
+    // with the raw v_exp_f32; pairs of scores in packed fp32 (v_pk_mul / v_pk_add); the cross-lane
+    // max over the 4 key groups by v_permlane16/32_swap; key masking only in the ragged last tile
     bf16x8 pf[2][2];
     #pragma unroll
     for (int qq = 0; qq < 2; ++qq) {
-      float tmax = -INFINITY;
-      const float gq = BIAS ? gate[wave * F2_QPW + qq * 16 + r16] : 0.f;
+      const float gq2 = BIAS ? gate[wave * F2_QPW + qq * 16 + r16] * LOG2E : 0.f;
+      f32x2 v2[8];
       #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
         #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = kbase + kb * 16 + 4 * g + r;
-          float v = sc[qq][kb][r] * a.scale;
-          if (BIAS) v = fmaf(gq, rb[key - qi[qq] + (Tk - 1)], v);
-          v = key < T ? v : -INFINITY;
-          sc[qq][kb][r] = v;
-          tmax = fmaxf(tmax, v);
+        for (int hh = 0; hh < 2; ++hh) {
+          f32x2 v = f32x2{sc[qq][kb][2 * hh], sc[qq][kb][2 * hh + 1]} * sl2;
+          if (BIAS) {
+            const int key = kbase + kb * 16 + 4 * g + 2 * hh - qi[qq] + (Tk - 1);
+            v = __builtin_elementwise_fma(f32x2{gq2, gq2}, f32x2{rb[key], rb[key + 1]}, v);
+          }
+          if (last) {
+            const int key = kbase + kb * 16 + 4 * g + 2 * hh;
+            v = f32x2{key < T ? v.x : -INFINITY, key + 1 < T ? v.y : -INFINITY};
+          }
+          v2[kb * 2 + hh] = v;
         }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      float tmax = fmaxf(fmaxf(v2[0].x, v2[0].y), v2[1].x);
+      tmax = fmaxf(fmaxf(tmax, v2[1].y), v2[2].x);
+      #pragma unroll
+      for (int e = 2; e < 8; ++e) tmax = e == 2 ? fmaxf(tmax, v2[2].y) : fmaxf(fmaxf(tmax, v2[e].x), v2[e].y);
+      {
+        const auto t16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
+        tmax = fmaxf(__uint_as_float(t16[0]), __uint_as_float(t16[1]));
+        const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
+        tmax = fmaxf(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
+      }
       const float m_new = fmaxf(m_run[qq], tmax);
-      const float alpha = exp2f((m_run[qq] - m_new) * LOG2E);
-      m_run[qq] = m_new;
-      l_run[qq] *= alpha;
-      #pragma unroll
-      for (int i = 0; i < 4; ++i) o[qq][i] *= alpha;
-      const float mb = m_new * LOG2E;
-      #pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
+      // rescale only when some row's max grew (alpha == 1 exactly otherwise: skipping is exact)
+      if (__any(m_new > m_run[qq])) {
+        const float alpha = __builtin_amdgcn_exp2f(m_run[qq] - m_new);
+        l_run[qq] *= f32x2{alpha, alpha};
         #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(fmaf(sc[qq][kb][r], LOG2E, -mb));
-          l_run[qq] += p;
-          pf[qq][kb >> 1][(kb & 1) * 4 + r] = (bf16)p;
+        for (int i = 0; i < 4; ++i) {
+          const f32x2 lo = f32x2{o[qq][i][0], o[qq][i][1]} * alpha, hi = f32x2{o[qq][i][2], o[qq][i][3]} * alpha;
+          o[qq][i] = f32x4{lo.x, lo.y, hi.x, hi.y};
         }
+      }
+      m_run[qq] = m_new;
+      const f32x2 mm = {-m_new, -m_new};
+      #pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const f32x2 d = v2[e] + mm;
+        const f32x2 pv = {__builtin_amdgcn_exp2f(d.x), __builtin_amdgcn_exp2f(d.y)};
+        l_run[qq] += pv;
+        pf[qq][e >> 2][(e & 3) * 2] = (bf16)pv.x;
+        pf[qq][e >> 2][(e & 3) * 2 + 1] = (bf16)pv.y;
+      }
     }
     #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -813,10 +839,13 @@ __global__ __launch_bounds__(256) void attention_flash2_kernel(AttnArgs a) {
       }
     if (kt + 1 < nkt) store_tile(cur ^ 1);         // buffer cur^1 was last read before the previous barrier
     __syncthreads();
-  }
+  };
+  const bool ragged = (T % F2_K) != 0;
+  for (int kt = 0; kt < nkt - (ragged ? 1 : 0); ++kt) tile_step(kt, std::integral_constant<bool, false>{});
+  if (ragged) tile_step(nkt - 1, std::integral_constant<bool, true>{});
   #pragma unroll
   for (int qq = 0; qq < 2; ++qq) {
-    float l = l_run[qq];
+    float l = l_run[qq].x + l_run[qq].y;
     l += __shfl_xor(l, 16, 64);
     l += __shfl_xor(l, 32, 64);
     if (qi[qq] < T) {
