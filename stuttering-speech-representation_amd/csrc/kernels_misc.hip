@@ -664,7 +664,7 @@ constexpr int F2_SVD = 36;                         // V^T row stride, dwords (16
 constexpr int F2_KS = F2_K * 128, F2_VS = AT_HD * F2_SVD * 4, F2_BUF = F2_KS + F2_VS;
 
 template <bool BIAS>
-__global__ __launch_bounds__(256) void attention_flash2_kernel(AttnArgs a) {
+__global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* gate = (float*)(smem + 2 * F2_BUF);       // [F2_Q]
   float* rb = gate + F2_Q;                         // [2*Tk]
