@@ -886,9 +886,18 @@ __global__ __launch_bounds__(640) void attention_full_kernel(AttnArgs a) {
   const int g = lane >> 4, r16 = lane & 15;
   const bf16* qkv = (const bf16*)a.qkv + (long long)b * T * H3;
 
-  // ---- 1. issue all global loads ----
+  // ---- 1. issue all global loads (the wave's Q fragments too: one HBM round trip per block) ----
   bf16x8 kreg[2], vreg[4], greg = bf16x8{};
   float rbv = 0.f, gc = 0.f;
+  const int qb = wave;
+  const int qi = qb * 16 + r16;
+  const bool qv = qi < T;
+  bf16x8 qf[2];
+  {
+    const bf16* qrow = qkv + (long long)(qv ? qi : 0) * H3 + h * AT_HD;
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks) qf[ks] = qv ? *(const bf16x8*)(qrow + ks * 32 + g * 8) : bf16x8{};
+  }
   #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int i = tid + u * NT, kr = i >> 3, ch = i & 7;
@@ -932,16 +941,9 @@ __global__ __launch_bounds__(640) void attention_full_kernel(AttnArgs a) {
   __syncthreads();
 
   const float LOG2E = 1.4426950408889634f;
-  const int qb = wave;
   if (qb * 16 >= T) return;
-  const int qi = qb * 16 + r16;
-  const bool qv = qi < T;
-  const bf16* qrow = qkv + (long long)(qv ? qi : 0) * H3 + h * AT_HD;
   f32x4 s[NKB];
   {
-    bf16x8 qf[2];
-    #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) qf[ks] = qv ? *(const bf16x8*)(qrow + ks * 32 + g * 8) : bf16x8{};
     #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -954,34 +956,51 @@ __global__ __launch_bounds__(640) void attention_full_kernel(AttnArgs a) {
       s[kb] = acc;
     }
   }
-  // exact softmax over the whole (padded) row: lane holds keys kb*16 + 4g + r
-  const float gq = BIAS ? gate[qb * 16 + r16] : 0.f;
-  float mx = -INFINITY;
+  // exact softmax over the whole (padded) row (lane holds keys kb*16 + 4g + r), log2 domain:
+  // v = s * scale * log2(e) (+ gate * log2(e) * bias) in packed fp32, p = 2^(v - max) with the raw
+  // v_exp_f32, cross-lane max / sum over the 4 key groups by v_permlane16/32_swap
+  const float gq2 = BIAS ? gate[qb * 16 + r16] * LOG2E : 0.f;
+  const float sl2 = a.scale * LOG2E;
+  f32x2 v2[NKB * 2];
   #pragma unroll
   for (int kb = 0; kb < NKB; ++kb)
     #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int key = kb * 16 + 4 * g + r;
-      float v = s[kb][r] * a.scale;
-      if (BIAS) v = fmaf(gq, rb[key - qi + (TP - 1)], v);
-      if (kb * 16 + 16 > T) v = key < T ? v : -INFINITY;   // only the last key block is ragged
-      s[kb][r] = v;
-      mx = fmaxf(mx, v);
+    for (int hh = 0; hh < 2; ++hh) {
+      const int key = kb * 16 + 4 * g + 2 * hh;
+      f32x2 v = f32x2{s[kb][2 * hh], s[kb][2 * hh + 1]} * sl2;
+      if (BIAS) {
+        const int d = key - qi + (TP - 1);
+        v = __builtin_elementwise_fma(f32x2{gq2, gq2}, f32x2{rb[d], rb[d + 1]}, v);
+      }
+      if (kb * 16 + 16 > T) v = f32x2{key < T ? v.x : -INFINITY, key + 1 < T ? v.y : -INFINITY};   // ragged block
+      v2[kb * 2 + hh] = v;
     }
-  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-  const float mb = mx * LOG2E;
-  float l = 0.f;
+  float mx = fmaxf(v2[0].x, v2[0].y);
   #pragma unroll
-  for (int kb = 0; kb < NKB; ++kb)
-    #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float p = exp2f(fmaf(s[kb][r], LOG2E, -mb));
-      s[kb][r] = p;
-      l += p;
-    }
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
+  for (int e = 1; e < NKB * 2; ++e) mx = fmaxf(fmaxf(mx, v2[e].x), v2[e].y);
+  {
+    const auto t16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+    mx = fmaxf(__uint_as_float(t16[0]), __uint_as_float(t16[1]));
+    const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+    mx = fmaxf(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
+  }
+  f32x2 l2 = {0.f, 0.f};
+  const f32x2 mm = {-mx, -mx};
+  #pragma unroll
+  for (int e = 0; e < NKB * 2; ++e) {
+    const f32x2 d = v2[e] + mm;
+    const f32x2 p = {__builtin_amdgcn_exp2f(d.x), __builtin_amdgcn_exp2f(d.y)};
+    l2 += p;
+    s[e >> 1][(e & 1) * 2] = p.x;
+    s[e >> 1][(e & 1) * 2 + 1] = p.y;
+  }
+  float l = l2.x + l2.y;
+  {
+    const auto t16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(l), __float_as_uint(l), false, false);
+    l = __uint_as_float(t16[0]) + __uint_as_float(t16[1]);
+    const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(l), __float_as_uint(l), false, false);
+    l = __uint_as_float(t32[0]) + __uint_as_float(t32[1]);
+  }
   // O^T = V^T . P^T
   f32x4 o[4];
   #pragma unroll
