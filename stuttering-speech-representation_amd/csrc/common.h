@@ -184,6 +184,15 @@ __host__ __device__ inline int mx_scale_exp(float amax) {
   E = E < -127 ? -127 : (E > 127 ? 127 : E);
   return E + 127;
 }
+// max over the 8 lanes (lane & ~7) .. (lane | 7): DPP quad_perm xor 1, xor 2, then row_half_mirror
+// (lane i <-> 7 - i within each 8-lane half-row swaps the two quads) -- VALU only, no LDS
+SSE_DEV float max8_dpp(float v) {
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true)));   // [1,0,3,2]
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true)));   // [2,3,0,1]
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, true)));  // half mirror
+  return v;
+}
+
 // 2^-(b - 127) as float (b in [0, 254]); exact (2^127 .. 2^-127, the last a denormal)
 __host__ __device__ inline float mx_inv_scale(int b) {
   union { float f; unsigned u; } v;

@@ -375,8 +375,13 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
   }
 
   if constexpr (TR) {
-    if (g.resid) g8_epilogue_direct<true>(g, acc, m0, n0, wm, wn, q, r16);
-    else g8_epilogue_direct<false>(g, acc, m0, n0, wm, wn, q, r16);
+    if constexpr (MX) {   // no residual on this path (launch_gemm8_mx): fp8 (Q8) or bf16 / fp32 out
+      if (g.c_scale) g8_epilogue_direct<false, true>(g, acc, m0, n0, wm, wn, q, r16);
+      else g8_epilogue_direct<false>(g, acc, m0, n0, wm, wn, q, r16);
+    } else {
+      if (g.resid) g8_epilogue_direct<true>(g, acc, m0, n0, wm, wn, q, r16);
+      else g8_epilogue_direct<false>(g, acc, m0, n0, wm, wn, q, r16);
+    }
     return;
   }
 
@@ -407,7 +412,12 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
       lw = *(const f32x4*)(g.rln_w + n);
       lb = *(const f32x4*)(g.rln_b + n);
     }
-    for (int base = threadIdx.x; base < CH; base += 512 * UNR) {
+    // MX-fp8 out: E8M0 bytes of this thread's 16 rows (w + 8k, k = 0..15: r16 = w + 8(k&1), i = (k>>1)&3,
+    // wm = k>>3) gathered into the 4 scale dwords of the A layout, stored after the half
+    unsigned scw[2][2] = {{0u, 0u}, {0u, 0u}};
+    #pragma unroll
+    for (int it = 0; it < CH / (512 * UNR); ++it) {
+      const int base = threadIdx.x + it * 512 * UNR;
       f32x4 v[UNR], rv[UNR];
       float2 st[UNR];
       long long off[UNR];
@@ -446,21 +456,14 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
         o += r;
         if (MX && g.c_scale) {
           // MX-fp8 out: the wave holds one row's 256 columns, 8 lanes = one 32-column block
-          float a = fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3])));
-          a = fmaxf(a, __shfl_xor(a, 1, 64));
-          a = fmaxf(a, __shfl_xor(a, 2, 64));
-          a = fmaxf(a, __shfl_xor(a, 4, 64));
+          const float a = max8_dpp(fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
           const int e = mx_scale_exp(a);
           const float inv = mx_inv_scale(e);
           int x = __builtin_amdgcn_cvt_pk_fp8_f32(o[0] * inv, o[1] * inv, 0, false);
           x = __builtin_amdgcn_cvt_pk_fp8_f32(o[2] * inv, o[3] * inv, x, true);
-          if (ok[u]) {
-            *(int*)((unsigned char*)g.Ct + off[u]) = x;
-            if ((threadIdx.x & 7) == 0) {
-              const int m = m0 + mi * 128 + ((base + u * 512) >> 6);
-              g.c_scale[mx_a_scale_off(m, n >> 5, g.N >> 7)] = (unsigned char)e;
-            }
-          }
+          if (ok[u]) *(int*)((unsigned char*)g.Ct + off[u]) = x;
+          const int k = it * UNR + u;   // compile-time after unrolling
+          scw[k & 1][(k >> 3) & 1] |= (unsigned)e << (8 * ((k >> 1) & 3));
           continue;
         }
         if (ok[u]) {
@@ -471,6 +474,14 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
           }
         }
       }
+    }
+    if (MX && g.c_scale && (threadIdx.x & 7) == 0) {
+      const int w = threadIdx.x >> 6;
+      #pragma unroll
+      for (int h8 = 0; h8 < 2; ++h8)
+        #pragma unroll
+        for (int wq = 0; wq < 2; ++wq)
+          *(unsigned*)(g.c_scale + mx_a_scale_off(m0 + mi * 128 + wq * 64 + w + 8 * h8, n >> 5, g.N >> 7)) = scw[h8][wq];
     }
   }
 }
@@ -903,8 +914,14 @@ int launch_gemm8_mx(const GemmArgs& a, hipStream_t s) {
   if (a.rows_per_seg != a.M || a.lda != a.K) return -3;
   if (a.c_scale && (a.Cf || !a.Ct)) return -3;
   dim3 grid((unsigned)(((a.M + 255) / 256) * (a.N / 256)));
-  // LDS-staged epilogue for every MX shape: the persistent direct-epilogue kernel exceeds 256
-  // VGPRs with the MX operand tuples and would spill inside the counted-vmcnt main loop
-  hipLaunchKernelGGL((gemm8_kernel<0, false, false, true>), grid, dim3(512), 0, s, a);
+  // Non-persistent for every MX shape: the persistent kernel exceeds 256 VGPRs with the MX operand
+  // tuples and would spill inside the counted-vmcnt main loop.  Without a residual the MFMAs
+  // compute C^T and the epilogue stores from registers (no LDS round trip; SSE_GEMM_MX_STAGED=1
+  // keeps the LDS-staged epilogue for A/B runs); residual GEMMs take the staged epilogue.
+  const char* stg = getenv("SSE_GEMM_MX_STAGED");
+  if (!a.resid && !(stg && stg[0] == '1'))
+    hipLaunchKernelGGL((gemm8_kernel<0, true, false, true>), grid, dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm8_kernel<0, false, false, true>), grid, dim3(512), 0, s, a);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -240,10 +240,7 @@ template <> SSE_DEV f32x4 load4<bf16>(const bf16* p) {
 // whose 7 neighbours (lane ^ 1, 2, 4) hold the rest of the 32-column block: amax, E8M0 exponent
 // (mx_scale_exp), e4m3 = RNE(x * 2^-E), one dword store; lane % 8 == 0 stores the scale byte.
 SSE_DEV void mx_quant4(f32x4 o, unsigned char* dst, unsigned char* scale, long long row, int c, int K, int lane) {
-  float a = fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3])));
-  a = fmaxf(a, __shfl_xor(a, 1, 64));
-  a = fmaxf(a, __shfl_xor(a, 2, 64));
-  a = fmaxf(a, __shfl_xor(a, 4, 64));
+  const float a = max8_dpp(fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
   const int e = mx_scale_exp(a);
   const float inv = mx_inv_scale(e);
   int x = __builtin_amdgcn_cvt_pk_fp8_f32(o[0] * inv, o[1] * inv, 0, false);
@@ -356,10 +353,7 @@ __global__ __launch_bounds__(256) void mx_quantize_kernel(const float* __restric
   if (role == 0) {
     mx_quant4(o, q + row * K + c, scale, row, c, K, lane);
   } else {
-    float a = fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3])));
-    a = fmaxf(a, __shfl_xor(a, 1, 64));
-    a = fmaxf(a, __shfl_xor(a, 2, 64));
-    a = fmaxf(a, __shfl_xor(a, 4, 64));
+    const float a = max8_dpp(fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
     const int e = mx_scale_exp(a);
     const float inv = mx_inv_scale(e);
     int v = __builtin_amdgcn_cvt_pk_fp8_f32(o[0] * inv, o[1] * inv, 0, false);

@@ -1,0 +1,8 @@
+# MX epilogue change: MX + GEMM kernel tests, WavLM bench (staged residual epilogue shared), Whisper fp8 bench.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_gpu_mx.py tests/test_gpu_kernels.py -x -q --timeout 200 --timeout-method thread > gpurun_out/mx2_tests.log 2>&1 || exit 1
+timeout -k 10 200 python -u bench.py --cpu-sample 0 > gpurun_out/bench_wavlm_1.log 2>&1 &&
+timeout -k 10 300 python -u bench.py --model whisper-large-v2 --dtype fp8 --steps 3 --warmup 1 --cpu-sample 0 > gpurun_out/bench_whisper_fp8.log 2>&1
