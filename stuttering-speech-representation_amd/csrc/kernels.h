@@ -23,6 +23,10 @@ int launch_layernorm_mx(const float* in, const float* w, const float* b, int row
                         unsigned char* q, unsigned char* scale, hipStream_t s);
 int launch_mx_quantize(const float* x, int R, int K, int role, unsigned char* q, unsigned char* scale, hipStream_t s);
 
+// kernels_posconv.hip: WavLM positional conv (bf16 path); -3 = shape not covered (use the GEMM)
+int launch_posconv_bf16(const bf16* xt, const bf16* W, const float* bias, float* x, int B, int T, int H, int G, int K,
+                        int pad, hipStream_t s);
+
 int launch_pool_mean(const float* x, int B, int T, int H, float* out, long long out_stride, hipStream_t s,
                      const float2* st = nullptr, const float* w = nullptr, const float* b = nullptr);
 

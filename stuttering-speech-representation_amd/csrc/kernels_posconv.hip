@@ -1,0 +1,164 @@
+// K4: WavLM positional conv embedding (HF/models/wavlm/modeling_wavlm.py:37-90), bf16 path:
+//   x[b][t][g*cg + n] += gelu( bias + sum_{j<K} sum_{c<cg} W[g*cg + n][j*cg + c] * xt[b][t + j - pad][g*cg + c] )
+// (weight-norm folded, SamePad's dropped last frame = only t < T is produced).  As a GEMM per group
+// it is M = B*T rows, N = cg = 48, K = 128 taps x 48 = 6144: N is too narrow for the 256x256
+// kernels and the generic 128x48 tile re-reads the same 255-frame input window from L2 for
+// every 64-deep K step (540 TF/s).  Here a block owns one group of TWO clips:
+//   * the clips' zero-padded input windows (TP + K - 1 frames x cg channels, bf16) are staged in
+//     LDS once; A fragments are read from the window at frame t + j (the conv's sliding window is
+//     just an address offset, no im2col),
+//   * the group's weights stream through a double-buffered LDS stage of 128 K (48 x 256 B rows,
+//     16-B chunks XOR-swizzled by row: conflict-free B fragment reads), register-staged (loads of
+//     stage s+1 issued before stage s's MFMAs, written after them, one barrier per stage),
+//   * each wave computes 4 row blocks (64 frames) x 3 column blocks (48 outputs) as C^T
+//     (v_mfma_f32_16x16x32_bf16 with the weight fragment as the MFMA's A operand), so a lane holds
+//     4 consecutive output channels of one frame: 16-B residual loads and stores, erf-GELU.
+// K order inside an MFMA: k = 32s + 8q + e -> tap k / cg, channel k % cg (cg % 8 == 0, so a lane's
+// 8 elements never straddle taps); A and B use the same map.
+#include "common.h"
+
+namespace {
+
+constexpr int PC_CG = 48;            // channels per group (WavLM: 768 / 16)
+constexpr int PC_KST = 128;          // K per weight stage
+constexpr int PC_STAGE = PC_CG * PC_KST * 2;   // 12 KiB
+
+template <int TP>
+__global__ __launch_bounds__(64 * (2 * TP / 64)) void posconv_kernel(const bf16* __restrict__ xt, const bf16* __restrict__ W,
+                                                                    const float* __restrict__ bias, float* __restrict__ x,
+                                                                    int B, int T, int H, int K, int pad) {
+  constexpr int NW = 2 * TP / 64;                 // waves: 4 row blocks of 16 each
+  constexpr int NT = 64 * NW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int WF = TP + K - 1;                      // window frames per clip
+  char* win = smem;                               // [2][WF][cg] bf16
+  char* wst = smem + ((2 * WF * PC_CG * 2 + 15) & ~15);   // [2][cg][PC_KST] bf16, swizzled
+  const int grp = blockIdx.y, b0 = blockIdx.x * 2;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane >> 4, r16 = lane & 15;
+  const int Ktot = K * PC_CG, nst = Ktot / PC_KST;
+  const bf16* wg = W + (long long)grp * PC_CG * Ktot;
+
+  // ---- weight stage staging: 768 16-B chunks (48 rows x 16) per stage ----
+  constexpr int WCH = PC_CG * (PC_KST / 8);
+  constexpr int WIT = (WCH + NT - 1) / NT;
+  bf16x8 wreg[WIT];
+  auto load_w = [&](int st) {
+    #pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      const int i = tid + it * NT;
+      if (i < WCH) wreg[it] = *(const bf16x8*)(wg + (long long)(i >> 4) * Ktot + st * PC_KST + (i & 15) * 8);
+    }
+  };
+  auto store_w = [&](int buf) {
+    #pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      const int i = tid + it * NT;
+      const int row = i >> 4, ch = i & 15;
+      if (i < WCH) *(bf16x8*)(wst + buf * PC_STAGE + row * (PC_KST * 2) + ((ch ^ (row & 15)) * 16)) = wreg[it];
+    }
+  };
+
+  load_w(0);
+  // ---- input windows: frame f of clip c holds xt[b0 + c][f - pad][grp*cg + 0..47] (zero outside) ----
+  {
+    const int n16 = 2 * WF * (PC_CG / 8);
+    for (int i = tid; i < n16; i += NT) {
+      const int c = i / (WF * 6), r = i - c * WF * 6, f = r / 6, ch = r - f * 6;
+      const int tt = f - pad, b = b0 + c;
+      bf16x8 v = bf16x8{};
+      if (b < B && tt >= 0 && tt < T) v = *(const bf16x8*)(xt + ((long long)b * T + tt) * H + grp * PC_CG + ch * 8);
+      *(bf16x8*)(win + ((c * WF + f) * PC_CG + ch * 8) * 2) = v;
+    }
+  }
+  store_w(0);
+  __syncthreads();
+
+  // ---- per wave: row blocks rb = 4*wave .. 4*wave+3 of the block's 2*TP rows ----
+  f32x4 acc[4][3];
+  #pragma unroll
+  for (int i = 0; i < 4; ++i)
+    #pragma unroll
+    for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int abase[4];   // byte offset of frame t (row r16 of the row block) in its clip's window
+  #pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rb = wave * 4 + i, c = (rb * 16) / TP, t = rb * 16 - c * TP + r16;
+    abase[i] = ((c * WF + t) * PC_CG) * 2;
+  }
+  int tap = (8 * q) / PC_CG, ch = (8 * q) % PC_CG;   // k = 32s + 8q -> (tap, channel)
+  for (int st = 0; st < nst; ++st) {
+    if (st + 1 < nst) load_w(st + 1);
+    const char* wb = wst + (st & 1) * PC_STAGE;
+    #pragma unroll
+    for (int ss = 0; ss < PC_KST / 32; ++ss) {
+      bf16x8 bf[3], af[4];
+      #pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int row = j * 16 + r16, chunk = ss * 4 + q;
+        bf[j] = *(const bf16x8*)(wb + row * (PC_KST * 2) + ((chunk ^ (row & 15)) * 16));
+      }
+      const int aoff = (tap * PC_CG + ch) * 2;
+      #pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8*)(win + abase[i] + aoff);
+      #pragma unroll
+      for (int i = 0; i < 4; ++i)
+        #pragma unroll
+        for (int j = 0; j < 3; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
+      ch += 32;
+      if (ch >= PC_CG) { ch -= PC_CG; ++tap; }
+    }
+    if (st + 1 < nst) store_w((st + 1) & 1);   // its last readers finished before the previous barrier
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane holds C[t][n .. n+3], n = j*16 + 4q; x += gelu(acc + bias) ----
+  #pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rb = wave * 4 + i, c = (rb * 16) / TP, t = rb * 16 - c * TP + r16, b = b0 + c;
+    if (b >= B || t >= T) continue;
+    float* xr = x + ((long long)b * T + t) * H + grp * PC_CG;
+    #pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int n = j * 16 + 4 * q;
+      const f32x4 bv = *(const f32x4*)(bias + grp * PC_CG + n);
+      f32x4 r = *(const f32x4*)(xr + n);
+      f32x4 o = acc[i][j] + bv;
+      #pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] += gelu_erf(o[e]);
+      *(f32x4*)(xr + n) = r;
+    }
+  }
+}
+
+template <int TP>
+int launch_tp(const bf16* xt, const bf16* W, const float* bias, float* x, int B, int T, int H, int G, int K, int pad,
+              hipStream_t s) {
+  const int WF = TP + K - 1;
+  const size_t lds = ((size_t)(2 * WF * PC_CG * 2 + 15) & ~(size_t)15) + 2 * (size_t)PC_STAGE;
+  if (lds > 160 * 1024) return -3;
+  constexpr int NT = 64 * (2 * TP / 64);
+  hipLaunchKernelGGL((posconv_kernel<TP>), dim3((B + 1) / 2, G), dim3(NT), lds, s, xt, W, bias, x, B, T, H, K, pad);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // namespace
+
+// -3: shape outside this kernel (the caller falls back to the grouped GEMM)
+int launch_posconv_bf16(const bf16* xt, const bf16* W, const float* bias, float* x, int B, int T, int H, int G, int K,
+                        int pad, hipStream_t s) {
+  if (H != G * PC_CG || (K * PC_CG) % PC_KST || T <= 0 || pad < 0 || pad >= K) return -3;
+  const int tp = ((T + 31) / 32) * 32;
+  switch (tp) {   // 2*TP rows per block, 4 row blocks per wave
+    case 32: return launch_tp<32>(xt, W, bias, x, B, T, H, G, K, pad, s);
+    case 64: return launch_tp<64>(xt, W, bias, x, B, T, H, G, K, pad, s);
+    case 96: return launch_tp<96>(xt, W, bias, x, B, T, H, G, K, pad, s);
+    case 128: return launch_tp<128>(xt, W, bias, x, B, T, H, G, K, pad, s);
+    case 160: return launch_tp<160>(xt, W, bias, x, B, T, H, G, K, pad, s);
+    case 192: return launch_tp<192>(xt, W, bias, x, B, T, H, G, K, pad, s);
+    case 224: return launch_tp<224>(xt, W, bias, x, B, T, H, G, K, pad, s);
+    case 256: return launch_tp<256>(xt, W, bias, x, B, T, H, G, K, pad, s);
+    default: return -3;
+  }
+}

@@ -674,7 +674,17 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     g.A = xt; g.B = m->ptr(m->pos_w); g.M = M; g.N = cg; g.K = K * cg;
     g.rows_per_seg = Tf; g.T_in = Tf; g.stride = 1; g.pad = K / 2; g.cin = cg; g.ld_in = H;
     g.bias = m->ptr<float>(m->pos_b); g.resid = x; g.Cf = x; g.ldc = H; g.act = ACT_GELU; g.zero = zero;
-    RC(prof(m, s, "gemm_conv:posconv", gflops(g, G), gbytes<T>(g, AMODE_CONV, G), [&] { return launch_gemm<T>(g, AMODE_CONV, G, s); }));
+    // bf16: the dedicated kernel (input window staged once per block, kernels_posconv.hip);
+    // SSE_POSCONV_GEMM=1 keeps the grouped GEMM for A/B runs
+    const char* pge = getenv("SSE_POSCONV_GEMM");
+    const bool use_gemm = sizeof(T) != 2 || (pge && pge[0] == '1');
+    RC(prof(m, s, "gemm_conv:posconv", gflops(g, G), gbytes<T>(g, AMODE_CONV, G), [&] {
+      if (!use_gemm) {
+        const int rc = launch_posconv_bf16((const bf16*)xt, m->ptr<bf16>(m->pos_w), m->ptr<float>(m->pos_b), x, B, Tf, H,
+                                           G, K, K / 2, s);
+        if (rc != -3) return rc;
+      }
+      return launch_gemm<T>(g, AMODE_CONV, G, s); }));
   }
   if (!c.stable_layer_norm)
     RC((launch_layernorm<float, T>(x, m->ptr<float>(m->enc_ln_w), m->ptr<float>(m->enc_ln_b), M, H, eps, ACT_NONE,

@@ -154,3 +154,24 @@ def test_bf16_lnfold_bit_identical(monkeypatch, wavlm_sd):
     assert torch.equal(a, b)
     for x, y in zip(ha, hb):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("n_clips,samples", [(7, 48000), (2, 16000), (3, 80000)])
+def test_bf16_posconv_kernel_matches_grouped_gemm(monkeypatch, wavlm_sd, n_clips, samples):
+    """The dedicated positional-conv kernel (input window staged once per block, kernels_posconv.hip)
+    against the grouped-GEMM path it replaces (SSE_POSCONV_GEMM=1), on hidden_states[0] (the
+    layer right after it) and the pooled layers: same math, fp32 accumulation in another order.
+    Odd clip counts (the second clip of the last block is empty) and T = 49 / 149 / 249 frames."""
+    from ssr_amd import config as C, synth
+    from ssr_amd.model import SSEModel
+    m = SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype="bf16")
+    w = torch.from_numpy(synth.synth_clips(n_clips, samples, seed=5)).cuda()
+    idx = [0, 6, 12]
+    a = m.embed(w, idx).cpu().numpy()
+    h0 = m.hidden_states(w[:1])[0].cpu().numpy()
+    monkeypatch.setenv("SSE_POSCONV_GEMM", "1")
+    b = m.embed(w, idx).cpu().numpy()
+    g0 = m.hidden_states(w[:1])[0].cpu().numpy()
+    assert _rel(h0.reshape(-1), g0.reshape(-1)) <= 1e-5
+    assert _rel(a[:, 0], b[:, 0]).max() <= 1e-5
+    assert _rel(a, b).max() <= 5e-3
