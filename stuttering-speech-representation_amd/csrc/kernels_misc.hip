@@ -654,8 +654,22 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
 // next tile's global loads are issued into registers before the current tile's MFMAs and
 // written to the other LDS buffer after them — one barrier per tile.
 constexpr int F2_QPW = 32, F2_Q = 128, F2_K = 64;
-constexpr int F2_SVD = 36;                         // V^T row stride, dwords (16k+4): conflict-free b64 reads
-constexpr int F2_KS = F2_K * 128, F2_VS = AT_HD * F2_SVD * 4, F2_BUF = F2_KS + F2_VS;
+// V is staged row-major ([key][64 dims], 160-B rows) and read transposed by ds_read_b64_tr_b16:
+// the 8 key rows x 32 B one half-wave touches land on 8 disjoint 8-bank ranges at a 40-dword stride
+constexpr int VR_STRIDE = 160;
+constexpr int F2_KS = F2_K * 128, F2_VS = F2_K * VR_STRIDE, F2_BUF = F2_KS + F2_VS;
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+// A operand of O^T += V^T . P^T for 32 keys from row-major V in LDS: lane (g, r16) gets dim
+// d0 + r16 of keys k0 + 4g + 0..3 (elements 0-3) and k0 + 16 + 4g + 0..3 (elements 4-7) -- the
+// key order of the P^T fragment built from the S^T accumulators.  Per 16-lane group, lane 4q+p
+// addresses row q, columns 4p..4p+3 of a 4 x 16 block (ds_read_b64_tr_b16); EXEC must be full.
+SSE_DEV bf16x8 v_frag_tr(const char* Vs, int k0, int d0, int g, int r16) {
+  const char* p = Vs + (k0 + 4 * g + (r16 >> 2)) * VR_STRIDE + (d0 + 4 * (r16 & 3)) * 2;
+  const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p));
+  const bf16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p + 16 * VR_STRIDE));
+  return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
 
 template <bool BIAS>
 __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
@@ -681,23 +695,17 @@ __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
       rb[u] = rh[d];
     }
   }
-  // staging roles: K rows (2 chunks / thread), V 4-key groups x 8-dim chunks (threads 0..127)
-  const int kr0 = tid >> 3, kch = tid & 7;                     // K chunk tid and tid + 256
-  const int vch = tid >> 4, vkg = tid & 15;                    // V: chunk-major so b64 writes are contiguous
-  bf16x8 kreg[2], vreg[4];
+  // staging roles: K and V rows, 2 chunks of 16 B per thread each (chunk tid and tid + 256)
+  const int kr0 = tid >> 3, kch = tid & 7;
+  bf16x8 kreg[2], vreg[2];
   auto load_tile = [&](int kt) {
     const int kb0 = kt * F2_K;
     #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int key = kb0 + kr0 + 32 * u;
-      kreg[u] = key < T ? *(const bf16x8*)(qkv + (long long)key * LQ + H + h * AT_HD + kch * 8) : bf16x8{};
-    }
-    if (tid < 128) {
-      #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int key = kb0 + vkg * 4 + u;
-        vreg[u] = key < T ? *(const bf16x8*)(qkv + (long long)key * LQ + 2 * H + h * AT_HD + vch * 8) : bf16x8{};
-      }
+      const bf16* row = qkv + (long long)key * LQ + h * AT_HD + kch * 8;
+      kreg[u] = key < T ? *(const bf16x8*)(row + H) : bf16x8{};
+      vreg[u] = key < T ? *(const bf16x8*)(row + 2 * H) : bf16x8{};
     }
   };
   auto store_tile = [&](int buf) {
@@ -707,13 +715,7 @@ __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
     for (int u = 0; u < 2; ++u) {
       const int kr = kr0 + 32 * u;
       *(bf16x8*)(Ks + kr * 128 + ((kch ^ ((kr >> 1) & 7)) * 16)) = kreg[u];
-    }
-    if (tid < 128) {
-      #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const bf16x4 pk = {vreg[0][e], vreg[1][e], vreg[2][e], vreg[3][e]};
-        *(bf16x4*)(Vs + (vch * 8 + e) * F2_SVD * 4 + vkg * 8) = pk;
-      }
+      *(bf16x8*)(Vs + kr * VR_STRIDE + kch * 16) = vreg[u];
     }
   };
 
@@ -824,10 +826,7 @@ __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
     for (int ks = 0; ks < 2; ++ks)
       #pragma unroll
       for (int db = 0; db < 4; ++db) {
-        const char* vrow = Vs + (db * 16 + r16) * F2_SVD * 4 + (ks * 32 + 4 * g) * 2;
-        const bf16x4 v0 = *(const bf16x4*)(vrow);
-        const bf16x4 v1 = *(const bf16x4*)(vrow + 32);
-        const bf16x8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        const bf16x8 vf = v_frag_tr(Vs, ks * 32, db * 16, g, r16);
         #pragma unroll
         for (int qq = 0; qq < 2; ++qq) o[qq][db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qq][ks], o[qq][db], 0, 0, 0);
       }
