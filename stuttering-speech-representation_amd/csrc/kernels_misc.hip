@@ -863,9 +863,8 @@ template <bool BIAS, int NKB>
 __global__ __launch_bounds__(640) void attention_full_kernel(AttnArgs a) {
   constexpr int TP = NKB * 16;                                   // padded keys
   constexpr int NT = 64 * NKB;                                   // threads (one wave per query block)
-  constexpr int SVD = ((TP / 2 + 15) / 16) * 16 + 4;             // V^T row stride in dwords (16k+4)
   constexpr int KS_BYTES = TP * 128;
-  constexpr int VS_BYTES = AT_HD * SVD * 4;
+  constexpr int VS_BYTES = TP * VR_STRIDE;                        // V row-major, read transposed
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ks = smem;
   char* Vs = smem + KS_BYTES;
@@ -880,7 +879,7 @@ __global__ __launch_bounds__(640) void attention_full_kernel(AttnArgs a) {
   const bf16* qkv = (const bf16*)a.qkv + (long long)b * T * H3;
 
   // ---- 1. issue all global loads (the wave's Q fragments too: one HBM round trip per block) ----
-  bf16x8 kreg[2], vreg[4], greg = bf16x8{};
+  bf16x8 kreg[2], vreg[2], greg = bf16x8{};
   float rbv = 0.f, gc = 0.f;
   const int qb = wave;
   const int qi = qb * 16 + r16;
@@ -894,16 +893,9 @@ __global__ __launch_bounds__(640) void attention_full_kernel(AttnArgs a) {
   #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int i = tid + u * NT, kr = i >> 3, ch = i & 7;
-    kreg[u] = kr < T ? *(const bf16x8*)(qkv + (long long)kr * H3 + H + h * AT_HD + ch * 8) : bf16x8{};
-  }
-  constexpr int VU = (TP / 4) * 8;                               // (8-dim chunk, 4-key group) units
-  const bool vth = tid < VU;
-  const int vch = tid / (TP / 4), vkg = tid - vch * (TP / 4);   // key group fastest: conflict-free
-  #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int key = vkg * 4 + u;
-    vreg[u] = (vth && key < T) ? *(const bf16x8*)(qkv + (long long)key * H3 + 2 * H + h * AT_HD + vch * 8)
-                               : bf16x8{};
+    const bf16* row = qkv + (long long)kr * H3 + h * AT_HD + ch * 8;
+    kreg[u] = kr < T ? *(const bf16x8*)(row + H) : bf16x8{};
+    vreg[u] = kr < T ? *(const bf16x8*)(row + 2 * H) : bf16x8{};
   }
   if (BIAS) {
     if (tid < T) greg = *(const bf16x8*)(qkv + (long long)tid * H3 + 3 * H + 8 * h);
@@ -914,18 +906,12 @@ __global__ __launch_bounds__(640) void attention_full_kernel(AttnArgs a) {
       rbv = a.relb[(long long)h * (2 * a.maxd + 1) + a.maxd + d];
     }
   }
-  // ---- 2. write LDS: K swizzled rows, V transposed (4 keys per 8-B write), gate, bias ----
+  // ---- 2. write LDS: K swizzled rows, V plain rows (read transposed), gate, bias ----
   #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int i = tid + u * NT, kr = i >> 3, ch = i & 7;
     *(bf16x8*)(Ks + kr * 128 + ((ch ^ ((kr >> 1) & 7)) * 16)) = kreg[u];
-  }
-  if (vth) {
-    #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const bf16x4 pk = {vreg[0][e], vreg[1][e], vreg[2][e], vreg[3][e]};
-      *(bf16x4*)(Vs + (vch * 8 + e) * SVD * 4 + vkg * 8) = pk;
-    }
+    *(bf16x8*)(Vs + kr * VR_STRIDE + ch * 16) = vreg[u];
   }
   if (BIAS) {
     if (tid < TP) gate[tid] = tid < T ? wavlm_gate_v(greg, gc) : 0.f;
@@ -1007,13 +993,7 @@ __global__ __launch_bounds__(640) void attention_full_kernel(AttnArgs a) {
       pf[4 + r] = (bf16)s[2 * ks + 1][r];
     }
     #pragma unroll
-    for (int db = 0; db < 4; ++db) {
-      const char* vrow = Vs + (db * 16 + r16) * SVD * 4 + (ks * 32 + 4 * g) * 2;
-      const bf16x4 v0 = *(const bf16x4*)(vrow);
-      const bf16x4 v1 = *(const bf16x4*)(vrow + 32);
-      const bf16x8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-      o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[db], 0, 0, 0);
-    }
+    for (int db = 0; db < 4; ++db) o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v_frag_tr(Vs, ks * 32, db * 16, g, r16), pf, o[db], 0, 0, 0);
   }
   if (qv) {
     const float inv = 1.0f / l;
@@ -1030,8 +1010,7 @@ __global__ __launch_bounds__(640) void attention_full_kernel(AttnArgs a) {
 template <bool BIAS, int NKB>
 int launch_attention_full(const AttnArgs& a, int B, hipStream_t s) {
   constexpr int TP = NKB * 16;
-  constexpr int SVD = ((TP / 2 + 15) / 16) * 16 + 4;
-  const size_t lds = (size_t)TP * 128 + (size_t)AT_HD * SVD * 4 + (size_t)TP * 4 + (size_t)2 * TP * 4;
+  const size_t lds = (size_t)TP * 128 + (size_t)TP * VR_STRIDE + (size_t)TP * 4 + (size_t)2 * TP * 4;
   hipLaunchKernelGGL((attention_full_kernel<BIAS, NKB>), dim3(a.nh, B), dim3(64 * NKB), lds, s, a);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
