@@ -860,7 +860,7 @@ __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
 // the threads, the gate's 8 projections, one relative-bias entry) and only then writes LDS, so
 // a block pays one HBM round trip before its MFMA work instead of one per loop trip.
 template <bool BIAS, int NKB>
-__global__ __launch_bounds__(640) void attention_full_kernel(AttnArgs a) {
+__global__ __launch_bounds__(640) void attention_full_kernel(AttnArgs a, int hpb) {
   constexpr int TP = NKB * 16;                                   // padded keys
   constexpr int NT = 64 * NKB;                                   // threads (one wave per query block)
   constexpr int KS_BYTES = TP * 128;
@@ -871,56 +871,62 @@ __global__ __launch_bounds__(640) void attention_full_kernel(AttnArgs a) {
   float* gate = (float*)(Vs + VS_BYTES);                          // [TP]
   float* rb = gate + TP;                                          // [2*TP]
 
-  const int h = blockIdx.x, b = blockIdx.y;
+  // block = (clip, hpb consecutive heads): the next head's K/V/Q/gate/bias loads are issued into
+  // registers before this head's MFMAs and written to LDS after them (one LDS image, two
+  // barriers per head), so a block pays one exposed HBM round trip, not one per head
+  const int h0 = blockIdx.x * hpb, b = blockIdx.y;
   const int T = a.T, H = a.H, H3 = a.ldq;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
   const bf16* qkv = (const bf16*)a.qkv + (long long)b * T * H3;
-
-  // ---- 1. issue all global loads (the wave's Q fragments too: one HBM round trip per block) ----
-  bf16x8 kreg[2], vreg[2], greg = bf16x8{};
-  float rbv = 0.f, gc = 0.f;
   const int qb = wave;
   const int qi = qb * 16 + r16;
   const bool qv = qi < T;
-  bf16x8 qf[2];
-  {
+  const float LOG2E = 1.4426950408889634f;
+
+  bf16x8 kreg[2], vreg[2], greg = bf16x8{}, qreg[2];
+  float rbv = 0.f, gc = 0.f;
+  auto prefetch = [&](int h) {
     const bf16* qrow = qkv + (long long)(qv ? qi : 0) * H3 + h * AT_HD;
     #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) qf[ks] = qv ? *(const bf16x8*)(qrow + ks * 32 + g * 8) : bf16x8{};
-  }
-  #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int i = tid + u * NT, kr = i >> 3, ch = i & 7;
-    const bf16* row = qkv + (long long)kr * H3 + h * AT_HD + ch * 8;
-    kreg[u] = kr < T ? *(const bf16x8*)(row + H) : bf16x8{};
-    vreg[u] = kr < T ? *(const bf16x8*)(row + 2 * H) : bf16x8{};
-  }
-  if (BIAS) {
-    if (tid < T) greg = *(const bf16x8*)(qkv + (long long)tid * H3 + 3 * H + 8 * h);
-    gc = a.gconst[h];
-    if (tid < 2 * TP - 1) {
-      int d = tid - (TP - 1);
-      d = d < -a.maxd ? -a.maxd : (d > a.maxd ? a.maxd : d);
-      rbv = a.relb[(long long)h * (2 * a.maxd + 1) + a.maxd + d];
+    for (int ks = 0; ks < 2; ++ks) qreg[ks] = qv ? *(const bf16x8*)(qrow + ks * 32 + g * 8) : bf16x8{};
+    #pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = tid + u * NT, kr = i >> 3, ch = i & 7;
+      const bf16* row = qkv + (long long)kr * H3 + h * AT_HD + ch * 8;
+      kreg[u] = kr < T ? *(const bf16x8*)(row + H) : bf16x8{};
+      vreg[u] = kr < T ? *(const bf16x8*)(row + 2 * H) : bf16x8{};
     }
-  }
-  // ---- 2. write LDS: K swizzled rows, V plain rows (read transposed), gate, bias ----
-  #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int i = tid + u * NT, kr = i >> 3, ch = i & 7;
-    *(bf16x8*)(Ks + kr * 128 + ((ch ^ ((kr >> 1) & 7)) * 16)) = kreg[u];
-    *(bf16x8*)(Vs + kr * VR_STRIDE + ch * 16) = vreg[u];
-  }
-  if (BIAS) {
-    if (tid < TP) gate[tid] = tid < T ? wavlm_gate_v(greg, gc) : 0.f;
-    if (tid < 2 * TP - 1) rb[tid] = rbv;
-  }
-  __syncthreads();
-
-  const float LOG2E = 1.4426950408889634f;
-  if (qb * 16 >= T) return;
+    if (BIAS) {
+      if (tid < T) greg = *(const bf16x8*)(qkv + (long long)tid * H3 + 3 * H + 8 * h);
+      gc = a.gconst[h];
+      if (tid < 2 * TP - 1) {
+        int d = tid - (TP - 1);
+        d = d < -a.maxd ? -a.maxd : (d > a.maxd ? a.maxd : d);
+        rbv = a.relb[(long long)h * (2 * a.maxd + 1) + a.maxd + d];
+      }
+    }
+  };
+  prefetch(h0);
+  for (int hh = 0; hh < hpb; ++hh) {
+    const int h = h0 + hh;
+    if (hh) __syncthreads();   // every wave is done reading the previous head's LDS image
+    // write LDS: K swizzled rows, V plain rows (read transposed), gate, bias
+    #pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = tid + u * NT, kr = i >> 3, ch = i & 7;
+      *(bf16x8*)(Ks + kr * 128 + ((ch ^ ((kr >> 1) & 7)) * 16)) = kreg[u];
+      *(bf16x8*)(Vs + kr * VR_STRIDE + ch * 16) = vreg[u];
+    }
+    if (BIAS) {
+      if (tid < TP) gate[tid] = tid < T ? wavlm_gate_v(greg, gc) : 0.f;
+      if (tid < 2 * TP - 1) rb[tid] = rbv;
+    }
+    const bf16x8 qf[2] = {qreg[0], qreg[1]};
+    __syncthreads();
+    if (hh + 1 < hpb) prefetch(h + 1);   // in flight during this head's MFMAs
+    if (qb * 16 < T) {
   f32x4 s[NKB];
   {
     #pragma unroll
@@ -1005,13 +1011,16 @@ __global__ __launch_bounds__(640) void attention_full_kernel(AttnArgs a) {
       *(bf16x4*)(orow + db * 16 + 4 * g) = ov;
     }
   }
+    }
+  }
 }
 
 template <bool BIAS, int NKB>
 int launch_attention_full(const AttnArgs& a, int B, hipStream_t s) {
   constexpr int TP = NKB * 16;
   const size_t lds = (size_t)TP * 128 + (size_t)TP * VR_STRIDE + (size_t)TP * 4 + (size_t)2 * TP * 4;
-  hipLaunchKernelGGL((attention_full_kernel<BIAS, NKB>), dim3(a.nh, B), dim3(64 * NKB), lds, s, a);
+  const int hpb = a.nh % 4 == 0 ? 4 : (a.nh % 3 == 0 ? 3 : (a.nh % 2 == 0 ? 2 : 1));   // heads per block
+  hipLaunchKernelGGL((attention_full_kernel<BIAS, NKB>), dim3(a.nh / hpb, B), dim3(64 * NKB), lds, s, a, hpb);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
