@@ -166,7 +166,9 @@ class WavLMOracle:
             x = layer_norm(x, p["encoder.layer_norm.weight"], p["encoder.layer_norm.bias"], eps)
         T = x.shape[0]
         bk = rel_position_buckets(T, T, s.num_buckets, s.max_distance)
-        bias = p["encoder.layers.0.attention.rel_attn_embed.weight"][bk].transpose(2, 0, 1)  # [nh, T, T]
+        # [nh, T, T], made contiguous: added to every layer's scores (a strided view makes numpy's
+        # broadcast add ~5x slower, which only mattered for the timed CPU baseline)
+        bias = np.ascontiguousarray(p["encoder.layers.0.attention.rel_attn_embed.weight"][bk].transpose(2, 0, 1))
         hs = []
         for l in range(s.layers):
             hs.append(x)
