@@ -327,11 +327,79 @@ template int launch_layernorm<float, bf16>(const float*, const float*, const flo
 template int launch_layernorm<bf16, bf16>(const bf16*, const float*, const float*, int, int, float, int, float*,
                                           bf16*, hipStream_t, float2*);
 
+// LayerNorm -> MX-fp8 GEMM operand (pre-LN Whisper, SSE_DTYPE_FP8).  Block = 64 consecutive rows
+// (4 waves x 16 rows, one row per wave at a time, the layernorm_kernel arithmetic), so the block
+// owns whole A-layout scale dwords (rows r16 + 16i, i = 0..3, of its 64-row group): the E8M0 bytes
+// go to LDS and leave as one dword store per (r16, block) instead of one byte store per
+// (row, block).  Data: e4m3 dwords (4 columns per lane).
+constexpr int LNMX_MAXB = 2048 / 32;
+__global__ __launch_bounds__(256) void layernorm_mx_kernel(const float* __restrict__ in, const float* __restrict__ w,
+                                                           const float* __restrict__ bta, int rows, int H, float eps,
+                                                           unsigned char* __restrict__ q, unsigned char* __restrict__ scale) {
+  __shared__ unsigned char sc[64 * LNMX_MAXB];
+  const int r0 = blockIdx.x * 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n4 = H >> 2, nb = H >> 5;
+  for (int rr = wave; rr < 64; rr += 4) {
+    const int row = r0 + rr;
+    if (row >= rows) break;
+    const float* x = in + (long long)row * H;
+    f32x4 v[8];
+    float s = 0.f;
+    #pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int g = lane + 64 * i;
+      if (g < n4) {
+        v[i] = *(const f32x4*)(x + 4 * g);
+        s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+      }
+    }
+    const float mean = wave_sum(s) / H;
+    float qs = 0.f;
+    #pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (lane + 64 * i < n4)
+        #pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = v[i][e] - mean;
+          qs = fmaf(d, d, qs);
+        }
+    const float rstd = 1.0f / sqrtf(wave_sum(qs) / H + eps);
+    #pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int g = lane + 64 * i;
+      if (g < n4) {
+        const int c = 4 * g;
+        const f32x4 wv = *(const f32x4*)(w + c), bv = *(const f32x4*)(bta + c);
+        f32x4 o;
+        #pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = fmaf((v[i][e] - mean) * rstd, wv[e], bv[e]);   // = ln_apply4
+        const float a = max8_dpp(fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
+        const int e8 = mx_scale_exp(a);
+        const float inv = mx_inv_scale(e8);
+        int xq = __builtin_amdgcn_cvt_pk_fp8_f32(o[0] * inv, o[1] * inv, 0, false);
+        xq = __builtin_amdgcn_cvt_pk_fp8_f32(o[2] * inv, o[3] * inv, xq, true);
+        *(int*)(q + (long long)row * H + c) = xq;
+        if ((lane & 7) == 0) sc[rr * LNMX_MAXB + (c >> 5)] = (unsigned char)e8;
+      }
+    }
+  }
+  __syncthreads();
+  // scale dwords of this 64-row group: (r16, block) -> bytes i = 0..3 of rows r16 + 16i
+  for (int u = threadIdx.x; u < 16 * nb; u += 256) {
+    const int r16 = u & 15, blk = u >> 4;
+    if (r0 + r16 >= rows) continue;
+    const unsigned v = (unsigned)sc[r16 * LNMX_MAXB + blk] | ((unsigned)sc[(r16 + 16) * LNMX_MAXB + blk] << 8) |
+                       ((unsigned)sc[(r16 + 32) * LNMX_MAXB + blk] << 16) |
+                       ((unsigned)sc[(r16 + 48) * LNMX_MAXB + blk] << 24);
+    *(unsigned*)(scale + mx_a_scale_off(r0 + r16, blk, H >> 7)) = v;
+  }
+}
+
 int launch_layernorm_mx(const float* in, const float* w, const float* b, int rows, int H, float eps,
                         unsigned char* q, unsigned char* scale, hipStream_t s) {
   if (H % 128 || H > 2048) return -3;
-  hipLaunchKernelGGL((layernorm_kernel<float, unsigned char>), dim3((rows + 3) / 4), dim3(256), 0, s, in, w, b, rows,
-                     H, eps, (int)ACT_NONE, (float*)nullptr, q, (float2*)scale);
+  hipLaunchKernelGGL(layernorm_mx_kernel, dim3((rows + 63) / 64), dim3(256), 0, s, in, w, b, rows, H, eps, q, scale);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
