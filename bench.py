@@ -59,6 +59,8 @@ def parse():
                     help="fp8: Whisper only, MX-fp8 QKV / fc1 / fc2 GEMMs (BASELINE configs[4])")
     ap.add_argument("--cpu-sample", type=int, default=None, help="clips for the CPU baseline (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-launch event timing")
+    ap.add_argument("--stream", action="store_true",
+                    help="clips streamed from pinned host memory each step (double-buffered H2D on a side stream)")
     ap.add_argument("--corpus", type=int, default=0,
                     help="BASELINE configs[3] mode: embed a corpus of this many clips (e.g. 50000) sharded "
                          "across the ranks with corpus.extract_corpus (tail batch + one all-gather timed)")
@@ -225,8 +227,36 @@ def main():
     if a.corpus:
         return corpus_run(a, model, spec, idx, clips, B, L, world, rank, dev, dist)
 
+    # --stream (configs[4] "streaming extraction"): each step's clips come from pinned host memory,
+    # copied on a side stream into the other of two device buffers while this step computes
+    # (double-buffered H2D; the next batch's copy waits only for the step that last read its buffer)
+    if a.stream:
+        host = [torch.from_numpy(synth.synth_clips(B, L, seed=1234 + k, first_clip=rank * B)).pin_memory()
+                for k in range(2)]
+        dbuf = [clips, torch.empty_like(clips)]
+        cs = torch.cuda.Stream(device=dev)
+        ready = [torch.cuda.Event(), torch.cuda.Event()]
+        done = [torch.cuda.Event(), torch.cuda.Event()]
+        for e in done:
+            e.record()
+        with torch.cuda.stream(cs):
+            dbuf[0].copy_(host[0], non_blocking=True)
+            ready[0].record(cs)
+        it = [0]
+
     def step():
-        model.embed(clips, idx, out=out)
+        if a.stream:
+            cur, nxt = it[0] % 2, (it[0] + 1) % 2
+            it[0] += 1
+            cs.wait_event(done[nxt])
+            with torch.cuda.stream(cs):
+                dbuf[nxt].copy_(host[nxt], non_blocking=True)
+                ready[nxt].record(cs)
+            torch.cuda.current_stream(dev).wait_event(ready[cur])
+            model.embed(dbuf[cur], idx, out=out)
+            done[cur].record()
+        else:
+            model.embed(clips, idx, out=out)
         if dist is not None:
             dist.all_gather_into_tensor(gathered, out)
 
@@ -273,7 +303,8 @@ def main():
             "value": round(value, 2), "unit": "clips/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(1e3 * t_max / a.steps, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": a.dtype,
-            "data": "synthetic 16 kHz clips (splitmix64 Gaussian+tones), random-init weights of the real architecture",
+            "data": "synthetic 16 kHz clips (splitmix64 Gaussian+tones), random-init weights of the real architecture"
+                    + ("; clips streamed from pinned host memory every step (double-buffered H2D)" if a.stream else ""),
             "config": {"workload": f"{spec.name} {a.dtype} embeddings, {B} x {secs:g} s clips per GPU per step"
                                    + (", RCCL all-gather of [B,4,H] per step" if world > 1 else ""),
                        "model": spec.name, "global_batch": world * B, "clip_samples": L,
