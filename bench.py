@@ -41,7 +41,7 @@ from ssr_amd import config as C, synth  # noqa: E402
 from ssr_amd.model import SSEModel  # noqa: E402
 
 # Algorithmic FLOPs per clip: 2 x MACs of every GEMM/conv + QK^T, AV.
-FLOP_PER_CLIP = {"wavlm-base": 42.39e9, "whisper-large-v2": 2272.67e9}
+FLOP_PER_CLIP = {"wavlm-base": 42.39e9, "wavlm-large": 109.6e9, "whisper-large-v2": 2272.67e9}
 PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3, "fp8": 5000.0}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
 
@@ -51,7 +51,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--model", default="wavlm-base", choices=["wavlm-base", "whisper-large-v2"])
+    ap.add_argument("--model", default="wavlm-base", choices=["wavlm-base", "wavlm-large", "whisper-large-v2"],
+                    help="wavlm-large: the reference's default --model_name (REF/WavLM_embeddings.py:34)")
     ap.add_argument("--batch", type=int, default=None,
                     help="clips per rank per step (default 256 WavLM / 64 Whisper bf16 / 128 Whisper fp8)")
     ap.add_argument("--seconds", type=float, default=None, help="clip length (default 3 s / 30 s)")
@@ -71,9 +72,9 @@ def cpu_baseline(model_name: str, n: int, seconds: float):
     """The oracle (numpy restatement of the reference path, batch-1 loop like the reference)
     timed on this host's cores.  Test infrastructure used only as the reported baseline."""
     from threadpoolctl import threadpool_info
-    if model_name == "wavlm-base":
+    if model_name.startswith("wavlm"):
         from oracle.wavlm import WavLMOracle
-        spec = C.WAVLM_BASE
+        spec = C.WAVLM_BASE if model_name == "wavlm-base" else C.WAVLM_LARGE
         o = WavLMOracle(spec, synth.synth_wavlm_state_dict(spec, seed=7))
         clips = synth.synth_clips(n + 1, int(16000 * seconds), seed=2024)
         o.embed(clips[:1], spec.default_layer_indices())            # warm-up (BLAS threads, page-in)
@@ -209,8 +210,8 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    wavlm = a.model == "wavlm-base"
-    spec = C.WAVLM_BASE if wavlm else C.WHISPER_LARGE_V2
+    wavlm = a.model.startswith("wavlm")
+    spec = {"wavlm-base": C.WAVLM_BASE, "wavlm-large": C.WAVLM_LARGE, "whisper-large-v2": C.WHISPER_LARGE_V2}[a.model]
     if a.dtype == "fp8" and wavlm:
         raise SystemExit("--dtype fp8 is the Whisper encoder mode (BASELINE configs[4])")
     B = a.batch or (256 if wavlm else (128 if a.dtype == "fp8" else 64))

@@ -193,6 +193,19 @@ SSE_DEV float max8_dpp(float v) {
   return v;
 }
 
+// sum over the 64 lanes of a wave without LDS: DPP xor 1, xor 2, half-row mirror (8 lanes), row
+// mirror (16 lanes), then v_permlane16_swap (32) and v_permlane32_swap (64); every lane gets the total
+SSE_DEV float wave_sum_fast(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, true));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, true));
+  const auto t16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(t16[0]) + __uint_as_float(t16[1]);
+  const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(t32[0]) + __uint_as_float(t32[1]);
+}
+
 // 2^-(b - 127) as float (b in [0, 254]); exact (2^127 .. 2^-127, the last a denormal)
 __host__ __device__ inline float mx_inv_scale(int b) {
   union { float f; unsigned u; } v;

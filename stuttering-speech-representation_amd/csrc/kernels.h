@@ -11,6 +11,10 @@ int launch_conv0_gn(const float* x, int B, int L, const float* norm, const float
                     float2* ss, TO* out, hipStream_t s);
 
 template <typename TO>
+int launch_conv0_ln(const float* x, int B, int L, const float* norm, const float* w0, const float* b0, int C, int k0,
+                    int s0, int T0, const float* lnw, const float* lnb, float eps, TO* out, hipStream_t s);
+
+template <typename TO>
 int launch_conv0_raw(const float* x, int B, int L, const float* norm, const float* w0, const float* b0, int C,
                      int k0, int s0, int T0, TO* out, hipStream_t s);
 

@@ -121,12 +121,17 @@ __global__ void gn_finalize_kernel(const double* __restrict__ mom, int B, int C,
   ss[i] = make_float2(sc, beta[c] - (float)mean * sc);
 }
 
-template <typename TO, bool RAW, bool FAST>
+// LNG (WavLM-large "layer" frontend, C == 512): the frame's 512 channels are exactly the wave's 64
+// lanes x 8, so LayerNorm over channels (layernorm_kernel's expression, statistics from the fp32
+// conv values) and GELU are applied before the single store -- no second pass over the
+// [B][T0][512] activation.
+template <typename TO, bool RAW, bool FAST, bool LNG = false>
 __global__ __launch_bounds__(256) void conv0_apply_kernel(const float* __restrict__ x, int L,
                                                           const float* __restrict__ norm,
                                                           const float* __restrict__ w0, const float* __restrict__ b0,
                                                           int C, int T0, const float2* __restrict__ ss,
-                                                          TO* __restrict__ out) {
+                                                          TO* __restrict__ out, const float* __restrict__ lnw = nullptr,
+                                                          const float* __restrict__ lnb = nullptr, float eps = 0.f) {
   constexpr int S0 = 5;
   __shared__ float xs[(C0_T - 1) * S0 + K0 + 2];
   const int chunk = blockIdx.x, b = blockIdx.y;
@@ -142,7 +147,7 @@ __global__ __launch_bounds__(256) void conv0_apply_kernel(const float* __restric
   // one 16-B store per frame); the block's 4 waves split the chunk's frames.  C % 8 == 0.
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (int c = lane * 8; c < C; c += 512) {
-    f32x2 w[4][K0], bias[4], sc[4], sh[4];
+    f32x2 w[4][K0], bias[4], sc[4], sh[4], gw[4], gb[4];
     #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int c0 = c + 2 * p;
@@ -156,8 +161,74 @@ __global__ __launch_bounds__(256) void conv0_apply_kernel(const float* __restric
         sc[p] = f32x2{s0v.x, s1v.x};
         sh[p] = f32x2{s0v.y, s1v.y};
       }
+      if (LNG) {
+        gw[p] = f32x2{lnw[c0], lnw[c0 + 1]};
+        gb[p] = f32x2{lnb[c0], lnb[c0 + 1]};
+      }
     }
     TO* ob = out + ((long long)b * T0 + t0) * C + c;
+    if constexpr (LNG) {
+      // two frames (t, t + 4) per trip: their reduction chains (DPP / permlane, each step dependent
+      // on the previous) interleave instead of stalling one after the other
+      for (int t = wv; t < nt; t += 8) {
+        const bool two = t + 4 < nt;
+        f32x2 y[2][4];
+        #pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          const int tf = two ? t + 4 * f : t;
+          #pragma unroll
+          for (int p = 0; p < 4; ++p) y[f][p] = bias[p];
+          #pragma unroll
+          for (int j = 0; j < K0; ++j) {
+            const float xv = xs[tf * S0 + j];
+            #pragma unroll
+            for (int p = 0; p < 4; ++p) y[f][p] = __builtin_elementwise_fma(w[p][j], f32x2{xv, xv}, y[f][p]);
+          }
+        }
+        float sm[2], qs[2], mean[2], rstd[2];
+        #pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          sm[f] = 0.f;
+          #pragma unroll
+          for (int p = 0; p < 4; ++p) sm[f] += y[f][p].x + y[f][p].y;
+        }
+        #pragma unroll
+        for (int f = 0; f < 2; ++f) mean[f] = wave_sum_fast(sm[f]) / C;
+        #pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          qs[f] = 0.f;
+          #pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            const float d0 = y[f][p].x - mean[f], d1 = y[f][p].y - mean[f];
+            qs[f] = fmaf(d0, d0, qs[f]);
+            qs[f] = fmaf(d1, d1, qs[f]);
+          }
+        }
+        #pragma unroll
+        for (int f = 0; f < 2; ++f) rstd[f] = 1.0f / sqrtf(wave_sum_fast(qs[f]) / C + eps);
+        #pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          if (f == 1 && !two) break;
+          f32x2 o[4];
+          #pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            const f32x2 z = {fmaf((y[f][p].x - mean[f]) * rstd[f], gw[p].x, gb[p].x),
+                             fmaf((y[f][p].y - mean[f]) * rstd[f], gw[p].y, gb[p].y)};
+            o[p] = FAST ? gelu_sig2(z) : gelu_erf2(z);
+          }
+          const long long row = (long long)(t + 4 * f) * C;
+          if constexpr (sizeof(TO) == 2) {
+            const bf16x8 o8 = {(bf16)o[0].x, (bf16)o[0].y, (bf16)o[1].x, (bf16)o[1].y,
+                               (bf16)o[2].x, (bf16)o[2].y, (bf16)o[3].x, (bf16)o[3].y};
+            *(bf16x8*)(ob + row) = o8;
+          } else {
+            *(f32x4*)((float*)ob + row) = f32x4{o[0].x, o[0].y, o[1].x, o[1].y};
+            *(f32x4*)((float*)ob + row + 4) = f32x4{o[2].x, o[2].y, o[3].x, o[3].y};
+          }
+        }
+      }
+      continue;
+    }
     for (int t = wv; t < nt; t += 4) {
       f32x2 y[4] = {bias[0], bias[1], bias[2], bias[3]};
       #pragma unroll
@@ -215,6 +286,25 @@ int launch_conv0_raw(const float* x, int B, int L, const float* norm, const floa
                      (const float2*)nullptr, out);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+// conv0 + LayerNorm(C) + GELU in one pass ("layer" frontend, C == 512); -3: not covered (the caller
+// runs launch_conv0_raw + launch_layernorm)
+template <typename TO>
+int launch_conv0_ln(const float* x, int B, int L, const float* norm, const float* w0, const float* b0, int C, int k0,
+                    int s0, int T0, const float* lnw, const float* lnb, float eps, TO* out, hipStream_t s) {
+  if (k0 != K0 || s0 != 5 || C != 512) return -3;
+  dim3 grid((T0 + C0_T - 1) / C0_T, B), block(256);
+  if (sizeof(TO) == 2 && !gelu_exact_env())   // bf16 output: gelu_sig2 (common.h)
+    hipLaunchKernelGGL((conv0_apply_kernel<TO, true, true, true>), grid, block, 0, s, x, L, norm, w0, b0, C, T0,
+                       (const float2*)nullptr, out, lnw, lnb, eps);
+  else
+    hipLaunchKernelGGL((conv0_apply_kernel<TO, true, false, true>), grid, block, 0, s, x, L, norm, w0, b0, C, T0,
+                       (const float2*)nullptr, out, lnw, lnb, eps);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+template int launch_conv0_ln<float>(const float*, int, int, const float*, const float*, const float*, int, int, int,
+                                    int, const float*, const float*, float, float*, hipStream_t);
+template int launch_conv0_ln<bf16>(const float*, int, int, const float*, const float*, const float*, int, int, int,
+                                   int, const float*, const float*, float, bf16*, hipStream_t);
 template int launch_conv0_raw<float>(const float*, int, int, const float*, const float*, const float*, int, int, int,
                                      int, float*, hipStream_t);
 template int launch_conv0_raw<bf16>(const float*, int, int, const float*, const float*, const float*, int, int, int,

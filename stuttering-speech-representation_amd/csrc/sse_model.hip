@@ -628,11 +628,18 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
   const float* b0 = m->conv_b[0] ? m->ptr<float>(m->conv_b[0]) : nullptr;
   if (c.feat_norm_layer) {
     // "layer" frontend (WavLM-large, HF modeling_wavlm.py:696-720): conv -> LN over channels -> GELU
+    // conv0 + LN + GELU fused (one pass over the largest activation); other widths: two passes
+    int frc = -3;
     RC(prof(m, s, "conv0_ln", 2.0 * B * (double)Ts[0] * C0 * c.conv_kernel[0], 0, [&] {
+      frc = launch_conv0_ln<T>(wave, B, L, norm, m->ptr<float>(m->conv_w[0]), b0, C0, c.conv_kernel[0],
+                               c.conv_stride[0], Ts[0], m->ptr<float>(m->conv_ln_w[0]), m->ptr<float>(m->conv_ln_b[0]),
+                               1e-5f, bufs[0], s);
+      if (frc != -3) return frc;
       return launch_conv0_raw<T>(wave, B, L, norm, m->ptr<float>(m->conv_w[0]), b0, C0, c.conv_kernel[0],
                                  c.conv_stride[0], Ts[0], bufs[0], s); }));
-    RC((launch_layernorm<T, T>(bufs[0], m->ptr<float>(m->conv_ln_w[0]), m->ptr<float>(m->conv_ln_b[0]), B * Ts[0], C0,
-                               1e-5f, ACT_GELU, nullptr, bufs[0], s)));
+    if (frc == -3)
+      RC((launch_layernorm<T, T>(bufs[0], m->ptr<float>(m->conv_ln_w[0]), m->ptr<float>(m->conv_ln_b[0]), B * Ts[0], C0,
+                                 1e-5f, ACT_GELU, nullptr, bufs[0], s)));
   } else {
     RC(prof(m, s, "conv0_gn", 2.0 * B * (double)Ts[0] * C0 * c.conv_kernel[0], 0, [&] {
       return launch_conv0_gn<T>(wave, B, L, norm, m->ptr<float>(m->conv_w[0]), b0, C0, c.conv_kernel[0],
