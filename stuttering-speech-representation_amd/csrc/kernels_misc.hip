@@ -402,10 +402,93 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TI* __restrict__ i
   }
 }
 
+// bf16 -> bf16 LayerNorm of narrow rows (H <= 512: the WavLM conv frontend's per-layer LN + GELU
+// and the feature projection's LN): one 16-B load per lane per row, R rows per wave with every load
+// issued first (the one-row-per-wave kernel keeps only 1 KiB in flight per wave: ~2.4 TB/s on these
+// rows), DPP/permlane reductions for the R rows interleaved.  GELU: the bf16 path's gelu_sig2.
+template <int R>
+__global__ __launch_bounds__(256) void layernorm_bf16_rows_kernel(const bf16* __restrict__ in, const float* __restrict__ w,
+                                                                  const float* __restrict__ bta, int rows, int H,
+                                                                  float eps, int act, bf16* __restrict__ out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long long r0 = ((long long)blockIdx.x * 4 + wave) * R;
+  const int nch = H >> 3;
+  const bool on = lane < nch;
+  bf16x8 v[R];
+  #pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const long long row = r0 + i;
+    v[i] = (on && row < rows) ? *(const bf16x8*)(in + row * H + lane * 8) : bf16x8{};
+  }
+  f32x4 w0 = {1.f, 1.f, 1.f, 1.f}, w1 = w0, b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0;
+  if (on) {
+    w0 = *(const f32x4*)(w + lane * 8);
+    w1 = *(const f32x4*)(w + lane * 8 + 4);
+    b0 = *(const f32x4*)(bta + lane * 8);
+    b1 = *(const f32x4*)(bta + lane * 8 + 4);
+  }
+  float x[R][8], mean[R], rstd[R];
+  #pragma unroll
+  for (int i = 0; i < R; ++i) {
+    float sm = 0.f;
+    #pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      x[i][e] = (float)v[i][e];
+      sm += x[i][e];
+    }
+    mean[i] = sm;
+  }
+  #pragma unroll
+  for (int i = 0; i < R; ++i) mean[i] = wave_sum_fast(mean[i]) / H;
+  #pragma unroll
+  for (int i = 0; i < R; ++i) {
+    float q = 0.f;
+    #pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = on ? x[i][e] - mean[i] : 0.f;
+      q = fmaf(d, d, q);
+    }
+    rstd[i] = q;
+  }
+  #pragma unroll
+  for (int i = 0; i < R; ++i) rstd[i] = 1.0f / sqrtf(wave_sum_fast(rstd[i]) / H + eps);
+  #pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const long long row = r0 + i;
+    float y[8];
+    #pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float wv = e < 4 ? w0[e] : w1[e - 4], bv = e < 4 ? b0[e] : b1[e - 4];
+      y[e] = fmaf((x[i][e] - mean[i]) * rstd[i], wv, bv);   // = ln_apply4
+    }
+    if (act != ACT_NONE) {
+      #pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        const f32x2 g2 = act == ACT_GELU ? gelu_erf2(f32x2{y[e], y[e + 1]}) : gelu_sig2(f32x2{y[e], y[e + 1]});
+        y[e] = g2.x;
+        y[e + 1] = g2.y;
+      }
+    }
+    if (on && row < rows) {
+      const bf16x8 o8 = {(bf16)y[0], (bf16)y[1], (bf16)y[2], (bf16)y[3], (bf16)y[4], (bf16)y[5], (bf16)y[6], (bf16)y[7]};
+      *(bf16x8*)(out + row * H + lane * 8) = o8;
+    }
+  }
+}
+
 template <typename TI, typename TO>
 int launch_layernorm(const TI* in, const float* w, const float* b, int rows, int H, float eps, int act,
                      float* out_f, TO* out_t, hipStream_t s, float2* stats) {
   if (H % 4 || H > 2048) return -3;
+  if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2) {
+    if (H % 8 == 0 && H <= 512 && !out_f && !stats && out_t) {
+      constexpr int R = 4;
+      const int a2 = act == ACT_GELU && !gelu_exact_env() ? (int)ACT_GELU_FAST : act;   // bf16 output
+      hipLaunchKernelGGL((layernorm_bf16_rows_kernel<R>), dim3((rows + 4 * R - 1) / (4 * R)), dim3(256), 0, s,
+                         (const bf16*)in, w, b, rows, H, eps, a2, (bf16*)out_t);
+      return hipGetLastError() == hipSuccess ? 0 : -2;
+    }
+  }
   hipLaunchKernelGGL((layernorm_kernel<TI, TO>), dim3((rows + 3) / 4), dim3(256), 0, s, in, w, b, rows, H, eps,
                      act, out_f, out_t, stats);
   return hipGetLastError() == hipSuccess ? 0 : -2;
