@@ -149,6 +149,16 @@ int sse_resample(const float* d_in, int B, int L, int orig_freq, int new_freq, f
 int sse_augment(const float* d_in, float* d_out, int B, int L, const int32_t* d_kind, const float* d_factor,
                 const int64_t* d_stream, uint64_t seed, void* stream);
 
+/* Pitch branch of augment_audio (REF/model_training_01.py:172-177): torchaudio.transforms.
+ * PitchShift(sample_rate, n_steps) with its defaults (bins_per_octave 12, n_fft 512, hop 128,
+ * periodic Hann) = STFT -> phase vocoder (rate 2^(-n_steps/12)) -> iSTFT (length round(L/rate))
+ * -> resample int(sample_rate/rate) -> sample_rate -> truncate / zero-pad to L.  d_in, d_out
+ * [B][L] (all clips share n_steps); L must exceed 256 (torch.stft's reflect padding, the
+ * reference raises and keeps the original clip).  No clamp: sse_augment kind 3 follows. */
+size_t sse_pitch_shift_workspace_bytes(int B, int L, int sample_rate, int n_steps);
+int sse_pitch_shift(const float* d_in, int B, int L, int sample_rate, int n_steps, float* d_out, void* d_ws,
+                    size_t ws_bytes, void* stream);
+
 /* Wav2Vec2FeatureExtractor zero_mean_unit_var_norm on device (feature_extraction_wav2vec2.py:94):
  * d_out[b] = (d_in[b] - mean_b) / sqrt(var_b + 1e-7).  Workspace: 8 * B bytes. */
 int sse_normalize(const float* d_in, int B, int L, float* d_out, void* d_ws, size_t ws_bytes, void* stream);

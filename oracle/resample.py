@@ -19,16 +19,20 @@ import math
 import numpy as np
 
 
-def resample_kernel(orig_freq: int, new_freq: int, lowpass_filter_width: int = 6, rolloff: float = 0.99):
-    """-> (kernel float32 [new, 2*width + orig], width, orig, new) after dividing by the gcd."""
+def resample_kernel(orig_freq: int, new_freq: int, lowpass_filter_width: int = 6, rolloff: float = 0.99,
+                    rows=None):
+    """-> (kernel float32 [new, 2*width + orig], width, orig, new) after dividing by the gcd.
+    ``rows = (p0, p1)`` builds only phases p0..p1-1 (large co-prime rate pairs, e.g. pitch shift's
+    int(16000/rate) -> 16000, have a 16000 x 17000 filter bank)."""
     g = math.gcd(int(orig_freq), int(new_freq))
     orig, new = int(orig_freq) // g, int(new_freq) // g
     base = min(orig, new) * rolloff
     width = math.ceil(lowpass_filter_width * orig / base)
+    p0, p1 = (0, new) if rows is None else rows
     idx = np.arange(-width, width + orig, dtype=np.float64)[None, :] / orig
     # torch.arange(0, -new, -1) is int64; "/ new" promotes to the default float32, then "+ idx"
     # (float64) promotes to float64
-    t = (np.arange(0, -new, -1, dtype=np.int64)[:, None] / np.float32(new)).astype(np.float32).astype(np.float64)
+    t = (np.arange(-p0, -p1, -1, dtype=np.int64)[:, None] / np.float32(new)).astype(np.float32).astype(np.float64)
     t = t + idx
     t = t * base
     t = np.clip(t, -lowpass_filter_width, lowpass_filter_width)
@@ -41,20 +45,32 @@ def resample_kernel(orig_freq: int, new_freq: int, lowpass_filter_width: int = 6
     return k.astype(np.float32), width, orig, new
 
 
+def _plan(orig_freq: int, new_freq: int, lowpass_filter_width: int = 6, rolloff: float = 0.99):
+    g = math.gcd(int(orig_freq), int(new_freq))
+    orig, new = int(orig_freq) // g, int(new_freq) // g
+    return math.ceil(lowpass_filter_width * orig / (min(orig, new) * rolloff)), orig, new
+
+
 def resample(wave: np.ndarray, orig_freq: int, new_freq: int) -> np.ndarray:
     """[..., L] float32 -> [..., ceil(new*L/orig)] float32 (torchaudio Resample default)."""
     if orig_freq == new_freq:
         return np.asarray(wave, dtype=np.float32).copy()
-    k, width, orig, new = resample_kernel(orig_freq, new_freq)
+    width, orig, new = _plan(orig_freq, new_freq)
     x = np.asarray(wave, dtype=np.float32)
     shape = x.shape
     x = x.reshape(-1, shape[-1])
     n, L = x.shape
     xp = np.pad(x, ((0, 0), (width, width + orig)))
-    K = k.shape[1]
+    K = 2 * width + orig
     n_blk = (xp.shape[1] - K) // orig + 1
     frames = np.lib.stride_tricks.as_strided(xp, shape=(n, n_blk, K), strides=(xp.strides[0], orig * 4, 4))
-    out = np.einsum("bik,pk->bip", frames.astype(np.float64), k.astype(np.float64)).reshape(n, -1)
+    frames = frames.astype(np.float64)
+    out = np.empty((n, n_blk, new), dtype=np.float64)
+    step = max(1, (1 << 22) // K)
+    for p0 in range(0, new, step):
+        k = resample_kernel(orig_freq, new_freq, rows=(p0, min(new, p0 + step)))[0]
+        out[:, :, p0:p0 + k.shape[0]] = frames @ k.astype(np.float64).T
+    out = out.reshape(n, -1)
     target = int(math.ceil(new * L / orig))
     return out[:, :target].astype(np.float32).reshape(shape[:-1] + (target,))
 

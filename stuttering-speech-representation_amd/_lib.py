@@ -28,7 +28,7 @@ EXPORTED = ("sse_weight_floats", "sse_model_create", "sse_model_destroy", "sse_o
             "sse_profile_start", "sse_profile_read", "sse_profile_stop", "sse_gemm", "sse_whisper_embed",
             "sse_whisper_decoder_hidden_states", "sse_mono", "sse_resample_length", "sse_resample_workspace_bytes",
             "sse_resample", "sse_augment", "sse_mx_scale_bytes", "sse_mx_scale_offset", "sse_mx_quantize",
-            "sse_mx_quantize_host", "sse_gemm_mx")
+            "sse_mx_quantize_host", "sse_gemm_mx", "sse_pitch_shift_workspace_bytes", "sse_pitch_shift")
 
 
 class SSEError(RuntimeError):
@@ -138,6 +138,10 @@ def lib() -> ctypes.CDLL:
     L.sse_resample.restype = i32
     L.sse_augment.argtypes = [vp, vp, i32, i32, vp, vp, vp, ctypes.c_uint64, vp]
     L.sse_augment.restype = i32
+    L.sse_pitch_shift_workspace_bytes.argtypes = [i32, i32, i32, i32]
+    L.sse_pitch_shift_workspace_bytes.restype = sz
+    L.sse_pitch_shift.argtypes = [vp, i32, i32, i32, i32, vp, vp, sz, vp]
+    L.sse_pitch_shift.restype = i32
     L.sse_mx_scale_bytes.argtypes = [i32, i32]
     L.sse_mx_scale_bytes.restype = sz
     L.sse_mx_scale_offset.argtypes = [i32, i32, i32, i32]

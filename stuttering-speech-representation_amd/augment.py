@@ -15,9 +15,10 @@ Drop-in for the reference's ``augment_audio`` / ``apply_data_augmentation``
   and ``apply_data_augmentation(..., cache=dict)`` computes every requested layer once and
   reuses it across the reference's per-layer loop (REF/model_training_1.py:920-940 recomputes
   all augmentations for every layer).
-* Pitch shift (model_training_01 only: torchaudio PitchShift = phase vocoder + resample) is not
-  built; like any failure inside the reference's augment_audio it logs a warning and returns the
-  original audio.
+* Pitch shift (model_training_01 only, REF/model_training_01.py:172-177): torchaudio
+  PitchShift's STFT -> phase vocoder -> iSTFT -> resample on the GPU (``sse_pitch_shift``,
+  kernels_pitch.hip), then the clamp.  Clips of 256 samples or fewer make torch.stft's reflect
+  padding raise in the reference; here too, and augment_audio returns the original clip.
 """
 from __future__ import annotations
 
@@ -83,6 +84,24 @@ def _pointwise(x: torch.Tensor, kinds, factors, streams, seed: int) -> torch.Ten
     return y
 
 
+def pitch_shift(x: torch.Tensor, sample_rate: int, n_steps: int) -> torch.Tensor:
+    """torchaudio.transforms.PitchShift(sample_rate, n_steps)(x) on the GPU: [L] or [B, L] fp32
+    cuda -> the same shape (no clamp).  Raises SSEError for L <= 256 (torch.stft's reflect pad)."""
+    if x.device.type != "cuda":
+        raise ValueError("pitch_shift runs on a GPU device (no CPU fallback)")
+    squeeze = x.dim() == 1
+    x = (x[None] if squeeze else x).to(torch.float32).contiguous()
+    B, L = x.shape
+    lib = _lib.lib()
+    n = lib.sse_pitch_shift_workspace_bytes(B, L, int(sample_rate), int(n_steps))
+    ws = torch.empty(max(n, 256), dtype=torch.uint8, device=x.device)
+    y = torch.empty_like(x)
+    _lib.check(lib.sse_pitch_shift(x.data_ptr(), B, L, int(sample_rate), int(n_steps), y.data_ptr(), ws.data_ptr(),
+                                   ws.numel(), ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)),
+               "sse_pitch_shift")
+    return y[0] if squeeze else y
+
+
 def augment_batch(waves, specs, seed: int = 0, streams=None, sample_rate: int = 16000) -> list:
     """Apply ``specs[i]`` to ``waves[i]`` (1-D float32 cuda tensors, any lengths) on the GPU.
     Returns a list of 1-D tensors (speed changes the length by at most a sample or two)."""
@@ -91,13 +110,13 @@ def augment_batch(waves, specs, seed: int = 0, streams=None, sample_rate: int = 
     out = [None] * n
     groups = {}
     for i, (w, sp) in enumerate(zip(waves, specs)):
-        if sp.kind == "pitch":
-            if sp.n_steps == 0:            # REF: `if n_steps != 0` -> unchanged, then clamp
-                sp = AugSpec("none")
-            else:
-                raise NotImplementedError("pitch shift (torchaudio PitchShift phase vocoder) is not built")
+        if sp.kind == "pitch" and sp.n_steps == 0:   # REF: `if n_steps != 0` -> unchanged, then clamp
+            sp = AugSpec("none")
         if sp.kind == "speed":
             w = resample(resample(w, sample_rate, sp.new_sr), sp.new_sr, sample_rate)
+            kind, fac = "clamp", 1.0
+        elif sp.kind == "pitch":
+            w = pitch_shift(w, sample_rate, sp.n_steps)
             kind, fac = "clamp", 1.0
         else:
             kind, fac = sp.kind, sp.factor

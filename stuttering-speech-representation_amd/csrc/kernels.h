@@ -62,3 +62,8 @@ int launch_resample(const float* x, int B, int L, int orig_freq, int new_freq, f
 int launch_mono(const float* x, int B, int C, int L, float* y, hipStream_t s);
 int launch_augment(const float* x, float* y, int B, int L, const int* kind, const float* factor,
                    const long long* stream, uint64_t seed, hipStream_t s);
+
+// kernels_pitch.hip (model_training_01's pitch branch)
+size_t pitch_shift_workspace_bytes(int B, int L, int sr, int n_steps);
+int launch_pitch_shift(const float* x, int B, int L, int sr, int n_steps, float* y, void* ws, size_t ws_bytes,
+                       hipStream_t s);

@@ -1224,6 +1224,18 @@ int sse_augment(const float* d_in, float* d_out, int B, int L, const int32_t* d_
   return rc == -1 ? SSE_ERR_INVALID : (rc ? SSE_ERR_HIP : SSE_OK);
 }
 
+size_t sse_pitch_shift_workspace_bytes(int B, int L, int sample_rate, int n_steps) {
+  if (B <= 0 || L <= 256 || sample_rate <= 0 || n_steps < -48 || n_steps > 48) return 0;
+  return pitch_shift_workspace_bytes(B, L, sample_rate, n_steps);
+}
+
+int sse_pitch_shift(const float* d_in, int B, int L, int sample_rate, int n_steps, float* d_out, void* d_ws,
+                    size_t ws_bytes, void* stream) {
+  if (!d_in || !d_out || !d_ws) return SSE_ERR_INVALID;
+  const int rc = launch_pitch_shift(d_in, B, L, sample_rate, n_steps, d_out, d_ws, ws_bytes, (hipStream_t)stream);
+  return rc == -4 ? SSE_ERR_WORKSPACE : (rc == -1 ? SSE_ERR_INVALID : (rc ? SSE_ERR_HIP : SSE_OK));
+}
+
 int sse_mono(const float* d_in, int B, int C, int L, float* d_out, void* stream) {
   if (!d_in || !d_out) return SSE_ERR_INVALID;
   const int rc = launch_mono(d_in, B, C, L, d_out, (hipStream_t)stream);

@@ -185,3 +185,50 @@ def test_augment_oracle_ops():
     assert abs(n.std() - 0.004) < 1e-4 and abs(n.mean()) < 5e-5
     s = augment(synth.synth_clips(1, 48000, seed=2)[0], "speed", new_sr=int(16000 * 0.97))
     assert s.shape == (48000,)
+
+
+def test_pitch_oracle_round_trip_and_tone():
+    """oracle/pitch.py (torchaudio PitchShift restated, parity unpinned): n_steps = 0 is an
+    STFT -> iSTFT round trip (Hann^2 envelope at hop n_fft/4 is exact), a tone moves to
+    f * 2^(n/12), the length is kept, and the clamp of augment() follows."""
+    from oracle.augment import augment
+    from oracle.pitch import pitch_shift
+    sr = 4000                                   # small co-prime resampling banks: seconds of CPU
+    t = np.arange(8000) / sr
+    x = (0.3 * np.sin(2 * np.pi * 200 * t)).astype(np.float32)
+    assert np.abs(pitch_shift(x, sr, 0) - x).max() < 1e-6
+    for n in (-2, -1, 1, 2):
+        y = pitch_shift(x, sr, n)
+        assert y.shape == x.shape
+        seg = y[1000:7000]
+        spec = np.abs(np.fft.rfft(seg * np.hanning(seg.size), n=8 * seg.size))
+        f = np.argmax(spec) * sr / (8 * seg.size)
+        assert abs(f / (200 * 2 ** (n / 12)) - 1) < 2e-3, (n, f)
+    loud = x * 8
+    assert np.abs(augment(loud, "pitch", sample_rate=sr, n_steps=1)).max() <= 1.0
+    assert np.array_equal(augment(loud, "pitch", sample_rate=sr, n_steps=0), np.clip(loud, -1, 1))
+
+
+def test_pitch_tables_follow_aten_cpu_kernels():
+    from oracle.pitch import arange_ts, hann512, linspace_pa
+    pa = linspace_pa()
+    assert pa.dtype == np.float32 and pa.shape == (257,) and pa[0] == 0 and pa[-1] == np.float32(np.pi * 128)
+    assert np.abs(pa - np.pi / 2 * np.arange(257)).max() < 1e-4
+    rate = 2.0 ** (1 / 6)
+    ts = arange_ts(37, rate)
+    assert ts.shape == (37,) and np.abs(ts - rate * np.arange(37)).max() < 1e-5
+    assert ts[-1] == np.float32(rate * 36)      # the tail (37 = 2*16 + 5) uses the scalar formula
+    w = hann512()
+    assert w[0] == 0 and w[256] == 1 and np.allclose(w, 0.5 - 0.5 * np.cos(2 * np.pi * np.arange(512) / 512), atol=1e-7)
+
+
+def test_pitch_short_clip_and_abi_sizes():
+    from oracle.pitch import pitch_shift
+    from ssr_amd import _lib
+    with pytest.raises(ValueError):
+        pitch_shift(np.zeros(256, np.float32), 16000, 1)
+    L = _lib.lib()
+    assert L.sse_pitch_shift_workspace_bytes(1, 256, 16000, 1) == 0      # reflect pad needs L > 256
+    assert L.sse_pitch_shift_workspace_bytes(1, 16000, 16000, 99) == 0
+    # 16 kHz, +2 semitones: the 17959 -> 16000 polyphase bank (16000 x 17973 fp32) dominates
+    assert L.sse_pitch_shift_workspace_bytes(1, 16000, 16000, 2) > 16000 * 17973 * 4
