@@ -256,7 +256,123 @@ __global__ __launch_bounds__(256) void conv0_apply_kernel(const float* __restric
   }
 }
 
-size_t conv0_moments_bytes(int B) { return (size_t)B * NMOM * sizeof(double); }
+// ---- bf16 GroupNorm path on the matrix cores ----
+// conv0 as MFMAs: out[t][c] = w_c . x_t with K = 10 taps.  v_mfma_f32_16x16x32_bf16 has K = 32, which
+// holds the three terms of a split-bf16 product, x = xh + xl, w = wh + wl (hi = RNE bf16, lo = bf16
+// of the exact remainder): sum_j xh wh + xl wh + xh wl (the dropped xl wl is ~2^-16 relative), so
+// one MFMA evaluates a 16-channel x 16-frame block of the fp32 convolution to ~1e-5 -- far below
+// the bf16 output rounding -- and the VALU is left with the GroupNorm affine, GELU and the packing.
+// K slots per lane group q (A = weights of channel r16, B = taps of frame r16):
+//   q0: xh0-7 | wh0-7   q1: xh8,9 xl0-5 | wh8,9 wh0-5   q2: xl6-9 xh0-3 | wh6-9 wl0-3   q3: xh4-9 0 0 | wl4-9 0 0
+// MFMAs compute C^T (channels x frames), so a lane holds 4 consecutive channels of one frame; two
+// channel blocks per step and a v_permlane16_swap give every lane 8 consecutive bf16 = one 16-B store.
+constexpr int C0M_T = 32;                // frames per block (2 blocks of 16)
+
+SSE_DEV void c0m_split(float v, bf16& h, bf16& l) {
+  h = (bf16)v;
+  l = (bf16)(v - (float)h);
+}
+
+// wf[cb][lane]: A fragment of channel block cb (16 channels) for lane (q, r16)
+__global__ void conv0_wfrag_kernel(const float* __restrict__ w0, int C, bf16x8* __restrict__ wf) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= (C / 16) * 64) return;
+  const int cb = i >> 6, lane = i & 63, q = lane >> 4, c = cb * 16 + (lane & 15);
+  bf16 h[K0], l[K0];
+  #pragma unroll
+  for (int j = 0; j < K0; ++j) c0m_split(w0[c * K0 + j], h[j], l[j]);
+  const bf16 z = (bf16)0.f;
+  bf16x8 f;
+  if (q == 0) f = bf16x8{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]};
+  else if (q == 1) f = bf16x8{h[8], h[9], h[0], h[1], h[2], h[3], h[4], h[5]};
+  else if (q == 2) f = bf16x8{h[6], h[7], h[8], h[9], l[0], l[1], l[2], l[3]};
+  else f = bf16x8{l[4], l[5], l[6], l[7], l[8], l[9], z, z};
+  wf[i] = f;
+}
+
+// A block owns one clip and walks its 32-frame chunks (blockIdx.x, + gridDim.x, ...): the clip's
+// weights and GroupNorm affine stay in registers, the next chunk's waveform is fetched while this
+// chunk computes, and the LDS tile turns the MFMA layout (4 channels x 16 frames per lane group)
+// into whole 1 KiB row stores that drain while the next chunk computes (one short-lived block per
+// chunk, or lane-scattered 64-B row pieces, both left the kernel at half the fill bandwidth).
+// Wave w computes channel blocks cb = w, w+4, ..., both 16-frame blocks of the chunk.
+constexpr int C0M_PAD = 16;              // bf16 per tile row of padding: row stride = 8 banks mod 64
+
+__global__ __launch_bounds__(256) void conv0_mfma_kernel(const float* __restrict__ x, int L,
+                                                         const float* __restrict__ norm,
+                                                         const bf16x8* __restrict__ wf, const float* __restrict__ b0,
+                                                         int T0, const float2* __restrict__ ss,
+                                                         bf16* __restrict__ out) {
+  constexpr int S0 = 5, C = 512, NCB = C / 16 / 4;
+  __shared__ float xs[(C0M_T - 1) * S0 + K0 + 2];
+  __shared__ __attribute__((aligned(16))) bf16 tile[C0M_T][C + C0M_PAD];
+  const int b = blockIdx.y, tid = threadIdx.x;
+  const int nchunk = (T0 + C0M_T - 1) / C0M_T;
+  const float* xb = x + (long long)b * L;
+  float mu = 0.f, rs = 1.f;
+  if (norm) { mu = norm[2 * b]; rs = norm[2 * b + 1]; }
+  const int lane = tid & 63, wv = tid >> 6, q = lane >> 4, r16 = lane & 15;
+  bf16x8 wfr[NCB];
+  f32x2 sc0[NCB], sh0[NCB], sc1[NCB], sh1[NCB];
+  {
+    const float2* ssb = ss + (long long)b * C;
+    #pragma unroll
+    for (int i = 0; i < NCB; ++i) {
+      const int cb = wv + 4 * i, c = cb * 16 + 4 * q;
+      wfr[i] = wf[cb * 64 + lane];
+      const f32x4 s01 = *(const f32x4*)(ssb + c), s23 = *(const f32x4*)(ssb + c + 2);
+      sc0[i] = f32x2{s01[0], s01[2]}; sh0[i] = f32x2{s01[1], s01[3]};
+      sc1[i] = f32x2{s23[0], s23[2]}; sh1[i] = f32x2{s23[1], s23[3]};
+      if (b0) {
+        const f32x4 bb = *(const f32x4*)(b0 + c);
+        sh0[i] = __builtin_elementwise_fma(f32x2{bb[0], bb[1]}, sc0[i], sh0[i]);
+        sh1[i] = __builtin_elementwise_fma(f32x2{bb[2], bb[3]}, sc1[i], sh1[i]);
+      }
+    }
+  }
+  auto fetch = [&](int ch) {
+    const int t0 = ch * C0M_T, nt = min(C0M_T, T0 - t0), nx = (nt - 1) * S0 + K0;
+    return tid < nx ? xb[(long long)t0 * S0 + tid] : 0.f;
+  };
+  float xv = blockIdx.x < nchunk ? fetch(blockIdx.x) : 0.f;
+  for (int ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
+    const int t0 = ch * C0M_T, nt = min(C0M_T, T0 - t0);
+    __syncthreads();                                // previous chunk: xs read, tile rows stored
+    if (tid < (C0M_T - 1) * S0 + K0) xs[tid] = norm ? (xv - mu) * rs : xv;
+    __syncthreads();
+    bf16x8 xf[C0M_T / 16];
+    #pragma unroll
+    for (int fb = 0; fb < C0M_T / 16; ++fb) {
+      const int tl = fb * 16 + r16;
+      bf16 h[K0], l[K0];
+      #pragma unroll
+      for (int j = 0; j < K0; ++j) c0m_split(tl < nt ? xs[tl * S0 + j] : 0.f, h[j], l[j]);
+      const bf16 z = (bf16)0.f;
+      if (q == 0) xf[fb] = bf16x8{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]};
+      else if (q == 1) xf[fb] = bf16x8{h[8], h[9], l[0], l[1], l[2], l[3], l[4], l[5]};
+      else if (q == 2) xf[fb] = bf16x8{l[6], l[7], l[8], l[9], h[0], h[1], h[2], h[3]};
+      else xf[fb] = bf16x8{h[4], h[5], h[6], h[7], h[8], h[9], z, z};
+    }
+    if (ch + (int)gridDim.x < nchunk) xv = fetch(ch + gridDim.x);
+    #pragma unroll
+    for (int i = 0; i < NCB; ++i) {
+      const int c = (wv + 4 * i) * 16 + 4 * q;
+      #pragma unroll
+      for (int fb = 0; fb < C0M_T / 16; ++fb) {
+        const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[i], xf[fb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        const f32x2 o0 = gelu_sig2(__builtin_elementwise_fma(f32x2{acc[0], acc[1]}, sc0[i], sh0[i]));
+        const f32x2 o1 = gelu_sig2(__builtin_elementwise_fma(f32x2{acc[2], acc[3]}, sc1[i], sh1[i]));
+        *(bf16x4*)&tile[fb * 16 + r16][c] = bf16x4{(bf16)o0.x, (bf16)o0.y, (bf16)o1.x, (bf16)o1.y};
+      }
+    }
+    __syncthreads();
+    bf16* ob = out + ((long long)b * T0 + t0) * C;
+    for (int r = wv; r < nt; r += 4) *(uint4*)(ob + (long long)r * C + lane * 8) = *(const uint4*)&tile[r][lane * 8];
+  }
+}
+
+size_t conv0_moments_bytes(int B) { return ((size_t)B * NMOM * sizeof(double) + 255) / 256 * 256 + 512 / 16 * 1024; }
+
 
 template <typename TO>
 int launch_conv0_gn(const float* x, int B, int L, const float* norm, const float* w0, const float* b0,
@@ -268,7 +384,18 @@ int launch_conv0_gn(const float* x, int B, int L, const float* norm, const float
                      beta, eps, ss);
   if (C % 8) return -3;
   dim3 grid((T0 + C0_T - 1) / C0_T, B), block(256);
-  if (sizeof(TO) == 2 && !gelu_exact_env())   // bf16 output: gelu_sig2 (common.h)
+  const char* ev = getenv("SSE_CONV0_VALU");   // A/B and tests: the VALU kernel below
+  const bool valu = ev && ev[0] == '1';
+  if (sizeof(TO) == 2 && !gelu_exact_env() && C == 512 && !valu) {   // matrix-core conv0
+    bf16x8* wf = (bf16x8*)((char*)mom + ((size_t)B * NMOM * sizeof(double) + 255) / 256 * 256);
+    hipLaunchKernelGGL(conv0_wfrag_kernel, dim3((C / 16 * 64 + 255) / 256), dim3(256), 0, s, w0, C, wf);
+    // 3 resident blocks per CU (168 VGPRs): spread each clip's chunks over G blocks, G * B ~ 3 * 256
+    const int nchunk = (T0 + C0M_T - 1) / C0M_T;
+    int G = (3 * 256 + B - 1) / B;
+    G = G < 1 ? 1 : (G > nchunk ? nchunk : G);
+    hipLaunchKernelGGL(conv0_mfma_kernel, dim3(G, B), dim3(256), 0, s, x, L, norm, (const bf16x8*)wf, b0, T0,
+                       (const float2*)ss, (bf16*)out);
+  } else if (sizeof(TO) == 2 && !gelu_exact_env())   // bf16 output: gelu_sig2 (common.h)
     hipLaunchKernelGGL((conv0_apply_kernel<TO, false, true>), grid, block, 0, s, x, L, norm, w0, b0, C, T0, ss, out);
   else
     hipLaunchKernelGGL((conv0_apply_kernel<TO, false, false>), grid, block, 0, s, x, L, norm, w0, b0, C, T0, ss, out);

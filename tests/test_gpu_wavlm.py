@@ -175,3 +175,31 @@ def test_bf16_posconv_kernel_matches_grouped_gemm(monkeypatch, wavlm_sd, n_clips
     assert _rel(h0.reshape(-1), g0.reshape(-1)) <= 1e-5
     assert _rel(a[:, 0], b[:, 0]).max() <= 1e-5
     assert _rel(a, b).max() <= 5e-3
+
+
+@pytest.mark.parametrize("samples", [16000, 20001, 48000])
+def test_bf16_conv0_matrix_core_matches_valu(monkeypatch, wavlm_sd, samples):
+    """conv0 + GroupNorm + GELU on the matrix cores (split-bf16 K = 32 MFMA, conv0_mfma_kernel)
+    against the packed-fp32 VALU kernel (SSE_CONV0_VALU=1).  The convolutions agree to ~1e-5 before
+    the bf16 output rounding; the rare rounding flips then propagate through six bf16 conv GEMMs like
+    any bf16 noise, so the two bf16 paths are compared by their distance to the fp32 path (which
+    runs conv0 in fp32 FMAs): the matrix-core path must be no farther from it than the VALU path."""
+    from ssr_amd import config as C, synth
+    from ssr_amd.model import SSEModel
+    w = torch.from_numpy(synth.synth_clips(3, samples, seed=17)).cuda()
+    idx = [0, 6, 12]
+    m32 = SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype="fp32")
+    ref, h_ref = m32.embed(w, idx).cpu().numpy(), m32.hidden_states(w[:1])[0].cpu().numpy().reshape(-1)
+    del m32
+    m = SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype="bf16")
+    a = m.embed(w, idx).cpu().numpy()
+    h0 = m.hidden_states(w[:1])[0].cpu().numpy().reshape(-1)
+    monkeypatch.setenv("SSE_CONV0_VALU", "1")
+    b = m.embed(w, idx).cpu().numpy()
+    g0 = m.hidden_states(w[:1])[0].cpu().numpy().reshape(-1)
+    e_m, e_v = _rel(h0, h_ref), _rel(g0, h_ref)
+    E_m, E_v = _rel(a, ref).max(), _rel(b, ref).max()
+    print("hidden_states[0] vs fp32: mfma", e_m, "valu", e_v, "| embeddings: mfma", E_m, "valu", E_v,
+          "| mfma vs valu", _rel(h0, g0))
+    assert _rel(h0, g0) <= 1e-2
+    assert e_m <= 1.25 * e_v and E_m <= 1.25 * E_v + 1e-3
