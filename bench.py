@@ -18,8 +18,10 @@ The JSON line carries:
                 stream (sse_profile_*) during a second timed region of the same K steps
                 (profiled_ms_per_step: that region's step time, events included); traffic from
                 the committed rocprofv3 PMC summary of the same workload.
-  cpu_baseline  the numpy oracle ("port") on this host's cores, a bounded sample of clips
-                (rank 0, N = 1 only).
+  cpu_baseline  the reference's CPU path on this host's cores, a bounded sample of clips (rank 0,
+                N = 1 only): WavLM = oracle/wavlm_aten.py, the reference's batch-1 loop on the same
+                ATen ops, calibrated against the reference itself ("calibrated-aten",
+                profiles/r2_cpu_baseline_calibration.json).
 """
 from __future__ import annotations
 
@@ -68,27 +70,64 @@ def parse():
     return ap.parse_args()
 
 
+def host_threads() -> int:
+    """CPU threads this process may use: its affinity set, capped by OMP_NUM_THREADS when the host
+    sets one (the GPU box gives each 1-GPU job a 16-CPU share of a 256-CPU machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(n, int(omp))) if omp.isdigit() and int(omp) > 0 else n
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+CALIBRATION = "profiles/r2_cpu_baseline_calibration.json"
+
+
 def cpu_baseline(model_name: str, n: int, seconds: float):
-    """The oracle (numpy restatement of the reference path, batch-1 loop like the reference)
-    timed on this host's cores.  Test infrastructure used only as the reported baseline."""
-    from threadpoolctl import threadpool_info
+    """The reference's CPU path timed on this host's cores (rank 0, N = 1).  WavLM: the ATen
+    restatement oracle/wavlm_aten.py (the reference's batch-1 loop on the same torch ops as HF
+    WavLMModel), calibrated against the reference itself (oracle/calibrate_cpu_baseline.py).
+    Test infrastructure, used only as the reported baseline."""
     if model_name.startswith("wavlm"):
-        from oracle.wavlm import WavLMOracle
+        from oracle.wavlm_aten import WavLMAten
+        thr = host_threads()
+        torch.set_num_threads(thr)
         spec = C.WAVLM_BASE if model_name == "wavlm-base" else C.WAVLM_LARGE
-        o = WavLMOracle(spec, synth.synth_wavlm_state_dict(spec, seed=7))
+        o = WavLMAten(spec, synth.synth_wavlm_state_dict(spec, seed=7))
         clips = synth.synth_clips(n + 1, int(16000 * seconds), seed=2024)
-        o.embed(clips[:1], spec.default_layer_indices())            # warm-up (BLAS threads, page-in)
+        idx = spec.default_layer_indices()
+        o.extract(clips[0], idx)                                     # warm-up (threads, page-in)
         t0 = time.perf_counter()
-        o.embed(clips[1:], spec.default_layer_indices())
+        for c in clips[1:]:
+            o.extract(c, idx)
         dt = time.perf_counter() - t0
-    else:
-        from oracle.whisper import WhisperOracle
-        spec = C.WHISPER_LARGE_V2
-        o = WhisperOracle(spec, synth.synth_whisper_state_dict(spec, seed=11))
-        clips = synth.synth_clips(n, int(16000 * seconds), seed=2024)
-        t0 = time.perf_counter()
-        o.embed(clips, spec.default_layer_indices())
-        dt = time.perf_counter() - t0
+        cal = None
+        if os.path.exists(os.path.join(ROOT, CALIBRATION)):
+            with open(os.path.join(ROOT, CALIBRATION)) as fh:
+                cal = json.load(fh)
+        return {"value": round(n / dt, 4), "unit": "clips/s", "cores": thr, "kind": "calibrated-aten",
+                "calibration_ratio": cal and cal["ratio"], "calibration_source": cal and CALIBRATION,
+                "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+                "sample": f"{n} synthetic {seconds:g} s clips, batch-1 loop of oracle/wavlm_aten.py (the reference's "
+                          f"fp32 ATen ops, torch.set_num_threads({thr})), {dt:.1f} s"}
+    # Whisper: the numpy oracle (uncalibrated port; the bench's default workload is WavLM)
+    from threadpoolctl import threadpool_info
+    from oracle.whisper import WhisperOracle
+    spec = C.WHISPER_LARGE_V2
+    o = WhisperOracle(spec, synth.synth_whisper_state_dict(spec, seed=11))
+    clips = synth.synth_clips(n, int(16000 * seconds), seed=2024)
+    t0 = time.perf_counter()
+    o.embed(clips, spec.default_layer_indices())
+    dt = time.perf_counter() - t0
     threads = max([p.get("num_threads", 1) for p in threadpool_info()] + [1])
     return {"value": round(n / dt, 4), "unit": "clips/s", "cores": int(threads), "kind": "port",
             "sample": f"{n} synthetic {seconds:g} s clips, batch-1 loop of oracle/{model_name.split('-')[0]}.py "
@@ -101,7 +140,7 @@ TRAFFIC_FILE = {("wavlm-base", "bf16"): "profiles/r1_pmc_traffic_wavlm_base_bf16
                 ("whisper-large-v2", "fp8"): "profiles/r1_pmc_traffic_whisper_large_v2_fp8.json"}
 TAG_SYMBOLS = {"gemm": ("gemm8_kernel<0, false, false, false>", "gemm8p_kernel"),
                "gemm_mx": ("gemm8_kernel<0, true, false, true>", "gemm8_kernel<0, false, false, true>"),
-               "attn": ("attention_",), "conv0_gn": ("conv0_apply",)}
+               "attn": ("attention_",), "conv0_gn": ("conv0_mfma", "conv0_moments", "gn_finalize")}
 
 
 def pmc_traffic(model_name, dtype, kernel, launch_counts):
@@ -222,11 +261,15 @@ def main():
     del sd
     idx = spec.default_layer_indices()
     clips = torch.from_numpy(synth.synth_clips(B, L, seed=1234, first_clip=rank * B)).to(dev)
-    out = torch.empty((B, len(idx), spec.hidden), dtype=torch.float32, device=dev)
-    gathered = torch.empty((world * B, len(idx), spec.hidden), dtype=torch.float32, device=dev) if world > 1 else None
+    # two output slots: step k's all-gather (RCCL, async on its own stream) overlaps step k+1's compute
+    outs = [torch.empty((B, len(idx), spec.hidden), dtype=torch.float32, device=dev) for _ in range(2)]
+    gathered = [torch.empty((world * B, len(idx), spec.hidden), dtype=torch.float32, device=dev)
+                for _ in range(2)] if world > 1 else None
+    pending = [None, None]
 
     if a.corpus:
         return corpus_run(a, model, spec, idx, clips, B, L, world, rank, dev, dist)
+    it_slot = [0]
 
     # --stream (configs[4] "streaming extraction"): each step's clips come from pinned host memory,
     # copied on a side stream into the other of two device buffers while this step computes
@@ -246,6 +289,12 @@ def main():
         it = [0]
 
     def step():
+        slot = it_slot[0] % 2
+        it_slot[0] += 1
+        out = outs[slot]
+        if pending[slot] is not None:        # the gather that last read this slot
+            pending[slot].wait()
+            pending[slot] = None
         if a.stream:
             cur, nxt = it[0] % 2, (it[0] + 1) % 2
             it[0] += 1
@@ -259,10 +308,17 @@ def main():
         else:
             model.embed(clips, idx, out=out)
         if dist is not None:
-            dist.all_gather_into_tensor(gathered, out)
+            pending[slot] = dist.all_gather_into_tensor(gathered[slot], out, async_op=True)
+
+    def drain():
+        for i in range(2):
+            if pending[i] is not None:
+                pending[i].wait()
+                pending[i] = None
 
     for _ in range(a.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
 
     def timed(profile):
@@ -275,6 +331,7 @@ def main():
         t0 = time.perf_counter()
         for _ in range(a.steps):
             step()
+        drain()
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
@@ -321,7 +378,7 @@ def main():
                 rf["traffic_source"] = src + " (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE, bytes per launch)"
             res["roofline"] = rf
         res["model_flops_frac"] = round(value / world * FLOP_PER_CLIP[a.model] / 1e12 / PEAK_TFLOPS[a.dtype], 4)
-        ncpu = a.cpu_sample if a.cpu_sample is not None else (48 if wavlm else 2)   # ~10-30 s of CPU work
+        ncpu = a.cpu_sample if a.cpu_sample is not None else (64 if wavlm else 2)   # ~10-30 s of CPU work
         if world == 1 and ncpu > 0:
             res["cpu_baseline"] = cpu_baseline(a.model, ncpu, secs)
         print(json.dumps(res), flush=True)

@@ -206,6 +206,19 @@ int sse_mel_filters(int n_mels, float* out);
 /* Library version string. */
 const char* sse_version(void);
 
+/* Kernel-selection switches for A/B equality tests (no reference counterpart; the library never
+ * reads the environment).  Process-wide; 0 is the production choice for every name:
+ *   "gemm_cfg"          1 = no 256x256 tile, 2 = 256x128 3-stage ring, 3 = 2-stage 256x256 kernel
+ *   "gemm_nonpersist"   1 = non-persistent 8-phase bf16 GEMM for every shape
+ *   "gelu_exact"        1 = erf-GELU in the bf16 path's epilogues
+ *   "conv0_valu"        1 = VALU conv0 + GroupNorm kernel instead of the matrix-core one
+ *   "posconv_gemm"      1 = grouped GEMM for the bf16 positional conv
+ *   "no_lnfold"         1 = materialise the post-LN LayerNorm outputs (bf16 WavLM-base)
+ *   "gemm_mx_staged"    1 = LDS-staged epilogue for every MX-fp8 GEMM
+ * sse_set_option returns the previous value (>= 0) or SSE_ERR_INVALID for an unknown name. */
+int sse_set_option(const char* name, int value);
+int sse_get_option(const char* name);
+
 #ifdef __cplusplus
 }
 #endif

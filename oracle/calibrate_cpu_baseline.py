@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""ORACLE tooling (container only): calibrate bench.py's CPU baseline against the reference itself.
+
+Times, in this container, on the same clips, weights and thread count:
+  * the reference's own ``extract_wavlm_embeddings`` (REF/WavLM_embeddings.py:267-341) on an HF
+    ``WavLMModel`` (imported the way tests/golden/make_golden.py does: torchaudio stub, temp cwd,
+    no bytecode written under /root/reference), batch-1 loop over ``N`` clips (REF :578-586);
+  * ``oracle/wavlm_aten.py`` (the ATen restatement bench.py times on the GPU box).
+The two are run in alternating rounds and each rate is the median over rounds.  The ratio
+restatement / reference must lie in [0.9, 1.1]; the result goes to
+profiles/r2_cpu_baseline_calibration.json (bench.py copies the ratio into its cpu_baseline).
+
+Usage: python oracle/calibrate_cpu_baseline.py [--clips 16] [--rounds 3] [--threads 8]
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import importlib.util
+import json
+import os
+import platform
+import statistics
+import subprocess
+import sys
+import tempfile
+import time
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+
+
+def cpu_model() -> str:
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return platform.processor() or "unknown"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clips", type=int, default=16)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--threads", type=int, default=os.cpu_count())
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r2_cpu_baseline_calibration.json"))
+    a = ap.parse_args()
+
+    spec_mg = importlib.util.spec_from_file_location("make_golden", os.path.join(ROOT, "tests", "golden", "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec_mg)
+    spec_mg.loader.exec_module(mg)          # imports torch + transformers first (stub order)
+    import numpy as np
+    import torch
+    from transformers import Wav2Vec2FeatureExtractor, WavLMConfig, WavLMModel
+    from ssr_amd import config as C, synth
+    from oracle.wavlm_aten import WavLMAten
+
+    torch.set_num_threads(a.threads)
+    spec = C.WAVLM_BASE
+    sd = synth.synth_wavlm_state_dict(spec, seed=7)
+    model = WavLMModel(WavLMConfig())
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=False)
+    model.eval()
+    fe = Wav2Vec2FeatureExtractor(do_normalize=False)
+    aten = WavLMAten(spec, sd)
+    clips = synth.synth_clips(a.clips + 1, 48000, seed=2024)
+    idx = spec.default_layer_indices()
+    paths = mg._register("calib", clips)
+
+    cwd = os.getcwd()
+    ref_rates, port_rates, max_rel = [], [], 0.0
+    with tempfile.TemporaryDirectory() as td:
+        os.chdir(td)
+        try:
+            mg._install_torchaudio_stub()
+            ref = mg._import_ref("ref_wavlm_embeddings", "WavLM_embeddings.py")
+            ref.extract_wavlm_embeddings(paths[0], model, fe, "cpu", idx)       # warm-up both
+            aten.extract(clips[0], idx)
+            for _ in range(a.rounds):
+                t0 = time.perf_counter()
+                got_ref = [ref.extract_wavlm_embeddings(p, model, fe, "cpu", idx) for p in paths[1:]]
+                ref_rates.append(a.clips / (time.perf_counter() - t0))
+                t0 = time.perf_counter()
+                got = [aten.extract(c, idx) for c in clips[1:]]
+                port_rates.append(a.clips / (time.perf_counter() - t0))
+                for d0, d1 in zip(got_ref, got):
+                    for k in d0:
+                        max_rel = max(max_rel, float(np.linalg.norm(d1[k] - d0[k]) / np.linalg.norm(d0[k])))
+        finally:
+            os.chdir(cwd)
+    r_ref, r_port = statistics.median(ref_rates), statistics.median(port_rates)
+    res = {"reference_clips_per_s": round(r_ref, 3), "restatement_clips_per_s": round(r_port, 3),
+           "ratio": round(r_port / r_ref, 4), "rounds_reference": [round(x, 3) for x in ref_rates],
+           "rounds_restatement": [round(x, 3) for x in port_rates], "threads": a.threads,
+           "host_cpus": os.cpu_count(), "cpu_model": cpu_model(), "clips": a.clips, "clip_s": 3.0,
+           "max_rel_l2_restatement_vs_reference": max_rel, "torch": torch.__version__,
+           "what": "REF/WavLM_embeddings.py:267-341 extract_wavlm_embeddings (HF WavLMModel, fp32, batch-1 loop) "
+                   "vs oracle/wavlm_aten.py on the same clips / weights / threads, alternating rounds, medians"}
+    os.makedirs(os.path.dirname(a.out), exist_ok=True)
+    with open(a.out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res, indent=1))
+    if not 0.9 <= res["ratio"] <= 1.1:
+        raise SystemExit(f"calibration ratio {res['ratio']} outside [0.9, 1.1]")
+
+
+if __name__ == "__main__":
+    main()

@@ -7,15 +7,14 @@ eager-PyTorch math.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 
 from .config import KIND_WAVLM, WavLMSpec, WhisperSpec
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# SSE_LIB_PATH: load another build of the same ABI (A/B timing of two builds on one box,
-# tools/ab_bench.sh); unset in tests and in the product path.
-LIB_PATH = os.environ.get("SSE_LIB_PATH") or os.path.join(_HERE, "libsse.so")
+LIB_PATH = os.path.join(_HERE, "libsse.so")
 
 SSE_DTYPE_F32 = 0
 SSE_DTYPE_BF16 = 1
@@ -28,7 +27,8 @@ EXPORTED = ("sse_weight_floats", "sse_model_create", "sse_model_destroy", "sse_o
             "sse_profile_start", "sse_profile_read", "sse_profile_stop", "sse_gemm", "sse_whisper_embed",
             "sse_whisper_decoder_hidden_states", "sse_mono", "sse_resample_length", "sse_resample_workspace_bytes",
             "sse_resample", "sse_augment", "sse_mx_scale_bytes", "sse_mx_scale_offset", "sse_mx_quantize",
-            "sse_mx_quantize_host", "sse_gemm_mx", "sse_pitch_shift_workspace_bytes", "sse_pitch_shift")
+            "sse_mx_quantize_host", "sse_gemm_mx", "sse_pitch_shift_workspace_bytes", "sse_pitch_shift",
+            "sse_set_option", "sse_get_option")
 
 
 class SSEError(RuntimeError):
@@ -158,6 +158,10 @@ def lib() -> ctypes.CDLL:
     L.sse_rel_bucket.restype = i32
     L.sse_mel_filters.argtypes = [i32, vp]
     L.sse_mel_filters.restype = i32
+    L.sse_set_option.argtypes = [ctypes.c_char_p, i32]
+    L.sse_set_option.restype = i32
+    L.sse_get_option.argtypes = [ctypes.c_char_p]
+    L.sse_get_option.restype = i32
     L.sse_version.argtypes = []
     L.sse_version.restype = ctypes.c_char_p
     _lib = L
@@ -177,3 +181,15 @@ def check(rc: int, what: str) -> None:
     if rc == -6:
         raise SSEOutOfMemoryError(rc, what)
     raise SSEError(rc, what)
+
+
+@contextlib.contextmanager
+def option(name: str, value: int):
+    """Temporarily set one of libsse.so's A/B kernel-selection switches (sse_set_option)."""
+    prev = lib().sse_set_option(name.encode(), int(value))
+    if prev < 0:
+        raise SSEError(prev, f"sse_set_option({name!r})")
+    try:
+        yield
+    finally:
+        lib().sse_set_option(name.encode(), prev)

@@ -47,6 +47,9 @@ VARIANTS = {
            "volume": (0.8, 1.2), "pitch": (-2, 2)},
 }
 
+# (augmentation_factor, minority_threshold) defaults of each reference variant's apply_data_augmentation
+VARIANT_DEFAULTS = {"1": (2, 200), "01": (3, 100)}
+
 
 @dataclass
 class AugSpec:
@@ -144,6 +147,20 @@ def augment_audio(waveform, sample_rate=16000, augmentation_type="random", *, rn
         return x.numpy()
 
 
+def _per_clip_fallback(run, part):
+    """run(part) -> one result per clip.  A failing batch (a clip shorter than the receptive field,
+    OOM, ...) is retried one clip at a time; a clip that still fails gets None and is skipped, as
+    the reference's per-sample try/except does (REF/model_training_1.py:379-419)."""
+    try:
+        return run(part)
+    except Exception as e:
+        if len(part) == 1:
+            logger.warning(f"Error extracting embeddings from augmented audio: {e}")
+            return [None]
+        logger.warning(f"Batched embedding of {len(part)} augmented clips failed ({e}); retrying one at a time")
+        return [r for j in part for r in _per_clip_fallback(run, [j])]
+
+
 def _embed_jobs(audios, model, feature_extractor, device, layer_names, model_type, batch):
     """Embed a list of 1-D cuda clips -> list of {layer_name: float32[H]} (None on failure)."""
     from .extract import extract_embeddings_from_audio_wavlm, extract_embeddings_from_audio_whisper
@@ -158,14 +175,20 @@ def _embed_jobs(audios, model, feature_extractor, device, layer_names, model_typ
             by_len = {}
             for j, a in enumerate(audios):
                 by_len.setdefault(int(a.shape[-1]), []).append(j)
+            if not valid:                      # no requested layer exists: {} per clip (REF :259-264)
+                return [{} for _ in audios]
+
+            def run(part):
+                x = torch.stack([audios[j] for j in part])
+                x = feature_extractor(x, sampling_rate=16000, return_tensors="pt").to(device).input_values
+                e = model.embed(x, valid).cpu().numpy()
+                return [{f"layer_{i}": e[r, q].copy() for q, i in enumerate(valid)} for r in range(len(part))]
+
             for L, js in by_len.items():
                 for c in range(0, len(js), batch):
                     part = js[c:c + batch]
-                    x = torch.stack([audios[j] for j in part])
-                    x = feature_extractor(x, sampling_rate=16000, return_tensors="pt").to(device).input_values
-                    e = model.embed(x, valid).cpu().numpy()
-                    for r, j in enumerate(part):
-                        out[j] = {f"layer_{i}": e[r, q].copy() for q, i in enumerate(valid)}
+                    for j, r in zip(part, _per_clip_fallback(run, part)):
+                        out[j] = r
             return out
         for j, a in enumerate(audios):
             out[j] = extract_embeddings_from_audio_wavlm(a.cpu().numpy(), model, feature_extractor, device, idx)
@@ -180,15 +203,24 @@ def _embed_jobs(audios, model, feature_extractor, device, layer_names, model_typ
             by_len = {}
             for j, a in enumerate(audios):
                 by_len.setdefault(int(a.shape[-1]), []).append(j)
+            if not enc and not dec:
+                return [{} for _ in audios]
+
+            def run(part):
+                e, d = model.sse.whisper_embed(torch.stack([audios[j] for j in part]), enc, dec)
+                e, d = e.cpu().numpy(), d.cpu().numpy()
+                res = []
+                for r in range(len(part)):
+                    x = {f"encoder_layer_{i}": e[r, q].copy() for q, i in enumerate(enc)}
+                    x.update({f"decoder_layer_{i}": d[r, q].copy() for q, i in enumerate(dec)})
+                    res.append(x)
+                return res
+
             for L, js in by_len.items():
                 for c in range(0, len(js), batch):
                     part = js[c:c + batch]
-                    e, d = model.sse.whisper_embed(torch.stack([audios[j] for j in part]), enc, dec)
-                    e, d = e.cpu().numpy(), d.cpu().numpy()
-                    for r, j in enumerate(part):
-                        res = {f"encoder_layer_{i}": e[r, q].copy() for q, i in enumerate(enc)}
-                        res.update({f"decoder_layer_{i}": d[r, q].copy() for q, i in enumerate(dec)})
-                        out[j] = res
+                    for j, r in zip(part, _per_clip_fallback(run, part)):
+                        out[j] = r
             return out
         for j, a in enumerate(audios):
             out[j] = extract_embeddings_from_audio_whisper(a.cpu().numpy(), model, feature_extractor, device,
@@ -199,12 +231,16 @@ def _embed_jobs(audios, model, feature_extractor, device, layer_names, model_typ
 
 
 def apply_data_augmentation(train_meta, train_embeddings, model, feature_extractor, device, layer_names, model_type,
-                            augmentation_factor=2, minority_threshold=200, *, rng=_random, variant="1", seed=0,
+                            augmentation_factor=None, minority_threshold=None, *, rng=_random, variant="1", seed=0,
                             batch=64, cache=None):
     """REF/model_training_1.py:318-464 twin, batched on the GPU.  ``cache`` (a dict) hoists the
     work out of the caller's per-layer loop: the first call augments and embeds every layer in
     ``layer_names`` once; later calls with the same clips reuse it (no further random draws)."""
     from .extract import load_audio
+    # per-variant defaults: REF/model_training_1.py:319 (2, 200), REF/model_training_01.py:291 (3, 100)
+    d_factor, d_thresh = VARIANT_DEFAULTS[variant]
+    augmentation_factor = d_factor if augmentation_factor is None else augmentation_factor
+    minority_threshold = d_thresh if minority_threshold is None else minority_threshold
     logger.info("\n=== Applying Data Augmentation ===")
     if "path" not in train_meta.columns:
         logger.warning("No audio file paths found. Skipping data augmentation.")

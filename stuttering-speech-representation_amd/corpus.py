@@ -53,7 +53,7 @@ def extract_corpus(clip_source: Callable[[int, int], np.ndarray | torch.Tensor],
         if not isinstance(wave, torch.Tensor):
             wave = torch.from_numpy(np.ascontiguousarray(wave))
         local[s - start:e - start] = embed_fn(wave.to(device, torch.float32))
-    if world == 1:
+    if not dist.is_initialized():
         return local[:n_items]
     full = torch.empty((world * per,) + tuple(out_shape), dtype=torch.float32, device=device)
     dist.all_gather_into_tensor(full, local, group=group)

@@ -112,11 +112,21 @@ SSE_DEV double wave_sum_d(double v) {
 // ACT_GELU_FAST: gelu_sig2, used by the bf16 path only (host picks it, see gelu_act<T>()).
 enum { ACT_NONE = 0, ACT_GELU = 1, ACT_GELU_FAST = 2 };
 
-// SSE_GELU_EXACT=1 keeps the erf form on the bf16 path too (A/B runs, equality tests).
-inline bool gelu_exact_env() {
-  static const bool exact = [] { const char* e = getenv("SSE_GELU_EXACT"); return e && e[0] == '1'; }();
-  return exact;
-}
+// Kernel-selection switches for A/B equality tests, set only through the C-ABI
+// (sse_set_option, include/sse.h); process-wide, 0 = the production choice.  Nothing is read from
+// the environment.
+enum {
+  OPT_GEMM_CFG = 0,     // 1: never 256x256, 2: 256x128 3-stage ring, 3: 2-stage 256x256 kernel
+  OPT_GEMM_NONPERSIST,  // 1: the non-persistent LDS-staged 8-phase kernel for every shape
+  OPT_GELU_EXACT,       // 1: erf-GELU on the bf16 path too
+  OPT_CONV0_VALU,       // 1: packed-fp32 VALU conv0 instead of the matrix-core kernel
+  OPT_POSCONV_GEMM,     // 1: grouped GEMM for the bf16 positional conv
+  OPT_NO_LNFOLD,        // 1: materialise post-LN LayerNorm outputs (bf16 WavLM-base)
+  OPT_GEMM_MX_STAGED,   // 1: LDS-staged epilogue for every MX-fp8 GEMM
+  OPT_COUNT
+};
+int sse_opt(int id);
+inline bool gelu_exact_env() { return sse_opt(OPT_GELU_EXACT) != 0; }
 
 // ---------------------------------------------------------------------------------------
 // GEMM descriptor.  C[m][n] = sum_k A(m, k) * Bt[n][k]  (+bias[n]) (act) (+resid[m][n]).

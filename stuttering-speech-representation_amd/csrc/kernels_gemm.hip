@@ -330,16 +330,15 @@ int launch_any(const GemmArgs& a, int amode, int groups, hipStream_t s) {
   // bf16 default for the big encoder GEMMs: 256x256 tile, 8 waves (2x4) of 128x64, 2-stage
   // 128 KiB LDS ring (1 block/CU).  Measured on the WavLM-base B=256 shapes vs the 128x128 tile:
   // qkv 837 vs 636, ffn1 691 vs 605, ffn2 931 vs 801, oproj 510 vs 489 TF/s (profiles/r1_gemm_configs.json).
-  // Otherwise 128x128, 4 waves of 64x64, 2 stages (2 blocks/CU).  SSE_GEMM_CFG (read per
-  // launch, so one process can A/B): 1 = never 256x256, 2 = 256x128 3-stage ring.
-  const char* fe = getenv("SSE_GEMM_CFG");
-  const int force = fe ? atoi(fe) : 0;
+  // Otherwise 128x128, 4 waves of 64x64, 2 stages (2 blocks/CU).  OPT_GEMM_CFG (tests, A/B):
+  // 1 = never 256x256, 2 = 256x128 3-stage ring.
+  const int force = sse_opt(OPT_GEMM_CFG);
   if (a.N % 128 == 0 && a.M >= 2048 && force == 2) return launch_cfg<T, 256, 128, 4, 2, 3>(a, amode, groups, s);
   if constexpr (sizeof(T) == 2) {
     // default for plain / SEG-row bf16 GEMMs with N % 256 == 0, K % 64 == 0: the 8-phase
     // ping-pong 256x256 kernel (kernels_gemm8.hip; measured vs this file's 256x256 2-stage loop:
     // qkv 863 vs 760, ffn1 721 vs 653, ffn2 997 vs 880, 4096^3 1353 vs 1192 TF/s).
-    // SSE_GEMM_CFG=3 keeps the 2-stage 256x256 kernel for A/B runs.
+    // OPT_GEMM_CFG = 3 keeps the 2-stage 256x256 kernel for A/B runs.
     if ((force == 0 || force == 4) && amode == AMODE_SEG && groups == 1 && a.N % 256 == 0 && a.K % 64 == 0 &&
         a.M >= 4096)
       return launch_gemm8_bf16(a, s);

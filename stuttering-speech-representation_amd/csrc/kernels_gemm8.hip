@@ -144,7 +144,7 @@ SSE_DEV i32x8 g8_cat(bf16x8 lo, bf16x8 hi) {
   return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-// DBG = 1 (SSE_GEMM_DEBUG=skip_epi, timing experiments only): no epilogue, a checksum keeps the MFMAs live.
+// DBG = 1 (timing experiments only, not launched by the library): no epilogue, a checksum keeps the MFMAs live.
 template <bool RES, bool Q8 = false>
 SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, int n0, int wm, int wn,
                                 int q, int r16);
@@ -880,19 +880,9 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
 int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
   if (a.M <= 0 || a.N % 256 || a.K % 64 || a.K <= 0) return -3;
   dim3 grid((unsigned)(((a.M + 255) / 256) * (a.N / 256)));
-  static const bool skip_epi = [] { const char* e = getenv("SSE_GEMM_DEBUG"); return e && !strcmp(e, "skip_epi"); }();
-  // A/B switches: SSE_GEMM_PERSIST=0 (non-persistent LDS-staged kernel for every shape),
-  // SSE_GEMM_NT=1 (non-temporal epilogue stores in that kernel)
-  const char* npe = getenv("SSE_GEMM_PERSIST");   // read per launch (tests flip it)
-  const bool np = npe && npe[0] == '0';
-  static const bool nt = [] { const char* e = getenv("SSE_GEMM_NT"); return e && e[0] == '1'; }();
-  if (skip_epi) {
-    hipLaunchKernelGGL((gemm8_kernel<1, true, false>), grid, dim3(512), 0, s, a);
-  } else if (a.resid || np) {
-    if (nt)
-      hipLaunchKernelGGL((gemm8_kernel<0, false, true>), grid, dim3(512), 0, s, a);
-    else
-      hipLaunchKernelGGL((gemm8_kernel<0, false, false>), grid, dim3(512), 0, s, a);
+  // OPT_GEMM_NONPERSIST (tests, A/B): the non-persistent LDS-staged kernel for every shape
+  if (a.resid || sse_opt(OPT_GEMM_NONPERSIST)) {
+    hipLaunchKernelGGL((gemm8_kernel<0, false, false>), grid, dim3(512), 0, s, a);
   } else {
     // persistent: one block per CU (LDS-bound), at most one per tile
     static int cus[64] = {0};
@@ -916,10 +906,9 @@ int launch_gemm8_mx(const GemmArgs& a, hipStream_t s) {
   dim3 grid((unsigned)(((a.M + 255) / 256) * (a.N / 256)));
   // Non-persistent for every MX shape: the persistent kernel exceeds 256 VGPRs with the MX operand
   // tuples and would spill inside the counted-vmcnt main loop.  Without a residual the MFMAs
-  // compute C^T and the epilogue stores from registers (no LDS round trip; SSE_GEMM_MX_STAGED=1
+  // compute C^T and the epilogue stores from registers (no LDS round trip; OPT_GEMM_MX_STAGED
   // keeps the LDS-staged epilogue for A/B runs); residual GEMMs take the staged epilogue.
-  const char* stg = getenv("SSE_GEMM_MX_STAGED");
-  if (!a.resid && !(stg && stg[0] == '1'))
+  if (!a.resid && !sse_opt(OPT_GEMM_MX_STAGED))
     hipLaunchKernelGGL((gemm8_kernel<0, true, false, true>), grid, dim3(512), 0, s, a);
   else
     hipLaunchKernelGGL((gemm8_kernel<0, false, false, true>), grid, dim3(512), 0, s, a);

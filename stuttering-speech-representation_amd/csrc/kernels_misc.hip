@@ -384,8 +384,7 @@ int launch_conv0_gn(const float* x, int B, int L, const float* norm, const float
                      beta, eps, ss);
   if (C % 8) return -3;
   dim3 grid((T0 + C0_T - 1) / C0_T, B), block(256);
-  const char* ev = getenv("SSE_CONV0_VALU");   // A/B and tests: the VALU kernel below
-  const bool valu = ev && ev[0] == '1';
+  const bool valu = sse_opt(OPT_CONV0_VALU) != 0;   // A/B and tests: the VALU kernel below
   if (sizeof(TO) == 2 && !gelu_exact_env() && C == 512 && !valu) {   // matrix-core conv0
     bf16x8* wf = (bf16x8*)((char*)mom + ((size_t)B * NMOM * sizeof(double) + 255) / 256 * 256);
     hipLaunchKernelGGL(conv0_wfrag_kernel, dim3((C / 16 * 64 + 255) / 256), dim3(256), 0, s, w0, C, wf);

@@ -28,9 +28,18 @@
 
 #define SSE_VERSION "sse 0.1.0 (gfx950)"
 
+// A/B switches (common.h OPT_*), set only through sse_set_option
+static int g_opt[OPT_COUNT] = {0};
+static const char* const g_opt_name[OPT_COUNT] = {"gemm_cfg", "gemm_nonpersist", "gelu_exact", "conv0_valu",
+                                                   "posconv_gemm", "no_lnfold", "gemm_mx_staged"};
+int sse_opt(int id) { return __atomic_load_n(&g_opt[id], __ATOMIC_RELAXED); }
+
 namespace {
 
-constexpr int MAXD = 4095;   // relative-position table covers |key - query| <= MAXD (saturates at 800)
+// relative-position table covers |key - query| <= MAXD; the attention kernels clamp d to +-MAXD, which
+// is exact for any clip length because the bucket saturates at max_distance (HF
+// _relative_positions_bucket: every |d| >= max_distance maps to the last bucket of its sign)
+constexpr int MAXD = 4095;
 
 inline uint16_t f2bf_bits(float f) {
   uint32_t u;
@@ -185,6 +194,7 @@ bool cfg_valid(const sse_cfg* c) {
   if (c->hidden % c->heads || c->hidden / c->heads != 64) return false;
   if (c->kind == SSE_KIND_WAVLM) {
     if (c->n_conv < 2 || c->n_conv > 8 || c->pos_groups <= 0 || c->hidden % c->pos_groups) return false;
+    if (c->max_distance > MAXD) return false;   // the clamp to +-MAXD must lie in the saturated range
   } else if (c->kind == SSE_KIND_WHISPER) {
     if (c->n_mels <= 0 || c->max_positions <= 0) return false;
     if (c->decoder_layers < 0 || (c->decoder_layers > 0 && c->dec_ffn <= 0)) return false;
@@ -682,9 +692,8 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     g.rows_per_seg = Tf; g.T_in = Tf; g.stride = 1; g.pad = K / 2; g.cin = cg; g.ld_in = H;
     g.bias = m->ptr<float>(m->pos_b); g.resid = x; g.Cf = x; g.ldc = H; g.act = ACT_GELU; g.zero = zero;
     // bf16: the dedicated kernel (input window staged once per block, kernels_posconv.hip);
-    // SSE_POSCONV_GEMM=1 keeps the grouped GEMM for A/B runs
-    const char* pge = getenv("SSE_POSCONV_GEMM");
-    const bool use_gemm = sizeof(T) != 2 || (pge && pge[0] == '1');
+    // OPT_POSCONV_GEMM keeps the grouped GEMM for A/B runs
+    const bool use_gemm = sizeof(T) != 2 || sse_opt(OPT_POSCONV_GEMM);
     RC(prof(m, s, "gemm_conv:posconv", gflops(g, G), gbytes<T>(g, AMODE_CONV, G), [&] {
       if (!use_gemm) {
         const int rc = launch_posconv_bf16((const bf16*)xt, m->ptr<bf16>(m->pos_w), m->ptr<float>(m->pos_b), x, B, Tf, H,
@@ -704,9 +713,8 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
   float* hf = c.stable_layer_norm ? (float*)(ws + w.hf) : nullptr;
   // bf16 post-LN: LayerNorm outputs are never written in fp32; the residual-adding GEMMs and
   // the embedding pool re-normalise on the fly from per-row (mean, rstd) (bit-identical values).
-  // SSE_NO_LNFOLD=1 restores the materialised flow (A/B and equality tests).
-  const char* nlf = getenv("SSE_NO_LNFOLD");
-  const bool lnfold = sizeof(T) == 2 && !c.stable_layer_norm && !(nlf && nlf[0] == '1');
+  // OPT_NO_LNFOLD restores the materialised flow (A/B and equality tests).
+  const bool lnfold = sizeof(T) == 2 && !c.stable_layer_norm && !sse_opt(OPT_NO_LNFOLD);
   float2* st1 = (float2*)(ws + w.st1);
   float2* st2 = (float2*)(ws + w.st2);
   for (int l = 0; l < c.layers; ++l) {
@@ -723,7 +731,6 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     AttnArgs a{};
     a.qkv = qkv; a.out = ctx; a.T = Tf; a.H = H; a.nh = nh; a.ldq = m->ldq; a.scale = 0.125f;
     a.gconst = m->ptr<float>(Lw.g_const); a.relb = m->ptr<float>(m->relb); a.maxd = MAXD;
-    if (Tf > MAXD) return SSE_ERR_UNSUPPORTED;
     RC(prof(m, s, "attn", 4.0 * B * (double)Tf * Tf * H, (double)B * Tf * (4.0 * H + 8.0 * nh) * sizeof(T),
             [&] { return launch_attention<T>(a, B, s); }));
     g = GemmArgs{};
@@ -970,6 +977,18 @@ int hs_frames(const sse_model* m, int L) {
 extern "C" {
 
 const char* sse_version(void) { return SSE_VERSION; }
+
+int sse_set_option(const char* name, int value) {
+  for (int i = 0; name && i < OPT_COUNT; ++i)
+    if (!std::strcmp(name, g_opt_name[i])) return __atomic_exchange_n(&g_opt[i], value, __ATOMIC_RELAXED);
+  return SSE_ERR_INVALID;
+}
+
+int sse_get_option(const char* name) {
+  for (int i = 0; name && i < OPT_COUNT; ++i)
+    if (!std::strcmp(name, g_opt_name[i])) return sse_opt(i);
+  return SSE_ERR_INVALID;
+}
 
 const char* sse_strerror(int err) {
   switch (err) {

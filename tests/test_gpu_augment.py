@@ -140,3 +140,29 @@ def test_apply_data_augmentation_matches_sequential(tmp_path):
     m3, e3 = apply_data_augmentation(meta, emb6, model, fe, "cuda:0", names, "wavlm", augmentation_factor=3,
                                      minority_threshold=3, rng=random.Random(999), seed=9, cache=cache)
     assert e3["layer_6"].shape == (11, 768) and m3["filename"].equals(m2["filename"])
+
+
+def test_apply_data_augmentation_drops_only_failing_clips(tmp_path):
+    """A minority clip shorter than WavLM's receptive field (300 < 400 samples) fails to embed; the
+    batched path retries its batch one clip at a time and drops only that clip's augmented copies,
+    like the reference's per-sample try/except (REF/model_training_1.py:379-419).  Also: the
+    variant-"01" defaults (augmentation_factor 3, minority_threshold 100, REF/model_training_01.py:291)."""
+    from ssr_amd import config as C, synth
+    from ssr_amd.augment import apply_data_augmentation
+    from ssr_amd.hf import Wav2Vec2FeatureExtractor, WavLMModel
+    lens = [16000, 300, 16000, 24000]
+    rows = []
+    for i, L in enumerate(lens):
+        p = str(tmp_path / f"g{i}.wav")
+        write_wav(p, synth.synth_clips(1, L, seed=70 + i)[0], fmt="float")
+        rows.append({"filename": f"g{i}", "path": p, "label": "rare" if i < 3 else "common"})
+    meta = pd.DataFrame(rows)
+    model = WavLMModel.from_state_dict(C.WAVLM_BASE, synth.synth_wavlm_state_dict(C.WAVLM_BASE), "cuda:0", "bf16")
+    fe = Wav2Vec2FeatureExtractor(do_normalize=False, device="cuda:0")
+    emb = {"layer_12": np.zeros((4, 768), np.float32)}
+    m2, e2 = apply_data_augmentation(meta, emb, model, fe, "cuda:0", ["layer_12"], "wavlm",
+                                     rng=random.Random(3), seed=1, variant="01")
+    # both classes are below 100 -> augmented x3 each; the 300-sample clip's 3 copies are dropped
+    names = list(m2["filename"][4:])
+    assert len(names) == 3 * 3 and not any(n.startswith("g1_aug") for n in names), names
+    assert e2["layer_12"].shape == (4 + 9, 768) and np.isfinite(e2["layer_12"]).all()

@@ -50,11 +50,12 @@ def test_gemm_rejects_bad_shapes():
 
 @pytest.mark.parametrize("M,N,K", [(4099, 512, 768), (8192, 768, 3072), (4100, 2560, 136), (4133, 768, 64),
                                    (5000, 256, 128), (6000, 512, 192), (4096, 256, 256)])
-def test_gemm_tile_configs_agree(monkeypatch, M, N, K):
-    """The default (8-phase ping-pong 256x256 where it applies), the 128x128 tile (SSE_GEMM_CFG=1),
-    the 256x128 3-stage ring (SSE_GEMM_CFG=2) and the 2-stage 256x256 kernel (SSE_GEMM_CFG=3) accumulate every output
+def test_gemm_tile_configs_agree(M, N, K):
+    """The default (8-phase ping-pong 256x256 where it applies), the 128x128 tile (gemm_cfg=1),
+    the 256x128 3-stage ring (gemm_cfg=2) and the 2-stage 256x256 kernel (gemm_cfg=3) accumulate every output
     in the same K order: results are bit-identical (K-tile counts 1, 2, 3, 4, 12, 48 cover the
     8-phase prologue / steady / tail paths)."""
+    from ssr_amd import _lib
     from ssr_amd.model import gemm
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
@@ -62,9 +63,9 @@ def test_gemm_tile_configs_agree(monkeypatch, M, N, K):
     bias = torch.randn(N, device="cuda", generator=g)
     resid = torch.randn(M, N, device="cuda", generator=g)
     outs = []
-    for cfg in ("0", "1", "2", "3"):
-        monkeypatch.setenv("SSE_GEMM_CFG", cfg)
-        outs.append(gemm(a, b, bias, resid, None))
+    for cfg in (0, 1, 2, 3):
+        with _lib.option("gemm_cfg", cfg):
+            outs.append(gemm(a, b, bias, resid, None))
     ref = _ref(a, b, bias, resid, None)
     for o in outs:
         assert ((o - ref).norm() / ref.norm()).item() <= 1e-5
@@ -110,11 +111,11 @@ def test_fast_gelu_pointwise():
 @pytest.mark.parametrize("M,N,K", [(16421, 1024, 64), (16421, 1024, 128), (16421, 768, 192), (16384, 1024, 256),
                                    (16421, 1024, 768), (9000, 2560, 768), (300, 512, 512)])
 @pytest.mark.parametrize("epi", ["plain", "bias_gelu_fast", "bias_f32_and_bf16"])
-def test_gemm_persistent_agrees(monkeypatch, M, N, K, epi):
+def test_gemm_persistent_agrees(M, N, K, epi):
     """The persistent 8-phase kernel (default for GEMMs without a residual: blocks walk several
     tiles, the next tile's prologue is issued before this tile's stores, which stay in flight)
-    against the non-persistent kernel (SSE_GEMM_PERSIST=0) and the 2-stage kernel
-    (SSE_GEMM_CFG=3): bit-identical.  Tile counts above the CU count, ragged M, K-tile counts
+    against the non-persistent kernel (gemm_nonpersist=1) and the 2-stage kernel
+    (gemm_cfg=3): bit-identical.  Tile counts above the CU count, ragged M, K-tile counts
     1, 2, 3, 4, 12 and every output combination."""
     from ssr_amd.model import gemm
     from ssr_amd import _lib
@@ -137,13 +138,10 @@ def test_gemm_persistent_agrees(monkeypatch, M, N, K, epi):
         return cf, ct
 
     outs = []
-    for env in ({}, {"SSE_GEMM_PERSIST": "0"}, {"SSE_GEMM_CFG": "3"}):
-        for k in ("SSE_GEMM_PERSIST", "SSE_GEMM_CFG"):
-            monkeypatch.delenv(k, raising=False)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        outs.append(run())
-        torch.cuda.synchronize()
+    for name, v in (("gemm_cfg", 0), ("gemm_nonpersist", 1), ("gemm_cfg", 3)):
+        with _lib.option(name, v):
+            outs.append(run())
+            torch.cuda.synchronize()
     ref = _ref(a, b, bias, None, "gelu" if act else None)
     assert ((outs[0][0].float() - ref).norm() / ref.norm()).item() <= 5e-3
     for o in outs[1:]:

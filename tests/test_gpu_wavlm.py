@@ -137,10 +137,10 @@ def test_wavlm_large_matches_reference(dtype, tol):
     assert rel.max() <= tol and _cos(got, g["emb"]).min() >= BF16_COS
 
 
-def test_bf16_lnfold_bit_identical(monkeypatch, wavlm_sd):
+def test_bf16_lnfold_bit_identical(wavlm_sd):
     """The bf16 post-LN path never writes LayerNorm outputs in fp32: the residual GEMMs and the
     pool re-normalise from per-row (mean, rstd).  It must reproduce the materialised flow
-    (SSE_NO_LNFOLD=1) bit for bit, pooled embeddings and every hidden state."""
+    (no_lnfold=1) bit for bit, pooled embeddings and every hidden state."""
     from ssr_amd import config as C, synth
     from ssr_amd.model import SSEModel
     m = SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype="bf16")
@@ -148,18 +148,19 @@ def test_bf16_lnfold_bit_identical(monkeypatch, wavlm_sd):
     idx = list(range(13))
     a = m.embed(w, idx).clone()
     ha = [h.clone() for h in m.hidden_states(w[:2])]
-    monkeypatch.setenv("SSE_NO_LNFOLD", "1")
-    b = m.embed(w, idx)
-    hb = m.hidden_states(w[:2])
+    from ssr_amd import _lib
+    with _lib.option("no_lnfold", 1):
+        b = m.embed(w, idx)
+        hb = m.hidden_states(w[:2])
     assert torch.equal(a, b)
     for x, y in zip(ha, hb):
         assert torch.equal(x, y)
 
 
 @pytest.mark.parametrize("n_clips,samples", [(7, 48000), (2, 16000), (3, 80000)])
-def test_bf16_posconv_kernel_matches_grouped_gemm(monkeypatch, wavlm_sd, n_clips, samples):
+def test_bf16_posconv_kernel_matches_grouped_gemm(wavlm_sd, n_clips, samples):
     """The dedicated positional-conv kernel (input window staged once per block, kernels_posconv.hip)
-    against the grouped-GEMM path it replaces (SSE_POSCONV_GEMM=1), on hidden_states[0] (the
+    against the grouped-GEMM path it replaces (posconv_gemm=1), on hidden_states[0] (the
     layer right after it) and the pooled layers: same math, fp32 accumulation in another order.
     Odd clip counts (the second clip of the last block is empty) and T = 49 / 149 / 249 frames."""
     from ssr_amd import config as C, synth
@@ -169,18 +170,19 @@ def test_bf16_posconv_kernel_matches_grouped_gemm(monkeypatch, wavlm_sd, n_clips
     idx = [0, 6, 12]
     a = m.embed(w, idx).cpu().numpy()
     h0 = m.hidden_states(w[:1])[0].cpu().numpy()
-    monkeypatch.setenv("SSE_POSCONV_GEMM", "1")
-    b = m.embed(w, idx).cpu().numpy()
-    g0 = m.hidden_states(w[:1])[0].cpu().numpy()
+    from ssr_amd import _lib
+    with _lib.option("posconv_gemm", 1):
+        b = m.embed(w, idx).cpu().numpy()
+        g0 = m.hidden_states(w[:1])[0].cpu().numpy()
     assert _rel(h0.reshape(-1), g0.reshape(-1)) <= 1e-5
     assert _rel(a[:, 0], b[:, 0]).max() <= 1e-5
     assert _rel(a, b).max() <= 5e-3
 
 
 @pytest.mark.parametrize("samples", [16000, 20001, 48000])
-def test_bf16_conv0_matrix_core_matches_valu(monkeypatch, wavlm_sd, samples):
+def test_bf16_conv0_matrix_core_matches_valu(wavlm_sd, samples):
     """conv0 + GroupNorm + GELU on the matrix cores (split-bf16 K = 32 MFMA, conv0_mfma_kernel)
-    against the packed-fp32 VALU kernel (SSE_CONV0_VALU=1).  The convolutions agree to ~1e-5 before
+    against the packed-fp32 VALU kernel (conv0_valu=1).  The convolutions agree to ~1e-5 before
     the bf16 output rounding; the rare rounding flips then propagate through six bf16 conv GEMMs like
     any bf16 noise, so the two bf16 paths are compared by their distance to the fp32 path (which
     runs conv0 in fp32 FMAs): the matrix-core path must be no farther from it than the VALU path."""
@@ -194,12 +196,32 @@ def test_bf16_conv0_matrix_core_matches_valu(monkeypatch, wavlm_sd, samples):
     m = SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype="bf16")
     a = m.embed(w, idx).cpu().numpy()
     h0 = m.hidden_states(w[:1])[0].cpu().numpy().reshape(-1)
-    monkeypatch.setenv("SSE_CONV0_VALU", "1")
-    b = m.embed(w, idx).cpu().numpy()
-    g0 = m.hidden_states(w[:1])[0].cpu().numpy().reshape(-1)
+    from ssr_amd import _lib
+    with _lib.option("conv0_valu", 1):
+        b = m.embed(w, idx).cpu().numpy()
+        g0 = m.hidden_states(w[:1])[0].cpu().numpy().reshape(-1)
     e_m, e_v = _rel(h0, h_ref), _rel(g0, h_ref)
     E_m, E_v = _rel(a, ref).max(), _rel(b, ref).max()
     print("hidden_states[0] vs fp32: mfma", e_m, "valu", e_v, "| embeddings: mfma", E_m, "valu", E_v,
           "| mfma vs valu", _rel(h0, g0))
     assert _rel(h0, g0) <= 1e-2
     assert e_m <= 1.25 * e_v and E_m <= 1.25 * E_v + 1e-3
+
+
+@pytest.mark.parametrize("dtype,tol", [("fp32", FP32_TOL), ("bf16", BF16_TOL)])
+def test_clip_longer_than_bias_table(dtype, tol, wavlm_sd):
+    """A clip of 4124 frames (> the 4095-distance relative-position table, ~82.5 s): the kernels
+    clamp |key - query| to the table edge, exact because the bucket saturates at max_distance = 800
+    (HF _relative_positions_bucket); the reference embeds any length (REF/WavLM_embeddings.py:297-307)."""
+    from oracle.wavlm import WavLMOracle
+    from ssr_amd import config as C, synth
+    from ssr_amd.model import SSEModel
+    L = 320 * 4124 + 80
+    assert C.WAVLM_BASE.frames(L) == 4124
+    clip = synth.synth_clips(1, L, seed=4124)
+    m = SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype=dtype)
+    got = m.embed(torch.from_numpy(clip).cuda(), [12, 6, 0]).cpu().numpy()
+    ref = WavLMOracle(C.WAVLM_BASE, wavlm_sd).embed(clip, [12, 6, 0])
+    rel = _rel(got, ref).max()
+    print(dtype, "T=4124 rel-L2", rel)
+    assert rel <= tol

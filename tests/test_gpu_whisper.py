@@ -167,3 +167,41 @@ def test_whisper_large_v2_embed():
         print(dtype, "whisper-large-v2+decoder enc rel", re, "dec rel", rd)
         assert re <= tol and rd <= tol
         del m
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("dtype,B,tol,cos_min", [("bf16", 64, 3e-2, 0.999), ("fp8", 128, 0.12, 0.99)])
+def test_whisper_large_v2_bench_batch(dtype, B, tol, cos_min):
+    """The bench shapes themselves (BASELINE configs[2]: bf16 B = 64 x 30 s; configs[4]: fp8
+    B = 128 x 30 s): M = B*1500 = 96k / 192k GEMM rows, the flash-attention grid at B*20 heads.
+    Property: clip i alone == clip i inside the full batch, bit for bit (no cross-clip reduction).
+    Parity: the reference fixture's clip (3 s, zero-padded to 30 s exactly as the feature extractor
+    pads, HF/models/whisper/feature_extraction_whisper.py:300-307) placed at two batch positions."""
+    p = os.path.join(GOLDEN, "whisper_large_v2.npz")
+    if not os.path.exists(p):
+        pytest.skip("large-v2 fixture not generated")
+    from ssr_amd import config as C, synth
+    from ssr_amd.model import SSEModel
+    g = np.load(p)
+    idx = [int(i) for i in g["layer_indices"]]
+    m = SSEModel(C.WHISPER_LARGE_V2, synth.synth_whisper_state_dict(C.WHISPER_LARGE_V2, seed=11), device="cuda:0",
+                 dtype=dtype)
+    clips = synth.synth_clips(B, 480000, seed=31)
+    fix = _clips(None, [3.0])[0]
+    pos = [5, B - 1]
+    for q in pos:
+        clips[q] = 0.0
+        clips[q, :fix.shape[0]] = fix
+    w = torch.from_numpy(clips).cuda()
+    full = m.embed(w, idx)
+    assert torch.isfinite(full).all()
+    for i in (0, 5, B // 2, B - 1):
+        one = m.embed(w[i:i + 1], idx)
+        assert torch.equal(full[i:i + 1], one), i
+    got = full.cpu().numpy()
+    for q in pos:
+        rel = _rel(got[q], g["emb"][0]).max()
+        cos = ((got[q] * g["emb"][0]).sum(-1) / (np.linalg.norm(got[q], axis=-1) *
+                                                  np.linalg.norm(g["emb"][0], axis=-1))).min()
+        print(dtype, B, "pos", q, "rel-L2", rel, "cos", cos)
+        assert rel <= tol and cos >= cos_min

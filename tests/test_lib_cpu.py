@@ -76,3 +76,16 @@ def test_ssemodel_refuses_cpu_device(wavlm_sd):
     from ssr_amd.model import SSEModel
     with pytest.raises(ValueError):
         SSEModel(C.WAVLM_BASE, wavlm_sd, device="cpu")
+
+
+def test_options_are_explicit_only():
+    """A/B kernel switches exist only through sse_set_option (the library reads no environment)."""
+    from ssr_amd import _lib
+    L = _lib.lib()
+    for name in (b"gemm_cfg", b"gemm_nonpersist", b"gelu_exact", b"conv0_valu", b"posconv_gemm", b"no_lnfold",
+                 b"gemm_mx_staged"):
+        assert L.sse_get_option(name) == 0
+        with _lib.option(name.decode(), 1):
+            assert L.sse_get_option(name) == 1
+        assert L.sse_get_option(name) == 0
+    assert L.sse_set_option(b"no_such_switch", 1) < 0

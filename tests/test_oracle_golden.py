@@ -125,3 +125,17 @@ def test_whisper_decoder_oracle_vs_reference(golden_manifest):
         enc, dec = o.embed_both(c[None], enc_idx, dec_idx)
         assert _rel(enc[0], g["emb"][i]).max() <= ORACLE_TOL
         assert _rel(dec[0], g["dec_emb"][i]).max() <= ORACLE_TOL
+
+
+def test_aten_restatement_matches_reference(wavlm_clips, wavlm_sd, golden_wavlm):
+    """bench.py's cpu_baseline (oracle/wavlm_aten.py: the reference's batch-1 loop on the same ATen
+    ops) reproduces the reference's own fixture, with and without do_normalize."""
+    from oracle.wavlm_aten import WavLMAten
+    from ssr_amd import config as C
+    o = WavLMAten(C.WAVLM_BASE, wavlm_sd)
+    idx = [int(i) for i in golden_wavlm["layer_indices"]]
+    for norm, n in ((0, 4), (1, 4)):
+        got = o.embed(wavlm_clips[:n], idx, do_normalize=bool(norm))
+        ref = golden_wavlm[f"emb_norm{norm}"][:n]
+        rel = np.linalg.norm(got - ref, axis=-1) / np.linalg.norm(ref, axis=-1)
+        assert rel.max() <= 1e-5, (norm, rel.max())

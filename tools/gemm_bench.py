@@ -4,6 +4,7 @@ import importlib, os, sys, json
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 importlib.import_module("stuttering-speech-representation_amd")
+from ssr_amd import _lib
 from ssr_amd.model import gemm
 
 SHAPES = {"qkv": (38144, 2432, 768, None), "oproj": (38144, 768, 768, "res"), "ffn1": (38144, 3072, 768, "gelu"),
@@ -11,7 +12,7 @@ SHAPES = {"qkv": (38144, 2432, 768, None), "oproj": (38144, 768, 768, "res"), "f
 cfgs = sys.argv[1:] or ["0"]
 res = {}
 for cfg, (name, (M, N, K, epi)) in [(c, kv) for kv in SHAPES.items() for c in cfgs]:
-    os.environ["SSE_GEMM_CFG"] = cfg
+    _lib.lib().sse_set_option(b"gemm_cfg", int(cfg))
     if name == "qkv":
         N = 2560      # ldq padded to 256 (sse_model.hip build_wavlm)
     a = torch.randn(M, K, device="cuda").bfloat16()

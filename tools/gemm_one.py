@@ -5,11 +5,12 @@ import importlib, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 importlib.import_module("stuttering-speech-representation_amd")
+from ssr_amd import _lib
 from ssr_amd.model import gemm
 
 M, N, K = (int(v) for v in sys.argv[1:4])
 epi, cfg, reps = sys.argv[4], sys.argv[5], int(sys.argv[6])
-os.environ["SSE_GEMM_CFG"] = cfg
+_lib.lib().sse_set_option(b"gemm_cfg", int(cfg))
 g = torch.Generator(device="cuda").manual_seed(1)
 a = (2 * torch.rand(M, K, device="cuda", generator=g) - 1).bfloat16()
 b = ((2 * torch.rand(N, K, device="cuda", generator=g) - 1) / K ** 0.5).bfloat16()
