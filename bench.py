@@ -378,7 +378,7 @@ def main():
                 rf["traffic_source"] = src + " (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE, bytes per launch)"
             res["roofline"] = rf
         res["model_flops_frac"] = round(value / world * FLOP_PER_CLIP[a.model] / 1e12 / PEAK_TFLOPS[a.dtype], 4)
-        ncpu = a.cpu_sample if a.cpu_sample is not None else (64 if wavlm else 2)   # ~10-30 s of CPU work
+        ncpu = a.cpu_sample if a.cpu_sample is not None else (256 if wavlm else 2)   # ~10-30 s of CPU work
         if world == 1 and ncpu > 0:
             res["cpu_baseline"] = cpu_baseline(a.model, ncpu, secs)
         print(json.dumps(res), flush=True)
