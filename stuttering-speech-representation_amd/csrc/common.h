@@ -166,7 +166,44 @@ struct GemmArgs {
   const unsigned char* a_scale;
   const unsigned char* b_scale;
   unsigned char* c_scale;
+  // Folded LayerNorm (post-LN bf16 path, no LayerNorm kernel): A holds bf16 of the UN-normalised
+  // rows x and B = W diag(ln_w) (bf16); the epilogue forms LN(x) W^T + b as
+  //   rstd_m * (acc - mean_m * acol[n]) + bias[n],   acol[n] = sum_k B[n][k],  bias = b + W ln_b,
+  // with (mean_m, rstd_m) combined from the per-256-column partials apart[m][apart_nt] (ln_part_stats).
+  const float2* apart;
+  int apart_nt;
+  const float* acol;
+  // residual LayerNorm from partials rpart[m][rpart_nt] (instead of rstats), affine rln_w / rln_b
+  const float2* rpart;
+  int rpart_nt;
+  float ln_eps;
+  // partials of the fp32 rows this GEMM writes (Cf): opart[m][N / 256] = (mean, M2) over each
+  // 256-column tile (residual GEMMs of the folded path)
+  float2* opart;
 };
+
+// (mean, rstd) of a row of 256 * nt values from its per-tile partials (mean_t, M2_t), Chan's pairwise
+// combination: mean = avg mean_t, M2 = sum M2_t + 256 sum (mean_t - mean)^2, rstd = 1 / sqrt(M2 / n + eps)
+SSE_DEV float2 ln_part_stats(const float2* __restrict__ part, int nt, long long m, float eps) {
+  const float2* p = part + m * nt;
+  float2 v[8];
+  float mean = 0.f;
+  #pragma unroll
+  for (int t = 0; t < 8; ++t)
+    if (t < nt) {
+      v[t] = p[t];
+      mean += v[t].x;
+    }
+  mean /= (float)nt;
+  float m2 = 0.f;
+  #pragma unroll
+  for (int t = 0; t < 8; ++t)
+    if (t < nt) {
+      const float d = v[t].x - mean;
+      m2 += v[t].y + 256.f * d * d;
+    }
+  return make_float2(mean, 1.0f / sqrtf(m2 / (float)(256 * nt) + eps));
+}
 
 // ---- MX-fp8 scale layouts (both operands: K-tiles of 128, one E8M0 byte per 32-element block) ----
 // The 8-phase MX GEMM stages, per 256-row (column) tile and K-tile, one 1 KiB scale block by

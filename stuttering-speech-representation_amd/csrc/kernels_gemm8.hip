@@ -390,8 +390,9 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
   constexpr int CH = 128 * 256 / 4;
   constexpr int UNR = 4;
   const bool has_bias = g.bias != nullptr, has_res = g.resid != nullptr, gelu = g.act == ACT_GELU, gelu_fast = g.act == ACT_GELU_FAST;
-  #pragma unroll
-  for (int mi = 0; mi < 2; ++mi) {
+  // compile-time mi / it (g8_sfor): acc[mi] and the MX scale words must stay in registers
+  g8_sfor<0, 2>([&](auto mic) {
+    constexpr int mi = decltype(mic)::value;
     __syncthreads();
     #pragma unroll
     for (int ni = 0; ni < 2; ++ni)
@@ -407,39 +408,54 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
     // (bias, LayerNorm w/b of the residual) are loaded once, only rows vary
     const int cc = (threadIdx.x & 63) * 4, n = n0 + cc;
     const f32x4 bv = has_bias ? *(const f32x4*)(g.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 lw = f32x4{1.f, 1.f, 1.f, 1.f}, lb = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (g.rstats) {
+    const bool rln = g.rstats || g.rpart, fold = g.apart != nullptr;
+    f32x4 lw = f32x4{1.f, 1.f, 1.f, 1.f}, lb = f32x4{0.f, 0.f, 0.f, 0.f}, ac = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (rln) {
       lw = *(const f32x4*)(g.rln_w + n);
       lb = *(const f32x4*)(g.rln_b + n);
     }
+    if (fold) ac = *(const f32x4*)(g.acol + n);
     // MX-fp8 out: E8M0 bytes of this thread's 16 rows (w + 8k, k = 0..15: r16 = w + 8(k&1), i = (k>>1)&3,
     // wm = k>>3) gathered into the 4 scale dwords of the A layout, stored after the half
     unsigned scw[2][2] = {{0u, 0u}, {0u, 0u}};
-    #pragma unroll
-    for (int it = 0; it < CH / (512 * UNR); ++it) {
+    g8_sfor<0, CH / (512 * UNR)>([&](auto itc) {
+      constexpr int it = decltype(itc)::value;
       const int base = threadIdx.x + it * 512 * UNR;
       f32x4 v[UNR], rv[UNR];
-      float2 st[UNR];
+      float2 st[UNR], ast[UNR];
       long long off[UNR];
+      int mrow[UNR];
       bool ok[UNR];
       #pragma unroll
       for (int u = 0; u < UNR; ++u) {
-        const int row = (base + u * 512) >> 6;
+        const int row = (base + u * 512) >> 6;   // uniform over the wave: one wave = one 256-column row
         const int m = m0 + mi * 128 + row;
         ok[u] = m < M;
-        off[u] = (long long)(ok[u] ? m : 0) * g.ldc + n;
+        const int mc = ok[u] ? m : 0;
+        mrow[u] = mc;
+        off[u] = (long long)mc * g.ldc + n;
         v[u] = *(const f32x4*)(Cs + row * G8_CLD + cc);
         rv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
         st[u] = make_float2(0.f, 1.f);
+        ast[u] = make_float2(0.f, 1.f);
         if (has_res) {
-          const long long ro = g.resid_rows ? (long long)((ok[u] ? m : 0) % g.resid_rows) * g.ldc + n : off[u];
+          const long long ro = g.resid_rows ? (long long)(mc % g.resid_rows) * g.ldc + n : off[u];
           rv[u] = g8_ld<NT>((const f32x4*)(g.resid + ro));
-          if (g.rstats) st[u] = g.rstats[ok[u] ? m : 0];
+          if (g.rstats) st[u] = g.rstats[mc];
+          else if (g.rpart) st[u] = ln_part_stats(g.rpart, g.rpart_nt, mc, g.ln_eps);
         }
+        if (fold) ast[u] = ln_part_stats(g.apart, g.apart_nt, mc, g.ln_eps);
       }
       #pragma unroll
       for (int u = 0; u < UNR; ++u) {
-        f32x4 o = v[u] + bv;
+        f32x4 o;
+        if (fold) {   // LN(x) W^T + b = rstd (acc - mean acol) + b
+          const float nm = -ast[u].x * ast[u].y;
+          #pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = fmaf(v[u][e], ast[u].y, fmaf(nm, ac[e], bv[e]));
+        } else {
+          o = v[u] + bv;
+        }
         if (gelu) {
           const f32x2 lo = gelu_erf2(f32x2{o[0], o[1]}), hi = gelu_erf2(f32x2{o[2], o[3]});
           o = f32x4{lo.x, lo.y, hi.x, hi.y};
@@ -449,11 +465,18 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
           o = f32x4{lo.x, lo.y, hi.x, hi.y};
         }
         f32x4 r = rv[u];
-        if (g.rstats) {   // LayerNorm of the residual, the exact expression of layernorm_kernel
+        if (rln) {   // LayerNorm of the residual, the exact expression of layernorm_kernel
           #pragma unroll
           for (int e = 0; e < 4; ++e) r[e] = fmaf((r[e] - st[u].x) * st[u].y, lw[e], lb[e]);
         }
         o += r;
+        if (g.opart) {   // (mean, M2) of this row's 256 columns, two-pass over the wave's registers
+          const float mt = wave_sum_fast(o[0] + o[1] + o[2] + o[3]) * (1.0f / 256.0f);
+          const f32x4 d = o - mt;
+          const float m2 = wave_sum_fast(d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3]);
+          if (ok[u] && (threadIdx.x & 63) == 0)
+            g.opart[(long long)mrow[u] * (g.N >> 8) + (n0 >> 8)] = make_float2(mt, m2);
+        }
         if (MX && g.c_scale) {
           // MX-fp8 out: the wave holds one row's 256 columns, 8 lanes = one 32-column block
           const float a = max8_dpp(fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
@@ -474,7 +497,7 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
           }
         }
       }
-    }
+    });
     if (MX && g.c_scale && (threadIdx.x & 7) == 0) {
       const int w = threadIdx.x >> 6;
       #pragma unroll
@@ -483,7 +506,7 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
         for (int wq = 0; wq < 2; ++wq)
           *(unsigned*)(g.c_scale + mx_a_scale_off(m0 + mi * 128 + wq * 64 + w + 8 * h8, n >> 5, g.N >> 7)) = scw[h8][wq];
     }
-  }
+  });
 }
 
 
@@ -518,7 +541,8 @@ SSE_DEV int g8p_tile(int b, int r, int G, int n_tiles) {
 template <bool RES, bool Q8>
 SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, int n0, int wm, int wn,
                                 int q, int r16) {
-  const bool has_bias = g.bias != nullptr, has_res = RES && g.resid != nullptr, ln = RES && g.rstats != nullptr;
+  const bool has_bias = g.bias != nullptr, has_res = RES && g.resid != nullptr;
+  const bool ln = RES && (g.rstats != nullptr || g.rpart != nullptr), fold = !RES && g.apart != nullptr;
   const bool gelu = g.act == ACT_GELU, gelu_fast = g.act == ACT_GELU_FAST;
   f32x4 bv[2][2], lw[2][2], lb[2][2];
   #pragma unroll
@@ -527,8 +551,18 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
     for (int j = 0; j < 2; ++j) {
       const int n = n0 + ni * 128 + wn * 32 + j * 16 + q * 4;
       bv[ni][j] = has_bias ? *(const f32x4*)(g.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-      lw[ni][j] = ln ? *(const f32x4*)(g.rln_w + n) : f32x4{1.f, 1.f, 1.f, 1.f};
+      // folded LayerNorm of A: lw holds acol (the column sums of the folded weight)
+      lw[ni][j] = ln ? *(const f32x4*)(g.rln_w + n) : (fold ? *(const f32x4*)(g.acol + n) : f32x4{1.f, 1.f, 1.f, 1.f});
       lb[ni][j] = ln ? *(const f32x4*)(g.rln_b + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  // folded LayerNorm: (mean, rstd) of this lane's 8 rows m0 + mi*128 + wm*64 + i*16 + r16
+  float2 ast[2][4];
+  #pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + mi * 128 + wm * 64 + i * 16 + r16;
+      ast[mi][i] = fold ? ln_part_stats(g.apart, g.apart_nt, m < g.M ? m : 0, g.ln_eps) : make_float2(0.f, 1.f);
     }
   f32x4 rv[4][2][2];
   float2 st[4];
@@ -544,7 +578,7 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
         #pragma unroll
         for (int j = 0; j < 2; ++j)
           rv[i][ni][j] = *(const f32x4*)(g.resid + rrow + n0 + ni * 128 + wn * 32 + j * 16 + q * 4);
-      st[i] = ln ? g.rstats[mc] : make_float2(0.f, 1.f);
+      st[i] = !ln ? make_float2(0.f, 1.f) : (g.rstats ? g.rstats[mc] : ln_part_stats(g.rpart, g.rpart_nt, mc, g.ln_eps));
     }
   };
   auto finish_half = [&](int mi) {   // acc[mi] <- bias, activation, (LayerNorm'd) residual
@@ -554,7 +588,14 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
       for (int ni = 0; ni < 2; ++ni)
         #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          f32x4 o = acc[mi][ni][i][j] + bv[ni][j];
+          f32x4 o;
+          if (fold) {   // LN(x) W^T + b = rstd (acc - mean acol) + b
+            const float nm = -ast[mi][i].x * ast[mi][i].y;
+            #pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = fmaf(acc[mi][ni][i][j][e], ast[mi][i].y, fmaf(nm, lw[ni][j][e], bv[ni][j][e]));
+          } else {
+            o = acc[mi][ni][i][j] + bv[ni][j];
+          }
           if (gelu) {
             const f32x2 lo = gelu_erf2(f32x2{o[0], o[1]}), hi = gelu_erf2(f32x2{o[2], o[3]});
             o = f32x4{lo.x, lo.y, hi.x, hi.y};

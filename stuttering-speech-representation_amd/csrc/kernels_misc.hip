@@ -744,18 +744,20 @@ int launch_mx_quantize(const float* x, int R, int K, int role, unsigned char* q,
 __global__ __launch_bounds__(256) void pool_mean_kernel(const float* __restrict__ x, int T, int H,
                                                         float* __restrict__ out, long long out_stride,
                                                         const float2* __restrict__ st, const float* __restrict__ w,
-                                                        const float* __restrict__ bb) {
+                                                        const float* __restrict__ bb, const float2* __restrict__ lpart,
+                                                        int nt, float eps) {
   __shared__ double part[4][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int n = blockIdx.x * 64 + lane, b = blockIdx.y;
   double s = 0.0;
   if (n < H) {
     const float* xb = x + (long long)b * T * H + n;
-    const float wn = st ? w[n] : 1.f, bn = st ? bb[n] : 0.f;
+    const bool ln = st || lpart;
+    const float wn = ln ? w[n] : 1.f, bn = ln ? bb[n] : 0.f;
     for (int t = wv; t < T; t += 4) {
       float v = xb[(long long)t * H];
-      if (st) {
-        const float2 q = st[(long long)b * T + t];
+      if (ln) {
+        const float2 q = st ? st[(long long)b * T + t] : ln_part_stats(lpart, nt, (long long)b * T + t, eps);
         v = fmaf((v - q.x) * q.y, wn, bn);
       }
       s += v;
@@ -767,8 +769,9 @@ __global__ __launch_bounds__(256) void pool_mean_kernel(const float* __restrict_
 }
 
 int launch_pool_mean(const float* x, int B, int T, int H, float* out, long long out_stride, hipStream_t s,
-                     const float2* st, const float* w, const float* b) {
-  hipLaunchKernelGGL(pool_mean_kernel, dim3((H + 63) / 64, B), dim3(256), 0, s, x, T, H, out, out_stride, st, w, b);
+                     const float2* st, const float* w, const float* b, const float2* part, int nt, float eps) {
+  hipLaunchKernelGGL(pool_mean_kernel, dim3((H + 63) / 64, B), dim3(256), 0, s, x, T, H, out, out_stride, st, w, b,
+                     part, nt, eps);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -41,6 +41,13 @@ namespace {
 // _relative_positions_bucket: every |d| >= max_distance maps to the last bucket of its sign)
 constexpr int MAXD = 4095;
 
+inline float bf_bits2f(uint16_t h) {
+  const uint32_t u = (uint32_t)h << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
 inline uint16_t f2bf_bits(float f) {
   uint32_t u;
   std::memcpy(&u, &f, 4);
@@ -142,10 +149,37 @@ struct Arena {
   }
 };
 
+// LayerNorm folded into the GEMM that consumes its output: B' = W diag(lw) (bf16), acol[n] = sum_k
+// bf16(B'[n][k]) (the operand values the MFMAs multiply), bias'[n] = bias[n] + sum_k W[n][k] lb[k]
+void put_folded(Arena& ar, const float* W, const float* bias, int N, int K, const float* lw, const float* lb,
+                size_t* w_off, size_t* c_off, size_t* b_off) {
+  std::vector<uint16_t> wf((size_t)N * K);
+  std::vector<float> cs(N), bf(N);
+  for (int n = 0; n < N; ++n) {
+    double c = 0.0, d = bias ? (double)bias[n] : 0.0;
+    for (int k = 0; k < K; ++k) {
+      const float w = W[(size_t)n * K + k];
+      const uint16_t h = f2bf_bits(w * lw[k]);
+      wf[(size_t)n * K + k] = h;
+      c += (double)bf_bits2f(h);
+      d += (double)w * (double)lb[k];
+    }
+    cs[n] = (float)c;
+    bf[n] = (float)d;
+  }
+  *w_off = ar.put(wf.data(), wf.size() * 2);
+  *c_off = ar.put_f32(cs.data(), N);
+  *b_off = ar.put_f32(bf.data(), N);
+}
+
 struct LayerW {
   size_t qkv_w, qkv_b, o_w, o_b, ln1_w, ln1_b, f1_w, f1_b, f2_w, f2_b, ln2_w, ln2_b;
   size_t g_const, g_w, g_b;   // WavLM gate
   size_t qkv_q, qkv_s, f1_q, f1_s, f2_q, f2_s;   // SSE_DTYPE_FP8: MX-fp8 copies (e4m3 + scales)
+  // folded LayerNorm (bf16 post-LN, common.h GemmArgs.apart): QKV folded with the previous layer's
+  // final LayerNorm (layers >= 1), FFN1 with this layer's attention LayerNorm: weight W diag(ln_w)
+  // (bf16), its column sums acol and bias b + W ln_b
+  size_t qkv_wf, qkv_c, qkv_bf, f1_wf, f1_c, f1_bf;
 };
 
 // Whisper decoder layer for the 1-token pass (HF/models/whisper/modeling_whisper.py:448-506)
@@ -170,6 +204,7 @@ struct sse_model {
   size_t c1_w, c1_b, c2_w, c2_b, positions;
   size_t dec_x0, dec_ln_w, dec_ln_b;   // decoder: embed_tokens[0] + embed_positions[0]; final LN
   std::vector<DecLayerW> dec;
+  bool ln_fold = false;   // folded-LayerNorm weights present (bf16 post-LN WavLM, LayerW.qkv_wf / f1_wf)
   int ldq = 0;   // QKV GEMM width: 3H (+ 8*heads gate columns for WavLM, then zero pad to 256 so the
                 // 256x256 MFMA tile applies)
   std::vector<LayerW> layers;
@@ -274,6 +309,8 @@ int build_wavlm(sse_model* m, Blob& bl, Arena& ar) {
     }
     m->relb = ar.put_f32(tab.data(), tab.size());
   }
+  const bool fold = BF && !c.stable_layer_norm && H % 256 == 0 && H <= 2048;
+  const float *prev_l2w = nullptr, *prev_l2b = nullptr;
   for (int l = 0; l < c.layers; ++l) {
     const float *qw = bl.take((size_t)H * H), *qb = bl.take(H), *kw = bl.take((size_t)H * H), *kb = bl.take(H);
     const float *vw = bl.take((size_t)H * H), *vb = bl.take(H), *ow = bl.take((size_t)H * H), *ob = bl.take(H);
@@ -316,8 +353,15 @@ int build_wavlm(sse_model* m, Blob& bl, Arena& ar) {
     L.f2_b = ar.put_f32(f2b, H);
     L.ln2_w = ar.put_f32(l2w, H);
     L.ln2_b = ar.put_f32(l2b, H);
+    if (fold) {
+      if (l > 0) put_folded(ar, qkv.data(), qkvb.data(), ldq, H, prev_l2w, prev_l2b, &L.qkv_wf, &L.qkv_c, &L.qkv_bf);
+      put_folded(ar, f1w, f1b, F, H, l1w, l1b, &L.f1_wf, &L.f1_c, &L.f1_bf);
+    }
+    prev_l2w = l2w;
+    prev_l2b = l2b;
     m->layers.push_back(L);
   }
+  m->ln_fold = fold;
   return bl.ok ? SSE_OK : SSE_ERR_WEIGHTS;
 }
 
@@ -500,7 +544,7 @@ int wavlm_frames(const sse_cfg& c, int L, int* Ts) {
 }
 
 struct WavlmWs {
-  size_t zero, norm, part, ss, bufA, bufB, x, xt, xb, qkv, ctx, ff, hf, st1, st2;
+  size_t zero, norm, part, ss, bufA, bufB, x, xt, xb, qkv, ctx, ff, hf, p1, p2;
 };
 
 WavlmWs wavlm_plan(const sse_model* m, int B, int L, Plan& p) {
@@ -530,8 +574,9 @@ WavlmWs wavlm_plan(const sse_model* m, int B, int L, Plan& p) {
   w.ctx = p.add(M * H * es);
   w.ff = p.add(M * (size_t)c.ffn * es);
   w.hf = c.stable_layer_norm ? p.add(M * H * 4) : 0;
-  w.st1 = p.add(M * 8);        // per-row LayerNorm (mean, rstd): post-LN bf16 path
-  w.st2 = p.add(M * 8);
+  const size_t nt = H % 256 == 0 ? (size_t)H / 256 : 0;   // folded path: per-256-column partials
+  w.p1 = p.add(M * nt * 8);
+  w.p2 = p.add(M * nt * 8);
   return w;
 }
 
@@ -592,11 +637,13 @@ struct Sink {
     }
     return 0;
   }
-  // hidden state = LayerNorm(x) with per-row stats st already computed (x itself un-normalised)
-  int emit_ln(int idx, const float* x, const float2* st, const float* w, const float* b, float eps) const {
+  // hidden state = LayerNorm(x) with per-row stats st, or per-256-column partials part [rows][nt],
+  // already computed (x itself un-normalised)
+  int emit_ln(int idx, const float* x, const float2* st, const float* w, const float* b, float eps,
+              const float2* part = nullptr, int nt = 0) const {
     for (int i = 0; i < n_ids; ++i)
       if (ids[i] == idx)
-        RC(launch_pool_mean(x, B, T, H, pooled + (size_t)i * H, (long long)n_ids * H, s, st, w, b));
+        RC(launch_pool_mean(x, B, T, H, pooled + (size_t)i * H, (long long)n_ids * H, s, st, w, b, part, nt, eps));
     if (hs)
       RC((launch_layernorm<float, float>(x, w, b, B * T, H, eps, ACT_NONE, hs + (size_t)idx * B * T * H,
                                          (float*)nullptr, s)));
@@ -711,20 +758,29 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
   T* ctx = (T*)(ws + w.ctx);
   T* ff = (T*)(ws + w.ff);
   float* hf = c.stable_layer_norm ? (float*)(ws + w.hf) : nullptr;
-  // bf16 post-LN: LayerNorm outputs are never written in fp32; the residual-adding GEMMs and
-  // the embedding pool re-normalise on the fly from per-row (mean, rstd) (bit-identical values).
-  // OPT_NO_LNFOLD restores the materialised flow (A/B and equality tests).
-  const bool lnfold = sizeof(T) == 2 && !c.stable_layer_norm && !sse_opt(OPT_NO_LNFOLD);
-  float2* st1 = (float2*)(ws + w.st1);
-  float2* st2 = (float2*)(ws + w.st2);
+  // bf16 post-LN (WavLM-base): no LayerNorm kernel inside the layer loop.  The residual GEMMs (oproj,
+  // ffn2) write the un-normalised sum x in fp32 (the residual stream), its bf16 copy into xb (the next
+  // GEMM's A operand) and per-256-column partial statistics (p1 / p2); the consumers apply the
+  // LayerNorm from those partials: QKV / FFN1 through folded weights (GemmArgs.apart:
+  // rstd (acc - mean acol) + b'), the next residual GEMM on its residual load (rpart), the pool on
+  // its loads.  OPT_NO_LNFOLD restores the materialised flow (LayerNorm kernels; A/B tests).
+  const bool lnfold = sizeof(T) == 2 && m->ln_fold && !sse_opt(OPT_NO_LNFOLD);
+  const int nt = H / 256;
+  float2* p1 = (float2*)(ws + w.p1);
+  float2* p2 = (float2*)(ws + w.p2);
   for (int l = 0; l < c.layers; ++l) {
     const LayerW& Lw = m->layers[l];
+    const LayerW* Lp = l > 0 ? &m->layers[l - 1] : nullptr;
     if (c.stable_layer_norm)
       RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, ACT_NONE,
                                      nullptr, xb, s)));
     GemmArgs g{};
     g.A = xb; g.B = m->ptr(Lw.qkv_w); g.M = M; g.N = m->ldq; g.K = H;
     g.rows_per_seg = M; g.lda = H; g.bias = m->ptr<float>(Lw.qkv_b); g.Ct = qkv; g.ldc = m->ldq; g.zero = zero;
+    if (lnfold && l > 0) {   // xb = bf16 of the previous layer's un-normalised sum: its final LN folded
+      g.B = m->ptr(Lw.qkv_wf); g.bias = m->ptr<float>(Lw.qkv_bf); g.acol = m->ptr<float>(Lw.qkv_c);
+      g.apart = p2; g.apart_nt = nt; g.ln_eps = eps;
+    }
     // algorithmic FLOPs count the 3H + 8*heads useful columns, not the zero pad to ldq
     RC(prof(m, s, "gemm:qkv", 2.0 * M * (3.0 * H + 8.0 * nh) * H, gbytes<T>(g),
             [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
@@ -736,33 +792,40 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     g = GemmArgs{};
     g.A = ctx; g.B = m->ptr(Lw.o_w); g.M = M; g.N = H; g.K = H; g.rows_per_seg = M; g.lda = H;
     g.bias = m->ptr<float>(Lw.o_b); g.resid = x; g.Cf = x; g.ldc = H; g.zero = zero;
-    if (lnfold && l > 0) {   // x holds the previous layer's un-normalised sum: LN2 applied here
-      g.rstats = st2; g.rln_w = m->ptr<float>(m->layers[l - 1].ln2_w); g.rln_b = m->ptr<float>(m->layers[l - 1].ln2_b);
+    if (lnfold) {
+      if (l > 0) {   // x holds the previous layer's un-normalised sum: its final LN applied here
+        g.rpart = p2; g.rpart_nt = nt; g.ln_eps = eps;
+        g.rln_w = m->ptr<float>(Lp->ln2_w); g.rln_b = m->ptr<float>(Lp->ln2_b);
+      }
+      g.Ct = xb; g.opart = p1;
     }
     RC(prof(m, s, "gemm:oproj", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
-    if (lnfold) {
-      RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, ACT_NONE,
-                                     nullptr, xb, s, st1)));
-    } else if (!c.stable_layer_norm) {
-      RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, ACT_NONE, x,
-                                     xb, s)));
-    } else {
-      RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, H, eps, ACT_NONE,
-                                     nullptr, xb, s)));
+    if (!lnfold) {
+      if (!c.stable_layer_norm)
+        RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, ACT_NONE, x,
+                                       xb, s)));
+      else
+        RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, H, eps, ACT_NONE,
+                                       nullptr, xb, s)));
     }
     g = GemmArgs{};
     g.A = xb; g.B = m->ptr(Lw.f1_w); g.M = M; g.N = F; g.K = H; g.rows_per_seg = M; g.lda = H;
     g.bias = m->ptr<float>(Lw.f1_b); g.Ct = ff; g.ldc = F; g.act = gelu_rounded_act<T>(); g.zero = zero;
+    if (lnfold) {   // xb = bf16 of the un-normalised attention sum: the attention LN folded
+      g.B = m->ptr(Lw.f1_wf); g.bias = m->ptr<float>(Lw.f1_bf); g.acol = m->ptr<float>(Lw.f1_c);
+      g.apart = p1; g.apart_nt = nt; g.ln_eps = eps;
+    }
     RC(prof(m, s, "gemm:ffn1", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     g = GemmArgs{};
     g.A = ff; g.B = m->ptr(Lw.f2_w); g.M = M; g.N = H; g.K = F; g.rows_per_seg = M; g.lda = F;
     g.bias = m->ptr<float>(Lw.f2_b); g.resid = x; g.Cf = x; g.ldc = H; g.zero = zero;
-    if (lnfold) { g.rstats = st1; g.rln_w = m->ptr<float>(Lw.ln1_w); g.rln_b = m->ptr<float>(Lw.ln1_b); }
+    if (lnfold) {
+      g.rpart = p1; g.rpart_nt = nt; g.ln_eps = eps; g.rln_w = m->ptr<float>(Lw.ln1_w); g.rln_b = m->ptr<float>(Lw.ln1_b);
+      g.Ct = xb; g.opart = p2;
+    }
     RC(prof(m, s, "gemm:ffn2", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     if (lnfold) {
-      RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, H, eps, ACT_NONE,
-                                     nullptr, xb, s, st2)));
-      RC(sink.emit_ln(l + 1, x, st2, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), eps));
+      RC(sink.emit_ln(l + 1, x, nullptr, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), eps, p2, nt));
       continue;
     }
     if (!c.stable_layer_norm) {

@@ -137,24 +137,35 @@ def test_wavlm_large_matches_reference(dtype, tol):
     assert rel.max() <= tol and _cos(got, g["emb"]).min() >= BF16_COS
 
 
-def test_bf16_lnfold_bit_identical(wavlm_sd):
-    """The bf16 post-LN path never writes LayerNorm outputs in fp32: the residual GEMMs and the
-    pool re-normalise from per-row (mean, rstd).  It must reproduce the materialised flow
-    (no_lnfold=1) bit for bit, pooled embeddings and every hidden state."""
-    from ssr_amd import config as C, synth
+def test_bf16_lnfold_matches_materialised(wavlm_sd):
+    """The bf16 post-LN path runs no LayerNorm kernel inside the layer loop: oproj / ffn2 write the
+    un-normalised sum (fp32 residual + bf16 GEMM operand) and per-256-column partial statistics;
+    QKV / FFN1 apply the LayerNorm through folded weights (rstd (acc - mean acol) + b'), the next
+    residual GEMM on its residual load, the pool on its loads.  Against the materialised flow
+    (no_lnfold=1: LayerNorm kernels, bf16(LN(x)) operands): both are bf16 paths with different
+    rounding points, so they are compared by tolerance and by their distance to the fp32 path."""
+    from ssr_amd import _lib, config as C, synth
     from ssr_amd.model import SSEModel
     m = SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype="bf16")
     w = torch.from_numpy(synth.synth_clips(6, 48000, seed=21)).cuda()
     idx = list(range(13))
-    a = m.embed(w, idx).clone()
+    a = m.embed(w, idx).cpu().numpy()
     ha = [h.clone() for h in m.hidden_states(w[:2])]
-    from ssr_amd import _lib
     with _lib.option("no_lnfold", 1):
-        b = m.embed(w, idx)
+        b = m.embed(w, idx).cpu().numpy()
         hb = m.hidden_states(w[:2])
-    assert torch.equal(a, b)
+    m32 = SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype="fp32")
+    r = m32.embed(w, idx).cpu().numpy()
+    e_a, e_b = _rel(a, r).max(), _rel(b, r).max()
+    print("folded vs materialised", _rel(a, b).max(), "| vs fp32: folded", e_a, "materialised", e_b)
+    assert _rel(a, b).max() <= 2e-2
+    assert e_a <= 1.25 * e_b + 1e-3 and e_a <= BF16_TOL
     for x, y in zip(ha, hb):
-        assert torch.equal(x, y)
+        x, y = x.cpu().numpy().reshape(2, -1), y.cpu().numpy().reshape(2, -1)
+        assert _rel(x, y).max() <= 2e-2
+    # the pool's LayerNorm from the GEMM partials == the LayerNorm kernel's own statistics
+    pooled_hs = torch.stack([h.mean(dim=1) for h in ha], dim=1).cpu().numpy()
+    assert _rel(a[:2], pooled_hs).max() <= 1e-5
 
 
 @pytest.mark.parametrize("n_clips,samples", [(7, 48000), (2, 16000), (3, 80000)])
