@@ -182,27 +182,36 @@ struct GemmArgs {
   float2* opart;
 };
 
-// (mean, rstd) of a row of 256 * nt values from its per-tile partials (mean_t, M2_t), Chan's pairwise
-// combination: mean = avg mean_t, M2 = sum M2_t + 256 sum (mean_t - mean)^2, rstd = 1 / sqrt(M2 / n + eps)
-SSE_DEV float2 ln_part_stats(const float2* __restrict__ part, int nt, long long m, float eps) {
-  const float2* p = part + m * nt;
-  float2 v[8];
+// (mean, rstd) of a row of 256 * NT values from its per-tile partials (mean_t, M2_t), Chan's pairwise
+// combination: mean = avg mean_t, M2 = sum M2_t + 256 sum (mean_t - mean)^2, rstd = 1 / sqrt(M2 / n + eps).
+// Branch-free for a compile-time tile count (the folded path is enabled for H / 256 in {2, 3, 4}).
+template <int NT>
+SSE_DEV float2 ln_part_combine(const float2 (&v)[NT], float eps) {
   float mean = 0.f;
   #pragma unroll
-  for (int t = 0; t < 8; ++t)
-    if (t < nt) {
-      v[t] = p[t];
-      mean += v[t].x;
-    }
-  mean /= (float)nt;
+  for (int t = 0; t < NT; ++t) mean += v[t].x;
+  mean *= 1.0f / NT;
   float m2 = 0.f;
   #pragma unroll
-  for (int t = 0; t < 8; ++t)
-    if (t < nt) {
-      const float d = v[t].x - mean;
-      m2 += v[t].y + 256.f * d * d;
-    }
-  return make_float2(mean, 1.0f / sqrtf(m2 / (float)(256 * nt) + eps));
+  for (int t = 0; t < NT; ++t) {
+    const float d = v[t].x - mean;
+    m2 += v[t].y + 256.f * d * d;
+  }
+  return make_float2(mean, 1.0f / sqrtf(m2 * (1.0f / (256 * NT)) + eps));
+}
+template <int NT>
+SSE_DEV float2 ln_part_stats_n(const float2* __restrict__ part, long long m, float eps) {
+  float2 v[NT];
+  #pragma unroll
+  for (int t = 0; t < NT; ++t) v[t] = part[m * NT + t];
+  return ln_part_combine<NT>(v, eps);
+}
+SSE_DEV float2 ln_part_stats(const float2* __restrict__ part, int nt, long long m, float eps) {
+  switch (nt) {
+    case 2: return ln_part_stats_n<2>(part, m, eps);
+    case 4: return ln_part_stats_n<4>(part, m, eps);
+    default: return ln_part_stats_n<3>(part, m, eps);
+  }
 }
 
 // ---- MX-fp8 scale layouts (both operands: K-tiles of 128, one E8M0 byte per 32-element block) ----

@@ -442,9 +442,9 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
           const long long ro = g.resid_rows ? (long long)(mc % g.resid_rows) * g.ldc + n : off[u];
           rv[u] = g8_ld<NT>((const f32x4*)(g.resid + ro));
           if (g.rstats) st[u] = g.rstats[mc];
-          else if (g.rpart) st[u] = ln_part_stats(g.rpart, g.rpart_nt, mc, g.ln_eps);
+          else if (g.rpart) st[u] = ln_part_stats_n<3>(g.rpart, mc, g.ln_eps);
         }
-        if (fold) ast[u] = ln_part_stats(g.apart, g.apart_nt, mc, g.ln_eps);
+        if (fold) ast[u] = ln_part_stats_n<3>(g.apart, mc, g.ln_eps);
       }
       #pragma unroll
       for (int u = 0; u < UNR; ++u) {
@@ -542,7 +542,7 @@ template <bool RES, bool Q8>
 SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, int n0, int wm, int wn,
                                 int q, int r16) {
   const bool has_bias = g.bias != nullptr, has_res = RES && g.resid != nullptr;
-  const bool ln = RES && (g.rstats != nullptr || g.rpart != nullptr), fold = !RES && g.apart != nullptr;
+  const bool ln = RES && (g.rstats != nullptr || g.rpart != nullptr);
   const bool gelu = g.act == ACT_GELU, gelu_fast = g.act == ACT_GELU_FAST;
   f32x4 bv[2][2], lw[2][2], lb[2][2];
   #pragma unroll
@@ -551,18 +551,8 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
     for (int j = 0; j < 2; ++j) {
       const int n = n0 + ni * 128 + wn * 32 + j * 16 + q * 4;
       bv[ni][j] = has_bias ? *(const f32x4*)(g.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-      // folded LayerNorm of A: lw holds acol (the column sums of the folded weight)
-      lw[ni][j] = ln ? *(const f32x4*)(g.rln_w + n) : (fold ? *(const f32x4*)(g.acol + n) : f32x4{1.f, 1.f, 1.f, 1.f});
+      lw[ni][j] = ln ? *(const f32x4*)(g.rln_w + n) : f32x4{1.f, 1.f, 1.f, 1.f};
       lb[ni][j] = ln ? *(const f32x4*)(g.rln_b + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  // folded LayerNorm: (mean, rstd) of this lane's 8 rows m0 + mi*128 + wm*64 + i*16 + r16
-  float2 ast[2][4];
-  #pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
-    #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + mi * 128 + wm * 64 + i * 16 + r16;
-      ast[mi][i] = fold ? ln_part_stats(g.apart, g.apart_nt, m < g.M ? m : 0, g.ln_eps) : make_float2(0.f, 1.f);
     }
   f32x4 rv[4][2][2];
   float2 st[4];
@@ -578,7 +568,7 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
         #pragma unroll
         for (int j = 0; j < 2; ++j)
           rv[i][ni][j] = *(const f32x4*)(g.resid + rrow + n0 + ni * 128 + wn * 32 + j * 16 + q * 4);
-      st[i] = !ln ? make_float2(0.f, 1.f) : (g.rstats ? g.rstats[mc] : ln_part_stats(g.rpart, g.rpart_nt, mc, g.ln_eps));
+      st[i] = !ln ? make_float2(0.f, 1.f) : (g.rstats ? g.rstats[mc] : ln_part_stats_n<3>(g.rpart, mc, g.ln_eps));
     }
   };
   auto finish_half = [&](int mi) {   // acc[mi] <- bias, activation, (LayerNorm'd) residual
@@ -588,14 +578,7 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
       for (int ni = 0; ni < 2; ++ni)
         #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          f32x4 o;
-          if (fold) {   // LN(x) W^T + b = rstd (acc - mean acol) + b
-            const float nm = -ast[mi][i].x * ast[mi][i].y;
-            #pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = fmaf(acc[mi][ni][i][j][e], ast[mi][i].y, fmaf(nm, lw[ni][j][e], bv[ni][j][e]));
-          } else {
-            o = acc[mi][ni][i][j] + bv[ni][j];
-          }
+          f32x4 o = acc[mi][ni][i][j] + bv[ni][j];
           if (gelu) {
             const f32x2 lo = gelu_erf2(f32x2{o[0], o[1]}), hi = gelu_erf2(f32x2{o[2], o[3]});
             o = f32x4{lo.x, lo.y, hi.x, hi.y};
@@ -695,45 +678,141 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
   }
 }
 
-// RES = false only: residual GEMMs keep the non-persistent LDS-staged kernel (their epilogue
-// would need the residual tile in registers next to the accumulators).
-template <bool RES, bool MX = false, bool Q8 = false>
+// Epilogue parameters of one tile of the persistent kernel, staged in LDS (one slot per tile,
+// two slots): bias[256] fp32 | acol[256] fp32 (folded LayerNorm column sums) | row partials
+// [256][3] (mean_t, M2_t) float2.  Each wave issues ONE LDS-DMA of 1 KiB per tile (waves 0-5 the
+// partials, 6 the bias, 7 acol) BEFORE that tile's prologue, so the epilogue issues no global
+// load at all: it never waits for the next tile's prologue (a global load issued after it could
+// only be waited for behind it: vector-memory ops retire in issue order).
+constexpr int G8P_EP = 2048 + 256 * 3 * 8;   // 8 KiB per slot
+constexpr int G8P_SMEM = G8_OPS + 2 * G8P_EP;
+
+// Direct epilogue of one tile (acc holds C^T blocks, see gemm8_kernel<TR = true>): lane holds
+// C[m][n .. n+3], m = m0 + mi*128 + wm*64 + i*16 + r16, n = n0 + ni*128 + wn*32 + j*16 + q*4.
+//   o = act(rstd_m * acc + (bias[n] - rstd_m mean_m acol[n]))   (folded LayerNorm of A, GemmArgs.apart)
+//   o = act(acc + bias[n])                                        (otherwise: rstd = 1 and the acol term
+//                                                                  is not formed, bit-identical to a plain add)
+template <int ACT>
+SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, int n0, int wm, int wn, int q,
+                          int r16, const char* ep, bool has_bias, bool fold) {
+  f32x4 bv[2][2], ac[2][2];
+  #pragma unroll
+  for (int ni = 0; ni < 2; ++ni)
+    #pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = ni * 128 + wn * 32 + j * 16 + q * 4;
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      const f32x4 b = *(const f32x4*)(ep + c * 4), a = *(const f32x4*)(ep + 1024 + c * 4);
+      bv[ni][j] = has_bias ? b : z;
+      ac[ni][j] = fold ? a : z;
+    }
+  float2 ast[2][4];
+  #pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float2* p = (const float2*)(ep + 2048) + (mi * 128 + wm * 64 + i * 16 + r16) * 3;
+      const float2 v[3] = {p[0], p[1], p[2]};
+      const float2 st = ln_part_combine<3>(v, g.ln_eps);
+      ast[mi][i] = fold ? st : make_float2(0.f, 1.f);
+    }
+  auto finish_half = [&](int mi) {
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float rs = ast[mi][i].y, nm = -ast[mi][i].x * ast[mi][i].y;
+      #pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+        #pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x4 o;
+          #pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = fmaf(acc[mi][ni][i][j][e], rs, fmaf(nm, ac[ni][j][e], bv[ni][j][e]));
+          if constexpr (ACT == ACT_GELU) {
+            const f32x2 lo = gelu_erf2(f32x2{o[0], o[1]}), hi = gelu_erf2(f32x2{o[2], o[3]});
+            o = f32x4{lo.x, lo.y, hi.x, hi.y};
+          } else if constexpr (ACT == ACT_GELU_FAST) {
+            const f32x2 lo = gelu_sig2(f32x2{o[0], o[1]}), hi = gelu_sig2(f32x2{o[2], o[3]});
+            o = f32x4{lo.x, lo.y, hi.x, hi.y};
+          }
+          acc[mi][ni][i][j] = o;
+        }
+    }
+  };
+  // fp32 out: one 16-B store per (i, ni, j).  bf16 out: the two j blocks of a lane pair are exchanged
+  // with v_permlane16_swap so every lane holds 8 consecutive columns: one 16-B store per (i, ni).
+  auto store_half = [&](int mi) {
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + mi * 128 + wm * 64 + i * 16 + r16;
+      const bool ok = m < g.M;
+      const long long row = (long long)(ok ? m : 0) * g.ldc;
+      #pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        if (g.Cf && ok) {
+          #pragma unroll
+          for (int j = 0; j < 2; ++j)
+            *(f32x4*)(g.Cf + row + n0 + ni * 128 + wn * 32 + j * 16 + q * 4) = acc[mi][ni][i][j];
+        }
+        if (g.Ct) {
+          const f32x4 o0 = acc[mi][ni][i][0], o1 = acc[mi][ni][i][1];
+          const bf16x4 x0 = {(bf16)o0[0], (bf16)o0[1], (bf16)o0[2], (bf16)o0[3]};
+          const bf16x4 x1 = {(bf16)o1[0], (bf16)o1[1], (bf16)o1[2], (bf16)o1[3]};
+          const uint2 X = __builtin_bit_cast(uint2, x0), Y = __builtin_bit_cast(uint2, x1);
+          const auto s0 = __builtin_amdgcn_permlane16_swap(X.x, Y.x, false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(X.y, Y.y, false, false);
+          if (ok) {
+            const uint4 v = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+            *(uint4*)((bf16*)g.Ct + row + n0 + ni * 128 + wn * 32 + (q & 1) * 16 + (q >> 1) * 8) = v;
+          }
+        }
+      }
+    }
+  };
+  finish_half(0);
+  store_half(0);
+  finish_half(1);
+  store_half(1);
+}
+
+// ======================================================================================
+// Persistent variant (default for bf16 GEMMs without a residual).  One block per CU walks tiles
+// r*G + remap(b) (round r, the same XCD-aware remap per round).  After a tile's last MFMA the block
+// issues the NEXT tile's epilogue-parameter DMA and six prologue half-tiles, then runs this tile's
+// epilogue from LDS: its math overlaps the prologue's HBM/L2 latency, and its stores are left in
+// flight -- the next tile's first K-tile waits vmcnt(2n + S) (S = store instructions issued after
+// its prologue), so it needs only the prologue loads and the stores drain under its MFMAs.
+// ======================================================================================
+template <int ACT>
 __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
-  __shared__ __attribute__((aligned(16))) char smem[MX ? G8_OPS_MX : G8_OPS];   // the ONLY shared object
+  __shared__ __attribute__((aligned(16))) char smem[G8P_SMEM];   // operands | 2 epilogue slots: the ONLY shared object
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   const int q = lane >> 4, r16 = lane & 15;
   const int M = g.M, K = g.K;
   const int n_tiles_n = g.N / 256;
-  constexpr int ES = MX ? 1 : 2;
-  const int nk = K / (128 / ES);
+  const int nk = K / 64;
   const int G = gridDim.x, b = blockIdx.x;
   // stores per wave of one full tile (the count the next tile's first K-tile may leave in
   // flight); under-counting is safe, so it is capped to keep 2n + S within vmcnt's 6 bits
   const int s_full = min(32 * (g.Cf ? 1 : 0) + 16 * (g.Ct ? 1 : 0), 54);   // 54 + 9 <= 63
+  const bool has_bias = g.bias != nullptr, fold = g.apart != nullptr;
 
   int round = 0;
   int tile = g8p_tile(b, 0, G, n_tiles);
   if (tile < 0) return;
 
   constexpr int NREC = 0x7FFFFFF0;
-  __amdgpu_buffer_rsrc_t a_rsrc, b_rsrc, s_rsrc;
-  unsigned a_voff[2][2], b_voff[2][2], s_voff = 0;
+  __amdgpu_buffer_rsrc_t a_rsrc, b_rsrc;
+  unsigned a_voff[2][2], b_voff[2][2];
   auto setup = [&](int tl) {
     const int m0 = (tl / n_tiles_n) * 256, n0 = (tl % n_tiles_n) * 256;
     const int mf = m0 < M ? m0 : M - 1;
     const int seg0 = mf / g.rows_per_seg, rr0 = mf - seg0 * g.rows_per_seg;
-    const long long a_base = ((long long)seg0 * g.seg_stride + (long long)rr0 * g.lda) * ES;   // bytes
+    const long long a_base = ((long long)seg0 * g.seg_stride + (long long)rr0 * g.lda) * 2;   // bytes
     a_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)g.A + a_base), (short)0, NREC, 0x00020000);
-    b_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)g.B + (long long)n0 * K * ES), (short)0, NREC,
+    b_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)g.B + (long long)n0 * K * 2), (short)0, NREC,
                                                0x00020000);
-    if constexpr (MX) {   // this tile's scale blocks; waves 0-3 stage A's 1 KiB, waves 4-7 B's
-      const unsigned char* sb = wave < 4 ? g.a_scale + (long long)(m0 >> 8) * nk * 1024
-                                         : g.b_scale + (long long)(n0 >> 8) * nk * 1024;
-      s_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)sb, (short)0, NREC, 0x00020000);
-      s_voff = (unsigned)((wave & 3) * 256 + lane * 4);
-    }
     #pragma unroll
     for (int h = 0; h < 2; ++h)
       #pragma unroll
@@ -743,9 +822,9 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
         int m = m0 + row;
         m = m < M ? m : M - 1;
         const int seg = m / g.rows_per_seg, rr = m - seg * g.rows_per_seg;
-        const long long el = ((long long)seg * g.seg_stride + (long long)rr * g.lda) * ES + ch * 16;
+        const long long el = ((long long)seg * g.seg_stride + (long long)rr * g.lda) * 2 + ch * 16;
         a_voff[h][s] = (unsigned)(el - a_base);
-        b_voff[h][s] = (unsigned)((long long)row * K * ES + ch * 16);
+        b_voff[h][s] = (unsigned)((long long)row * K * 2 + ch * 16);
       }
   };
   auto issue = [&](int k) {
@@ -755,11 +834,6 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
     if (tl >= nk) return;
     char* dst = smem + (tl & 1) * G8_BUF + half * G8_HALF;
     const unsigned soff = (unsigned)tl * 128u;
-    if constexpr (MX) {
-      if (half == 0)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(s_rsrc, LPTR(smem + G8_OPS + (tl & 3) * G8_SC + wave * 256), 4,
-                                                 s_voff, (unsigned)tl * 1024u, 0, 0);
-    }
     if (half < 2) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, LPTR(dst + wave * 1024), 16, a_voff[half][0], soff, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, LPTR(dst + (wave + 8) * 1024), 16, a_voff[half][1], soff, 0, 0);
@@ -769,74 +843,70 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
                                                0);
     }
   };
+  // epilogue-parameter DMA of tile tl into slot: one 1 KiB piece per wave; absent operands read as
+  // an empty buffer (num_records 0, nothing is fetched; the epilogue ignores the slot bytes)
+  const void* zb = g.zero;
+  auto ep_issue = [&](int tl, int slot) {
+    const int m0 = (tl / n_tiles_n) * 256, n0 = (tl % n_tiles_n) * 256;
+    char* dst = smem + G8_OPS + slot * G8P_EP;
+    __amdgpu_buffer_rsrc_t r;
+    unsigned soff;
+    int off;
+    if (wave < 6) {
+      r = __builtin_amdgcn_make_buffer_rsrc((void*)(fold ? (const void*)g.apart : zb), (short)0, fold ? M * 24 : 0,
+                                            0x00020000);
+      soff = (unsigned)(m0 * 24 + wave * 1024);
+      off = 2048 + wave * 1024;
+    } else if (wave == 6) {
+      r = __builtin_amdgcn_make_buffer_rsrc((void*)(has_bias ? (const void*)g.bias : zb), (short)0,
+                                            has_bias ? g.N * 4 : 0, 0x00020000);
+      soff = (unsigned)(n0 * 4);
+      off = 0;
+    } else {
+      r = __builtin_amdgcn_make_buffer_rsrc((void*)(fold ? (const void*)g.acol : zb), (short)0, fold ? g.N * 4 : 0,
+                                            0x00020000);
+      soff = (unsigned)(n0 * 4);
+      off = 1024;
+    }
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, LPTR(dst + off), 16, (unsigned)lane * 16u, soff, 0, 0);
+  };
 
   f32x4 acc[2][2][4][2];
   bf16x8 af[4][2], b0f[2][2], b1f[2][2];
-  int sa = 0, sb = 0;
-  auto read_sa = [&](int t, int mi) {
-    if constexpr (MX) sa = *(const int*)(smem + G8_OPS + (t & 3) * G8_SC + (((mi * 2 + wm) * 4 + q) * 16 + r16) * 4);
-  };
-  auto read_sb = [&](int t) {
-    if constexpr (MX) sb = *(const int*)(smem + G8_OPS + (t & 3) * G8_SC + 1024 + ((wn * 4 + q) * 16 + r16) * 4);
-  };
-  // MX: the same two 16-B reads per fragment, landing in one 8-dword operand tuple
-  i32x8 afx[4], b0x[2], b1x[2];
-  auto rd32 = [&](const char* hb, int row) {
-    const i32x4 lo = *(const i32x4*)(hb + row * 128 + ((q ^ ((row >> 1) & 7)) * 16));
-    const i32x4 hi = *(const i32x4*)(hb + row * 128 + (((q + 4) ^ ((row >> 1) & 7)) * 16));
-    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-  };
   auto read_a = [&](const char* hb) {
     #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = wm * 64 + i * 16 + r16;
-      if constexpr (MX) {
-        afx[i] = rd32(hb, row);
-      } else {
-        #pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-          af[i][ks] = *(const bf16x8*)(hb + row * 128 + (((q + 4 * ks) ^ ((row >> 1) & 7)) * 16));
-      }
+      #pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        af[i][ks] = *(const bf16x8*)(hb + row * 128 + (((q + 4 * ks) ^ ((row >> 1) & 7)) * 16));
     }
   };
-  auto read_b = [&](const char* hb, bf16x8 (&bf)[2][2], i32x8 (&bx)[2]) {
+  auto read_b = [&](const char* hb, bf16x8 (&bf)[2][2]) {
     #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int row = wn * 32 + j * 16 + r16;
-      if constexpr (MX) {
-        bx[j] = rd32(hb, row);
-      } else {
-        #pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-          bf[j][ks] = *(const bf16x8*)(hb + row * 128 + (((q + 4 * ks) ^ ((row >> 1) & 7)) * 16));
-      }
+      #pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        bf[j][ks] = *(const bf16x8*)(hb + row * 128 + (((q + 4 * ks) ^ ((row >> 1) & 7)) * 16));
     }
   };
-  auto mma = [&](f32x4 (&c)[4][2], const bf16x8 (&bf)[2][2], const i32x8 (&bx)[2], auto ni_c) {
-    constexpr int NI = decltype(ni_c)::value;
+  auto mma = [&](f32x4 (&c)[4][2], const bf16x8 (&bf)[2][2]) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
-    if constexpr (MX) {
-      g8_sfor<0, 4>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        g8_sfor<0, 2>([&](auto jc) {
-          constexpr int j = decltype(jc)::value;
-          c[i][j] = g8_mx<NI * 2 + j, i>(bx[j], afx[i], c[i][j], sb, sa);
-        });
-      });
-    } else {
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
       #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+      for (int i = 0; i < 4; ++i)
         #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          #pragma unroll
-          for (int j = 0; j < 2; ++j) c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][ks], af[i][ks], c[i][j], 0, 0, 0);
-    }
+        for (int j = 0; j < 2; ++j) c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][ks], af[i][ks], c[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   };
 
+  int slot = 0;
+  ep_issue(tile, 0);
   setup(tile);
   for (int k = -6; k < 0; ++k) issue(k);
   int S = 0;   // store instructions issued after the current tile's prologue
@@ -850,7 +920,8 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
         for (int i = 0; i < 4; ++i)
           #pragma unroll
           for (int j = 0; j < 2; ++j) acc[a][c][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    g8_vmcnt_dyn<MX>(g8_count<MX>(-1, nk) + S);
+    // the epilogue-parameter DMA precedes the prologue: retired by the same counted waits
+    g8_vmcnt_dyn<false>(g8_count<false>(-1, nk) + S);
     g8_barrier();
     if (wm == 1) g8_barrier();   // group 1 runs one barrier behind
 
@@ -863,38 +934,32 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
       auto issue_wait = [&](int kk) {
         issue(kk);
         if constexpr (FI) {
-          g8_vmcnt_dyn<MX>(g8_count<MX>(kk, nk) + S);
+          g8_vmcnt_dyn<false>(g8_count<false>(kk, nk) + S);
         } else if constexpr (ST) {
-          if constexpr (MX) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-          else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         } else {
-          g8_wait<MX>(kk, nk);
+          g8_wait<false>(kk, nk);
         }
       };
-      const std::integral_constant<int, 0> ni0;
-      const std::integral_constant<int, 1> ni1;
       read_a(buf);
-      read_b(buf + 2 * G8_HALF, b0f, b0x);
-      read_sa(t, 0);
-      read_sb(t);
+      read_b(buf + 2 * G8_HALF, b0f);
       issue_wait(k);
       g8_barrier();
-      mma(acc[0][0], b0f, b0x, ni0);
+      mma(acc[0][0], b0f);
       g8_barrier();
-      read_b(buf + 3 * G8_HALF, b1f, b1x);
+      read_b(buf + 3 * G8_HALF, b1f);
       issue_wait(k + 1);
       g8_barrier();
-      mma(acc[0][1], b1f, b1x, ni1);
+      mma(acc[0][1], b1f);
       g8_barrier();
       read_a(buf + G8_HALF);
-      read_sa(t, 1);
       issue_wait(k + 2);
       g8_barrier();
-      mma(acc[1][1], b1f, b1x, ni1);
+      mma(acc[1][1], b1f);
       g8_barrier();
       issue_wait(k + 3);
       g8_barrier();
-      mma(acc[1][0], b0f, b0x, ni0);
+      mma(acc[1][0], b0f);
       g8_barrier();
     };
     run_tile(0, std::integral_constant<bool, false>{}, std::integral_constant<bool, true>{});
@@ -906,13 +971,319 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
     ++round;
     const int next = g8p_tile(b, round, G, n_tiles);
     if (next >= 0) {
+      ep_issue(next, slot ^ 1);
       setup(next);
       for (int k = -6; k < 0; ++k) issue(k);
     }
-    g8_epilogue_direct<RES, Q8>(g, acc, m0, n0, wm, wn, q, r16);
+    g8p_epilogue<ACT>(g, acc, m0, n0, wm, wn, q, r16, smem + G8_OPS + slot * G8P_EP, has_bias, fold);
     if (next < 0) break;
+    slot ^= 1;
     S = m0 + 256 <= M ? s_full : 0;
     tile = next;
+  }
+}
+
+// ======================================================================================
+// Residual GEMMs (C = A B^T + bias + LN?(resid), fp32 out, optional bf16 copy and LayerNorm
+// partials of the output rows): one tile per block, the persistent kernel's 8-phase main loop,
+// then a register-direct epilogue (acc holds C^T blocks) whose loads all precede its first store:
+//   1. LDS-DMA of the epilogue parameters into the (now free) operand LDS: bias, rln_w, rln_b
+//      (1 KiB each) and the residual rows' LayerNorm partials [256][3] (6 KiB);
+//   2. the residual rows of half 0 (16 x 16 B per lane) -- in flight together with the DMA;
+//   3. half 0 finished in registers, THEN half 1's residual loads, THEN half 0's stores: the wait
+//      for half 1 never includes a store (vector-memory ops retire in issue order).
+// LayerNorm partials of the written rows (OPART, the folded post-LN path): per row, each wave
+// reduces its 64 columns (16 in-lane values, lanes q = 0..3) to (mean_c, M2_c), the 4 waves' chunks
+// meet in LDS and one thread per row combines them (Chan) into the 256-column (mean_t, M2_t).
+// ======================================================================================
+template <bool LN, bool OPART>
+__global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[G8_OPS];   // the ONLY shared object
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int q = lane >> 4, r16 = lane & 15;
+  const int M = g.M, K = g.K;
+  const int n_tiles_n = g.N / 256;
+  const int nk = K / 64;
+  int bid = blockIdx.x;
+  {   // XCD-aware bijective remap (as gemm8_kernel)
+    const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
+    bid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
+  }
+  const int m0 = (bid / n_tiles_n) * 256, n0 = (bid % n_tiles_n) * 256;
+
+  constexpr int NREC = 0x7FFFFFF0;
+  __amdgpu_buffer_rsrc_t a_rsrc, b_rsrc;
+  unsigned a_voff[2][2], b_voff[2][2];
+  {
+    const int mf = m0 < M ? m0 : M - 1;
+    const int seg0 = mf / g.rows_per_seg, rr0 = mf - seg0 * g.rows_per_seg;
+    const long long a_base = ((long long)seg0 * g.seg_stride + (long long)rr0 * g.lda) * 2;
+    a_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)g.A + a_base), (short)0, NREC, 0x00020000);
+    b_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)g.B + (long long)n0 * K * 2), (short)0, NREC,
+                                               0x00020000);
+    #pragma unroll
+    for (int h = 0; h < 2; ++h)
+      #pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int row = h * 128 + (wave + 8 * s) * 8 + (lane >> 3);
+        const int ch = (lane & 7) ^ ((row >> 1) & 7);
+        int m = m0 + row;
+        m = m < M ? m : M - 1;
+        const int seg = m / g.rows_per_seg, rr = m - seg * g.rows_per_seg;
+        const long long el = ((long long)seg * g.seg_stride + (long long)rr * g.lda) * 2 + ch * 16;
+        a_voff[h][s] = (unsigned)(el - a_base);
+        b_voff[h][s] = (unsigned)((long long)row * K * 2 + ch * 16);
+      }
+  }
+  auto issue = [&](int k) {
+    if (k < -6) return;
+    int tl, half;
+    g8_target(k, tl, half);
+    if (tl >= nk) return;
+    char* dst = smem + (tl & 1) * G8_BUF + half * G8_HALF;
+    const unsigned soff = (unsigned)tl * 128u;
+    if (half < 2) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, LPTR(dst + wave * 1024), 16, a_voff[half][0], soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, LPTR(dst + (wave + 8) * 1024), 16, a_voff[half][1], soff, 0, 0);
+    } else {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, LPTR(dst + wave * 1024), 16, b_voff[half - 2][0], soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, LPTR(dst + (wave + 8) * 1024), 16, b_voff[half - 2][1], soff, 0,
+                                               0);
+    }
+  };
+  f32x4 acc[2][2][4][2];
+  #pragma unroll
+  for (int a = 0; a < 2; ++a)
+    #pragma unroll
+    for (int c = 0; c < 2; ++c)
+      #pragma unroll
+      for (int i = 0; i < 4; ++i)
+        #pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][c][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[4][2], b0f[2][2], b1f[2][2];
+  auto read_a = [&](const char* hb) {
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wm * 64 + i * 16 + r16;
+      #pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        af[i][ks] = *(const bf16x8*)(hb + row * 128 + (((q + 4 * ks) ^ ((row >> 1) & 7)) * 16));
+    }
+  };
+  auto read_b = [&](const char* hb, bf16x8 (&bf)[2][2]) {
+    #pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = wn * 32 + j * 16 + r16;
+      #pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        bf[j][ks] = *(const bf16x8*)(hb + row * 128 + (((q + 4 * ks) ^ ((row >> 1) & 7)) * 16));
+    }
+  };
+  auto mma = [&](f32x4 (&c)[4][2], const bf16x8 (&bf)[2][2]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      #pragma unroll
+      for (int i = 0; i < 4; ++i)
+        #pragma unroll
+        for (int j = 0; j < 2; ++j) c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][ks], af[i][ks], c[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  for (int k = -6; k < 0; ++k) issue(k);
+  g8_wait<false>(-1, nk);
+  g8_barrier();
+  if (wm == 1) g8_barrier();   // group 1 runs one barrier behind
+  auto run_tile = [&](int t, auto steady) {
+    constexpr bool ST = decltype(steady)::value;
+    const char* buf = smem + (t & 1) * G8_BUF;
+    const int k = 4 * t;
+    auto issue_wait = [&](int kk) {
+      issue(kk);
+      if constexpr (ST) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else g8_wait<false>(kk, nk);
+    };
+    read_a(buf);
+    read_b(buf + 2 * G8_HALF, b0f);
+    issue_wait(k);
+    g8_barrier();
+    mma(acc[0][0], b0f);
+    g8_barrier();
+    read_b(buf + 3 * G8_HALF, b1f);
+    issue_wait(k + 1);
+    g8_barrier();
+    mma(acc[0][1], b1f);
+    g8_barrier();
+    read_a(buf + G8_HALF);
+    issue_wait(k + 2);
+    g8_barrier();
+    mma(acc[1][1], b1f);
+    g8_barrier();
+    issue_wait(k + 3);
+    g8_barrier();
+    mma(acc[1][0], b0f);
+    g8_barrier();
+  };
+  int t = 0;
+  for (; t + 2 < nk; ++t) run_tile(t, std::integral_constant<bool, true>{});
+  for (; t < nk; ++t) run_tile(t, std::integral_constant<bool, false>{});
+  if (wm == 0) g8_barrier();   // balance group 1's extra barrier: every wave's LDS reads are done
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // ---- epilogue ----
+  // LDS (operand area, free now): [0, 1K) bias | [1K, 2K) rln_w | [2K, 3K) rln_b | [3K, 9K) partials
+  // [256][3] | [16K, 24K) chunk statistics [2 halves][128 rows][4 waves] float2
+  const bool has_bias = g.bias != nullptr;
+  {
+    __amdgpu_buffer_rsrc_t r;
+    unsigned soff = 0;
+    int off = 0;
+    bool go = true;
+    if (wave < 6) {
+      go = LN;
+      r = __builtin_amdgcn_make_buffer_rsrc((void*)(LN ? (const void*)g.rpart : g.zero), (short)0, LN ? M * 24 : 0,
+                                            0x00020000);
+      soff = (unsigned)(m0 * 24 + wave * 1024);
+      off = 3072 + wave * 1024;
+    } else if (wave == 6) {
+      go = has_bias;
+      r = __builtin_amdgcn_make_buffer_rsrc((void*)(has_bias ? (const void*)g.bias : g.zero), (short)0,
+                                            has_bias ? g.N * 4 : 0, 0x00020000);
+      soff = (unsigned)(n0 * 4);
+    } else {
+      go = LN;
+      r = __builtin_amdgcn_make_buffer_rsrc((void*)(LN ? (const void*)g.rln_w : g.zero), (short)0, LN ? g.N * 4 : 0,
+                                            0x00020000);
+      soff = (unsigned)(n0 * 4);
+      off = 1024;
+    }
+    if (go) __builtin_amdgcn_raw_ptr_buffer_load_lds(r, LPTR(smem + off), 16, (unsigned)lane * 16u, soff, 0, 0);
+    if (LN && wave == 7) {
+      r = __builtin_amdgcn_make_buffer_rsrc((void*)g.rln_b, (short)0, g.N * 4, 0x00020000);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, LPTR(smem + 2048), 16, (unsigned)lane * 16u, soff, 0, 0);
+    }
+  }
+  f32x4 rv[4][2][2];
+  auto load_half = [&](int mi) {
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + mi * 128 + wm * 64 + i * 16 + r16;
+      const int mc = m < M ? m : 0;
+      const long long rrow = g.resid_rows ? (long long)(mc % g.resid_rows) * g.ldc : (long long)mc * g.ldc;
+      #pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+        #pragma unroll
+        for (int j = 0; j < 2; ++j)
+          rv[i][ni][j] = *(const f32x4*)(g.resid + rrow + n0 + ni * 128 + wn * 32 + j * 16 + q * 4);
+    }
+  };
+  __builtin_amdgcn_sched_barrier(0);
+  load_half(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // parameter DMA (and half 0's rows) landed
+  __syncthreads();
+  __builtin_amdgcn_sched_barrier(0);
+  // column parameters are read from LDS where they are used (registers hold acc + one half's rows)
+  float2* cst = (float2*)(smem + 16384);
+  auto finish_half = [&](int mi) {
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float2 st = make_float2(0.f, 1.f);
+      if constexpr (LN) {
+        const float2* p = (const float2*)(smem + 3072) + (mi * 128 + wm * 64 + i * 16 + r16) * 3;
+        const float2 v[3] = {p[0], p[1], p[2]};
+        st = ln_part_combine<3>(v, g.ln_eps);
+      }
+      float sum = 0.f;
+      #pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+        #pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int c = ni * 128 + wn * 32 + j * 16 + q * 4;
+          f32x4 r = rv[i][ni][j];
+          if constexpr (LN) {   // LayerNorm of the residual, the exact expression of layernorm_kernel
+            const f32x4 lw = *(const f32x4*)(smem + 1024 + c * 4), lb = *(const f32x4*)(smem + 2048 + c * 4);
+            #pragma unroll
+            for (int e = 0; e < 4; ++e) r[e] = fmaf((r[e] - st.x) * st.y, lw[e], lb[e]);
+          }
+          const f32x4 bvv = *(const f32x4*)(smem + c * 4);
+          const f32x4 bv = has_bias ? bvv : f32x4{0.f, 0.f, 0.f, 0.f};
+          const f32x4 o = (acc[mi][ni][i][j] + bv) + r;
+          acc[mi][ni][i][j] = o;
+          sum += (o[0] + o[1]) + (o[2] + o[3]);
+        }
+      if constexpr (OPART) {   // this wave's 64 columns of the row: lanes r16 + 16q
+        sum += __shfl_xor(sum, 16, 64);
+        sum += __shfl_xor(sum, 32, 64);
+        const float mc = sum * (1.0f / 64.0f);
+        float m2 = 0.f;
+        #pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          #pragma unroll
+          for (int j = 0; j < 2; ++j)
+            #pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float d = acc[mi][ni][i][j][e] - mc;
+              m2 = fmaf(d, d, m2);
+            }
+        m2 += __shfl_xor(m2, 16, 64);
+        m2 += __shfl_xor(m2, 32, 64);
+        if (q == 0) cst[(mi * 128 + wm * 64 + i * 16 + r16) * 4 + wn] = make_float2(mc, m2);
+      }
+    }
+  };
+  auto store_half = [&](int mi) {
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + mi * 128 + wm * 64 + i * 16 + r16;
+      const bool ok = m < M;
+      const long long row = (long long)(ok ? m : 0) * g.ldc;
+      #pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        if (ok) {
+          #pragma unroll
+          for (int j = 0; j < 2; ++j)
+            *(f32x4*)(g.Cf + row + n0 + ni * 128 + wn * 32 + j * 16 + q * 4) = acc[mi][ni][i][j];
+        }
+        if (g.Ct) {
+          const f32x4 o0 = acc[mi][ni][i][0], o1 = acc[mi][ni][i][1];
+          const bf16x4 x0 = {(bf16)o0[0], (bf16)o0[1], (bf16)o0[2], (bf16)o0[3]};
+          const bf16x4 x1 = {(bf16)o1[0], (bf16)o1[1], (bf16)o1[2], (bf16)o1[3]};
+          const uint2 X = __builtin_bit_cast(uint2, x0), Y = __builtin_bit_cast(uint2, x1);
+          const auto s0 = __builtin_amdgcn_permlane16_swap(X.x, Y.x, false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(X.y, Y.y, false, false);
+          if (ok) {
+            const uint4 v = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+            *(uint4*)((bf16*)g.Ct + row + n0 + ni * 128 + wn * 32 + (q & 1) * 16 + (q >> 1) * 8) = v;
+          }
+        }
+      }
+    }
+  };
+  // sched_barriers keep the phases in this order (the register budget holds one half's rows)
+  finish_half(0);
+  __builtin_amdgcn_sched_barrier(0);
+  load_half(1);   // before the first store
+  __builtin_amdgcn_sched_barrier(0);
+  store_half(0);
+  __builtin_amdgcn_sched_barrier(0);
+  finish_half(1);
+  __builtin_amdgcn_sched_barrier(0);
+  store_half(1);
+  if constexpr (OPART) {
+    __syncthreads();
+    if (threadIdx.x < 256) {
+      const int r = threadIdx.x, m = m0 + r;
+      const float2* c = cst + r * 4;
+      const float2 c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3];
+      const float mean = 0.25f * ((c0.x + c1.x) + (c2.x + c3.x));
+      const float d0 = c0.x - mean, d1 = c1.x - mean, d2 = c2.x - mean, d3 = c3.x - mean;
+      const float m2 = ((c0.y + c1.y) + (c2.y + c3.y)) + 64.f * ((d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3));
+      if (m < M) g.opart[(long long)m * n_tiles_n + (n0 >> 8)] = make_float2(mean, m2);
+    }
   }
 }
 
@@ -920,10 +1291,23 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
 
 int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
   if (a.M <= 0 || a.N % 256 || a.K % 64 || a.K <= 0) return -3;
+  // folded-LayerNorm partials: rows of 3 column tiles (H = 768); opart tiles = N / 256
+  if ((a.apart && a.apart_nt != 3) || (a.rpart && a.rpart_nt != 3) || (a.opart && a.N != 768)) return -3;
   dim3 grid((unsigned)(((a.M + 255) / 256) * (a.N / 256)));
   // OPT_GEMM_NONPERSIST (tests, A/B): the non-persistent LDS-staged kernel for every shape
-  if (a.resid || sse_opt(OPT_GEMM_NONPERSIST)) {
+  if (sse_opt(OPT_GEMM_NONPERSIST)) {
     hipLaunchKernelGGL((gemm8_kernel<0, false, false>), grid, dim3(512), 0, s, a);
+  } else if (a.resid) {
+    // residual GEMMs: fp32 out (Cf) required; the rstats form is the staged kernel's only
+    if (!a.Cf || a.rstats || (a.opart && !a.rpart && a.rln_w)) {
+      hipLaunchKernelGGL((gemm8_kernel<0, false, false>), grid, dim3(512), 0, s, a);
+    } else if (a.rpart) {
+      if (a.opart) hipLaunchKernelGGL((gemm8r_kernel<true, true>), grid, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((gemm8r_kernel<true, false>), grid, dim3(512), 0, s, a);
+    } else {
+      if (a.opart) hipLaunchKernelGGL((gemm8r_kernel<false, true>), grid, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((gemm8r_kernel<false, false>), grid, dim3(512), 0, s, a);
+    }
   } else {
     // persistent: one block per CU (LDS-bound), at most one per tile
     static int cus[64] = {0};
@@ -933,7 +1317,12 @@ int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
       return -2;
     const int n_tiles = (int)grid.x;
     const int G = n_tiles < cus[dev] ? n_tiles : cus[dev];
-    hipLaunchKernelGGL(gemm8p_kernel<false>, dim3(G), dim3(512), 0, s, a, n_tiles);
+    if (a.act == ACT_GELU)
+      hipLaunchKernelGGL(gemm8p_kernel<ACT_GELU>, dim3(G), dim3(512), 0, s, a, n_tiles);
+    else if (a.act == ACT_GELU_FAST)
+      hipLaunchKernelGGL(gemm8p_kernel<ACT_GELU_FAST>, dim3(G), dim3(512), 0, s, a, n_tiles);
+    else
+      hipLaunchKernelGGL(gemm8p_kernel<ACT_NONE>, dim3(G), dim3(512), 0, s, a, n_tiles);
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -309,7 +309,7 @@ int build_wavlm(sse_model* m, Blob& bl, Arena& ar) {
     }
     m->relb = ar.put_f32(tab.data(), tab.size());
   }
-  const bool fold = BF && !c.stable_layer_norm && H % 256 == 0 && H <= 2048;
+  const bool fold = BF && !c.stable_layer_norm && H == 768;   // the GEMM epilogues combine 3 column-tile partials
   const float *prev_l2w = nullptr, *prev_l2b = nullptr;
   for (int l = 0; l < c.layers; ++l) {
     const float *qw = bl.take((size_t)H * H), *qb = bl.take(H), *kw = bl.take((size_t)H * H), *kb = bl.take(H);
