@@ -64,6 +64,7 @@ def parse():
     ap.add_argument("--no-profile", action="store_true", help="skip the per-launch event timing")
     ap.add_argument("--stream", action="store_true",
                     help="clips streamed from pinned host memory each step (double-buffered H2D on a side stream)")
+    ap.add_argument("--lib", default=None, help="load this build of libsse.so instead of the in-tree one (A/B)")
     ap.add_argument("--corpus", type=int, default=0,
                     help="BASELINE configs[3] mode: embed a corpus of this many clips (e.g. 50000) sharded "
                          "across the ranks with corpus.extract_corpus (tail batch + one all-gather timed)")
@@ -236,6 +237,9 @@ def corpus_run(a, model, spec, idx, clips, B, L, world, rank, dev, dist):
 
 def main():
     a = parse()
+    if a.lib:
+        from ssr_amd import _lib
+        _lib.use_library(a.lib)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

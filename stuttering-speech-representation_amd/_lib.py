@@ -82,6 +82,16 @@ def make_cfg(spec, do_normalize: bool = False) -> sse_cfg:
 _lib = None
 
 
+def use_library(path: str) -> None:
+    """Load another build of the same ABI instead of the in-tree libsse.so (same-box A/B timing,
+    ``bench.py --lib``).  Must be called before the first ``lib()``; explicit only, never read
+    from the environment."""
+    global LIB_PATH
+    if _lib is not None:
+        raise RuntimeError("libsse.so is already loaded")
+    LIB_PATH = os.path.abspath(path)
+
+
 def lib() -> ctypes.CDLL:
     """Load libsse.so (raises ImportError with the build hint if it is absent)."""
     global _lib

@@ -739,38 +739,68 @@ int launch_mx_quantize(const float* x, int R, int K, int role, unsigned char* q,
 
 // ---------------------------------------------------------------------------------------
 // K8/K12: out[b*out_stride + n] = mean_t x[b][t][n]  (torch.mean(hs, dim=1), fp64 accumulation).
-// Block = 64 columns x 4 waves; wave w sums frames t = w, w+4, ... (fp64), LDS combine.  With
-// stats, each element is first normalised exactly as layernorm_kernel would have written it.
+// Block = (256 columns, clip), 4 waves; lane owns 4 consecutive columns (16-B loads, one 1 KiB row
+// piece per wave-instruction), wave w sums frames t = w, w+4, ... with 4 frames' loads in flight,
+// then an LDS combine.  With per-row LayerNorm statistics (st: (mean, rstd); or lpart: per-256-column
+// partials, ln_part_stats), each element is first normalised exactly as layernorm_kernel would have
+// written it; the clip's per-frame statistics are formed once into LDS.
+constexpr int POOL_TMAX = 1024;   // frames whose statistics fit the LDS table (longer clips: per-frame loads)
 __global__ __launch_bounds__(256) void pool_mean_kernel(const float* __restrict__ x, int T, int H,
                                                         float* __restrict__ out, long long out_stride,
                                                         const float2* __restrict__ st, const float* __restrict__ w,
                                                         const float* __restrict__ bb, const float2* __restrict__ lpart,
                                                         int nt, float eps) {
-  __shared__ double part[4][64];
+  __shared__ double part[4][256];
+  __shared__ float2 fst[POOL_TMAX];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int n = blockIdx.x * 64 + lane, b = blockIdx.y;
-  double s = 0.0;
+  const int n = blockIdx.x * 256 + lane * 4, b = blockIdx.y;
+  const bool ln = st || lpart;
+  const bool tab = ln && T <= POOL_TMAX;
+  if (tab) {
+    for (int t = threadIdx.x; t < T; t += 256)
+      fst[t] = st ? st[(long long)b * T + t] : ln_part_stats(lpart, nt, (long long)b * T + t, eps);
+    __syncthreads();
+  }
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   if (n < H) {
     const float* xb = x + (long long)b * T * H + n;
-    const bool ln = st || lpart;
-    const float wn = ln ? w[n] : 1.f, bn = ln ? bb[n] : 0.f;
-    for (int t = wv; t < T; t += 4) {
-      float v = xb[(long long)t * H];
+    const f32x4 wn = ln ? *(const f32x4*)(w + n) : f32x4{1.f, 1.f, 1.f, 1.f};
+    const f32x4 bn = ln ? *(const f32x4*)(bb + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    auto add = [&](f32x4 v, int t) {
       if (ln) {
-        const float2 q = st ? st[(long long)b * T + t] : ln_part_stats(lpart, nt, (long long)b * T + t, eps);
-        v = fmaf((v - q.x) * q.y, wn, bn);
+        const float2 q = tab ? fst[t] : (st ? st[(long long)b * T + t] : ln_part_stats(lpart, nt, (long long)b * T + t, eps));
+        #pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaf((v[e] - q.x) * q.y, wn[e], bn[e]);
       }
-      s += v;
+      s0 += v[0];
+      s1 += v[1];
+      s2 += v[2];
+      s3 += v[3];
+    };
+    int t = wv;
+    for (; t + 12 < T; t += 16) {   // 4 frames of this wave in flight
+      const f32x4 v0 = *(const f32x4*)(xb + (long long)t * H), v1 = *(const f32x4*)(xb + (long long)(t + 4) * H);
+      const f32x4 v2 = *(const f32x4*)(xb + (long long)(t + 8) * H), v3 = *(const f32x4*)(xb + (long long)(t + 12) * H);
+      add(v0, t);
+      add(v1, t + 4);
+      add(v2, t + 8);
+      add(v3, t + 12);
     }
+    for (; t < T; t += 4) add(*(const f32x4*)(xb + (long long)t * H), t);
   }
-  part[wv][lane] = s;
+  part[wv][lane * 4 + 0] = s0;
+  part[wv][lane * 4 + 1] = s1;
+  part[wv][lane * 4 + 2] = s2;
+  part[wv][lane * 4 + 3] = s3;
   __syncthreads();
-  if (wv == 0 && n < H) out[b * out_stride + n] = (float)((part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]) / T);
+  const int c = threadIdx.x, nc = blockIdx.x * 256 + c;
+  if (nc < H) out[b * out_stride + nc] = (float)((part[0][c] + part[1][c] + part[2][c] + part[3][c]) / T);
 }
 
 int launch_pool_mean(const float* x, int B, int T, int H, float* out, long long out_stride, hipStream_t s,
                      const float2* st, const float* w, const float* b, const float2* part, int nt, float eps) {
-  hipLaunchKernelGGL(pool_mean_kernel, dim3((H + 63) / 64, B), dim3(256), 0, s, x, T, H, out, out_stride, st, w, b,
+  if (H % 4) return -3;
+  hipLaunchKernelGGL(pool_mean_kernel, dim3((H + 255) / 256, B), dim3(256), 0, s, x, T, H, out, out_stride, st, w, b,
                      part, nt, eps);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
