@@ -177,9 +177,12 @@ struct GemmArgs {
   const float2* rpart;
   int rpart_nt;
   float ln_eps;
-  // partials of the fp32 rows this GEMM writes (Cf): opart[m][N / 256] = (mean, M2) over each
-  // 256-column tile (residual GEMMs of the folded path)
+  // partials of the rows this GEMM writes: opart[m][N / 256] = (mean, M2) over each 256-column
+  // tile (residual GEMMs of the folded path; of the rounded values when the output is bf16)
   float2* opart;
+  // bf16 residual [M][ldc] (instead of resid; folded post-LN path: the residual stream is kept in
+  // bf16 and the output is bf16 Ct only)
+  const bf16* resid_t;
 };
 
 // (mean, rstd) of a row of 256 * NT values from its per-tile partials (mean_t, M2_t), Chan's pairwise

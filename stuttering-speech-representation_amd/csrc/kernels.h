@@ -33,7 +33,8 @@ int launch_posconv_bf16(const bf16* xt, const bf16* W, const float* bias, float*
 
 // st: per-row (mean, rstd), or part: per-256-column partials [rows][nt] (ln_part_stats): each element
 // is LayerNorm'd with (w, b) before the mean
-int launch_pool_mean(const float* x, int B, int T, int H, float* out, long long out_stride, hipStream_t s,
+template <typename TI>
+int launch_pool_mean(const TI* x, int B, int T, int H, float* out, long long out_stride, hipStream_t s,
                      const float2* st = nullptr, const float* w = nullptr, const float* b = nullptr,
                      const float2* part = nullptr, int nt = 0, float eps = 0.f);
 

@@ -996,7 +996,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
 // reduces its 64 columns (16 in-lane values, lanes q = 0..3) to (mean_c, M2_c), the 4 waves' chunks
 // meet in LDS and one thread per row combines them (Chan) into the 256-column (mean_t, M2_t).
 // ======================================================================================
-template <bool LN, bool OPART>
+template <bool LN, bool OPART, bool RB>
 __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[G8_OPS];   // the ONLY shared object
   const int lane = threadIdx.x & 63;
@@ -1167,7 +1167,10 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(r, LPTR(smem + 2048), 16, (unsigned)lane * 16u, soff, 0, 0);
     }
   }
+  // RB: the bf16 residual is read in the store layout (8 consecutive columns per lane, one 16-B load
+  // per (i, ni)) and redistributed with the inverse v_permlane16_swap
   f32x4 rv[4][2][2];
+  uint4 rvb[4][2];
   auto load_half = [&](int mi) {
     #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1175,10 +1178,31 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
       const int mc = m < M ? m : 0;
       const long long rrow = g.resid_rows ? (long long)(mc % g.resid_rows) * g.ldc : (long long)mc * g.ldc;
       #pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
+      for (int ni = 0; ni < 2; ++ni) {
+        if constexpr (RB) {
+          rvb[i][ni] = *(const uint4*)(g.resid_t + rrow + n0 + ni * 128 + wn * 32 + (q & 1) * 16 + (q >> 1) * 8);
+        } else {
+          #pragma unroll
+          for (int j = 0; j < 2; ++j)
+            rv[i][ni][j] = *(const f32x4*)(g.resid + rrow + n0 + ni * 128 + wn * 32 + j * 16 + q * 4);
+        }
+      }
+    }
+  };
+  auto unpack_half = [&]() {   // RB: rvb -> rv (columns j*16 + q*4 .. +3 of each (i, ni))
+    if constexpr (RB) {
+      #pragma unroll
+      for (int i = 0; i < 4; ++i)
         #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          rv[i][ni][j] = *(const f32x4*)(g.resid + rrow + n0 + ni * 128 + wn * 32 + j * 16 + q * 4);
+        for (int ni = 0; ni < 2; ++ni) {
+          const uint4 v = rvb[i][ni];
+          const auto x = __builtin_amdgcn_permlane16_swap(v.x, v.z, false, false);
+          const auto y = __builtin_amdgcn_permlane16_swap(v.y, v.w, false, false);
+          const bf16x4 x0 = __builtin_bit_cast(bf16x4, make_uint2(x[0], y[0]));
+          const bf16x4 x1 = __builtin_bit_cast(bf16x4, make_uint2(x[1], y[1]));
+          rv[i][ni][0] = f32x4{(float)x0[0], (float)x0[1], (float)x0[2], (float)x0[3]};
+          rv[i][ni][1] = f32x4{(float)x1[0], (float)x1[1], (float)x1[2], (float)x1[3]};
+        }
     }
   };
   __builtin_amdgcn_sched_barrier(0);
@@ -1189,6 +1213,7 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
   // column parameters are read from LDS where they are used (registers hold acc + one half's rows)
   float2* cst = (float2*)(smem + 16384);
   auto finish_half = [&](int mi) {
+    unpack_half();
     #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float2 st = make_float2(0.f, 1.f);
@@ -1211,7 +1236,11 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
           }
           const f32x4 bvv = *(const f32x4*)(smem + c * 4);
           const f32x4 bv = has_bias ? bvv : f32x4{0.f, 0.f, 0.f, 0.f};
-          const f32x4 o = (acc[mi][ni][i][j] + bv) + r;
+          f32x4 o = (acc[mi][ni][i][j] + bv) + r;
+          if constexpr (RB) {   // bf16 output: the statistics describe the rounded values
+            #pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = (float)(bf16)o[e];
+          }
           acc[mi][ni][i][j] = o;
           sum += (o[0] + o[1]) + (o[2] + o[3]);
         }
@@ -1243,12 +1272,12 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
       const long long row = (long long)(ok ? m : 0) * g.ldc;
       #pragma unroll
       for (int ni = 0; ni < 2; ++ni) {
-        if (ok) {
+        if (!RB && ok) {
           #pragma unroll
           for (int j = 0; j < 2; ++j)
             *(f32x4*)(g.Cf + row + n0 + ni * 128 + wn * 32 + j * 16 + q * 4) = acc[mi][ni][i][j];
         }
-        if (g.Ct) {
+        if (RB || g.Ct) {
           const f32x4 o0 = acc[mi][ni][i][0], o1 = acc[mi][ni][i][1];
           const bf16x4 x0 = {(bf16)o0[0], (bf16)o0[1], (bf16)o0[2], (bf16)o0[3]};
           const bf16x4 x1 = {(bf16)o1[0], (bf16)o1[1], (bf16)o1[2], (bf16)o1[3]};
@@ -1295,18 +1324,28 @@ int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
   if ((a.apart && a.apart_nt != 3) || (a.rpart && a.rpart_nt != 3) || (a.opart && a.N != 768)) return -3;
   dim3 grid((unsigned)(((a.M + 255) / 256) * (a.N / 256)));
   // OPT_GEMM_NONPERSIST (tests, A/B): the non-persistent LDS-staged kernel for every shape
-  if (sse_opt(OPT_GEMM_NONPERSIST)) {
+  if (sse_opt(OPT_GEMM_NONPERSIST) && !a.resid_t) {
     hipLaunchKernelGGL((gemm8_kernel<0, false, false>), grid, dim3(512), 0, s, a);
+  } else if (a.resid_t) {
+    // bf16 residual stream (folded post-LN path): bf16 out only
+    if (!a.Ct || a.Cf || a.resid || a.resid_rows || a.rstats) return -3;
+    if (a.rpart) {
+      if (a.opart) hipLaunchKernelGGL((gemm8r_kernel<true, true, true>), grid, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((gemm8r_kernel<true, false, true>), grid, dim3(512), 0, s, a);
+    } else {
+      if (a.opart) hipLaunchKernelGGL((gemm8r_kernel<false, true, true>), grid, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((gemm8r_kernel<false, false, true>), grid, dim3(512), 0, s, a);
+    }
   } else if (a.resid) {
     // residual GEMMs: fp32 out (Cf) required; the rstats form is the staged kernel's only
     if (!a.Cf || a.rstats || (a.opart && !a.rpart && a.rln_w)) {
       hipLaunchKernelGGL((gemm8_kernel<0, false, false>), grid, dim3(512), 0, s, a);
     } else if (a.rpart) {
-      if (a.opart) hipLaunchKernelGGL((gemm8r_kernel<true, true>), grid, dim3(512), 0, s, a);
-      else hipLaunchKernelGGL((gemm8r_kernel<true, false>), grid, dim3(512), 0, s, a);
+      if (a.opart) hipLaunchKernelGGL((gemm8r_kernel<true, true, false>), grid, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((gemm8r_kernel<true, false, false>), grid, dim3(512), 0, s, a);
     } else {
-      if (a.opart) hipLaunchKernelGGL((gemm8r_kernel<false, true>), grid, dim3(512), 0, s, a);
-      else hipLaunchKernelGGL((gemm8r_kernel<false, false>), grid, dim3(512), 0, s, a);
+      if (a.opart) hipLaunchKernelGGL((gemm8r_kernel<false, true, false>), grid, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((gemm8r_kernel<false, false, false>), grid, dim3(512), 0, s, a);
     }
   } else {
     // persistent: one block per CU (LDS-bound), at most one per tile

@@ -625,6 +625,8 @@ template int launch_layernorm<float, bf16>(const float*, const float*, const flo
                                            float*, bf16*, hipStream_t, float2*);
 template int launch_layernorm<bf16, bf16>(const bf16*, const float*, const float*, int, int, float, int, float*,
                                           bf16*, hipStream_t, float2*);
+template int launch_layernorm<bf16, float>(const bf16*, const float*, const float*, int, int, float, int, float*,
+                                           float*, hipStream_t, float2*);
 
 // LayerNorm -> MX-fp8 GEMM operand (pre-LN Whisper, SSE_DTYPE_FP8).  Block = 64 consecutive rows
 // (4 waves x 16 rows, one row per wave at a time, the layernorm_kernel arithmetic), so the block
@@ -745,7 +747,8 @@ int launch_mx_quantize(const float* x, int R, int K, int role, unsigned char* q,
 // partials, ln_part_stats), each element is first normalised exactly as layernorm_kernel would have
 // written it; the clip's per-frame statistics are formed once into LDS.
 constexpr int POOL_TMAX = 1024;   // frames whose statistics fit the LDS table (longer clips: per-frame loads)
-__global__ __launch_bounds__(256) void pool_mean_kernel(const float* __restrict__ x, int T, int H,
+template <typename TI>
+__global__ __launch_bounds__(256) void pool_mean_kernel(const TI* __restrict__ x, int T, int H,
                                                         float* __restrict__ out, long long out_stride,
                                                         const float2* __restrict__ st, const float* __restrict__ w,
                                                         const float* __restrict__ bb, const float2* __restrict__ lpart,
@@ -763,7 +766,7 @@ __global__ __launch_bounds__(256) void pool_mean_kernel(const float* __restrict_
   }
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   if (n < H) {
-    const float* xb = x + (long long)b * T * H + n;
+    const TI* xb = x + (long long)b * T * H + n;
     const f32x4 wn = ln ? *(const f32x4*)(w + n) : f32x4{1.f, 1.f, 1.f, 1.f};
     const f32x4 bn = ln ? *(const f32x4*)(bb + n) : f32x4{0.f, 0.f, 0.f, 0.f};
     auto add = [&](f32x4 v, int t) {
@@ -779,14 +782,14 @@ __global__ __launch_bounds__(256) void pool_mean_kernel(const float* __restrict_
     };
     int t = wv;
     for (; t + 12 < T; t += 16) {   // 4 frames of this wave in flight
-      const f32x4 v0 = *(const f32x4*)(xb + (long long)t * H), v1 = *(const f32x4*)(xb + (long long)(t + 4) * H);
-      const f32x4 v2 = *(const f32x4*)(xb + (long long)(t + 8) * H), v3 = *(const f32x4*)(xb + (long long)(t + 12) * H);
+      const f32x4 v0 = load4<TI>(xb + (long long)t * H), v1 = load4<TI>(xb + (long long)(t + 4) * H);
+      const f32x4 v2 = load4<TI>(xb + (long long)(t + 8) * H), v3 = load4<TI>(xb + (long long)(t + 12) * H);
       add(v0, t);
       add(v1, t + 4);
       add(v2, t + 8);
       add(v3, t + 12);
     }
-    for (; t < T; t += 4) add(*(const f32x4*)(xb + (long long)t * H), t);
+    for (; t < T; t += 4) add(load4<TI>(xb + (long long)t * H), t);
   }
   part[wv][lane * 4 + 0] = s0;
   part[wv][lane * 4 + 1] = s1;
@@ -797,13 +800,18 @@ __global__ __launch_bounds__(256) void pool_mean_kernel(const float* __restrict_
   if (nc < H) out[b * out_stride + nc] = (float)((part[0][c] + part[1][c] + part[2][c] + part[3][c]) / T);
 }
 
-int launch_pool_mean(const float* x, int B, int T, int H, float* out, long long out_stride, hipStream_t s,
+template <typename TI>
+int launch_pool_mean(const TI* x, int B, int T, int H, float* out, long long out_stride, hipStream_t s,
                      const float2* st, const float* w, const float* b, const float2* part, int nt, float eps) {
   if (H % 4) return -3;
-  hipLaunchKernelGGL(pool_mean_kernel, dim3((H + 255) / 256, B), dim3(256), 0, s, x, T, H, out, out_stride, st, w, b,
-                     part, nt, eps);
+  hipLaunchKernelGGL(pool_mean_kernel<TI>, dim3((H + 255) / 256, B), dim3(256), 0, s, x, T, H, out, out_stride, st, w,
+                     b, part, nt, eps);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+template int launch_pool_mean<float>(const float*, int, int, int, float*, long long, hipStream_t, const float2*,
+                                     const float*, const float*, const float2*, int, float);
+template int launch_pool_mean<bf16>(const bf16*, int, int, int, float*, long long, hipStream_t, const float2*,
+                                    const float*, const float*, const float2*, int, float);
 
 // ---------------------------------------------------------------------------------------
 // K5/K6/K11: attention, flash style.  Block = (64 queries, head, clip), 4 waves x 16 queries.

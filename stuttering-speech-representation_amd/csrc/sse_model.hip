@@ -528,7 +528,8 @@ double gbytes(const GemmArgs& g, int amode = AMODE_SEG, int groups = 1) {
   const double mn = (double)g.M * g.N * groups;
   const double b = (double)g.N * g.K * groups * e;
   const double c = mn * ((g.Cf ? 4.0 : 0.0) + (g.Ct ? e : 0.0));
-  const double r = g.resid ? (g.resid_rows ? (double)g.resid_rows * g.N * groups * 4.0 : mn * 4.0) : 0.0;
+  const double r = g.resid ? (g.resid_rows ? (double)g.resid_rows * g.N * groups * 4.0 : mn * 4.0)
+                           : (g.resid_t ? mn * 2.0 : 0.0);
   return a + b + c + r;
 }
 
@@ -639,14 +640,15 @@ struct Sink {
   }
   // hidden state = LayerNorm(x) with per-row stats st, or per-256-column partials part [rows][nt],
   // already computed (x itself un-normalised)
-  int emit_ln(int idx, const float* x, const float2* st, const float* w, const float* b, float eps,
+  template <typename TI>
+  int emit_ln(int idx, const TI* x, const float2* st, const float* w, const float* b, float eps,
               const float2* part = nullptr, int nt = 0) const {
     for (int i = 0; i < n_ids; ++i)
       if (ids[i] == idx)
-        RC(launch_pool_mean(x, B, T, H, pooled + (size_t)i * H, (long long)n_ids * H, s, st, w, b, part, nt, eps));
+        RC(launch_pool_mean<TI>(x, B, T, H, pooled + (size_t)i * H, (long long)n_ids * H, s, st, w, b, part, nt, eps));
     if (hs)
-      RC((launch_layernorm<float, float>(x, w, b, B * T, H, eps, ACT_NONE, hs + (size_t)idx * B * T * H,
-                                         (float*)nullptr, s)));
+      RC((launch_layernorm<TI, float>(x, w, b, B * T, H, eps, ACT_NONE, hs + (size_t)idx * B * T * H,
+                                      (float*)nullptr, s)));
     return 0;
   }
 };
@@ -758,16 +760,19 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
   T* ctx = (T*)(ws + w.ctx);
   T* ff = (T*)(ws + w.ff);
   float* hf = c.stable_layer_norm ? (float*)(ws + w.hf) : nullptr;
-  // bf16 post-LN (WavLM-base): no LayerNorm kernel inside the layer loop.  The residual GEMMs (oproj,
-  // ffn2) write the un-normalised sum x in fp32 (the residual stream), its bf16 copy into xb (the next
-  // GEMM's A operand) and per-256-column partial statistics (p1 / p2); the consumers apply the
-  // LayerNorm from those partials: QKV / FFN1 through folded weights (GemmArgs.apart:
-  // rstd (acc - mean acol) + b'), the next residual GEMM on its residual load (rpart), the pool on
-  // its loads.  OPT_NO_LNFOLD restores the materialised flow (LayerNorm kernels; A/B tests).
+  // bf16 post-LN (WavLM-base): no LayerNorm kernel inside the layer loop, and the residual stream
+  // in bf16.  The residual GEMMs (oproj, ffn2) write the un-normalised sum in bf16 -- xs after the
+  // attention, xb after the FFN: at once the residual of the next residual GEMM and the A operand
+  // of the next GEMM -- plus per-256-column partial statistics of the rounded values (p1 / p2);
+  // the consumers apply the LayerNorm from those partials: QKV / FFN1 through folded weights
+  // (GemmArgs.apart: rstd (acc - mean acol) + b'), the next residual GEMM on its residual load
+  // (rpart), the pool on its loads.  OPT_NO_LNFOLD restores the materialised flow (LayerNorm
+  // kernels, fp32 residual; A/B tests).
   const bool lnfold = sizeof(T) == 2 && m->ln_fold && !sse_opt(OPT_NO_LNFOLD);
   const int nt = H / 256;
   float2* p1 = (float2*)(ws + w.p1);
   float2* p2 = (float2*)(ws + w.p2);
+  T* xs = xt;   // bf16 residual sum after the attention (xt, the projection output, is free by now)
   for (int l = 0; l < c.layers; ++l) {
     const LayerW& Lw = m->layers[l];
     const LayerW* Lp = l > 0 ? &m->layers[l - 1] : nullptr;
@@ -792,12 +797,13 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     g = GemmArgs{};
     g.A = ctx; g.B = m->ptr(Lw.o_w); g.M = M; g.N = H; g.K = H; g.rows_per_seg = M; g.lda = H;
     g.bias = m->ptr<float>(Lw.o_b); g.resid = x; g.Cf = x; g.ldc = H; g.zero = zero;
-    if (lnfold) {
-      if (l > 0) {   // x holds the previous layer's un-normalised sum: its final LN applied here
+    if (lnfold) {   // residual = xb: layer 0 the encoder LN output, later the previous layer's bf16 sum
+      g.resid = nullptr; g.Cf = nullptr; g.resid_t = (const bf16*)xb;
+      if (l > 0) {   // the previous layer's final LN applied on the residual load
         g.rpart = p2; g.rpart_nt = nt; g.ln_eps = eps;
         g.rln_w = m->ptr<float>(Lp->ln2_w); g.rln_b = m->ptr<float>(Lp->ln2_b);
       }
-      g.Ct = xb; g.opart = p1;
+      g.Ct = xs; g.opart = p1;
     }
     RC(prof(m, s, "gemm:oproj", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     if (!lnfold) {
@@ -811,8 +817,8 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     g = GemmArgs{};
     g.A = xb; g.B = m->ptr(Lw.f1_w); g.M = M; g.N = F; g.K = H; g.rows_per_seg = M; g.lda = H;
     g.bias = m->ptr<float>(Lw.f1_b); g.Ct = ff; g.ldc = F; g.act = gelu_rounded_act<T>(); g.zero = zero;
-    if (lnfold) {   // xb = bf16 of the un-normalised attention sum: the attention LN folded
-      g.B = m->ptr(Lw.f1_wf); g.bias = m->ptr<float>(Lw.f1_bf); g.acol = m->ptr<float>(Lw.f1_c);
+    if (lnfold) {   // xs = bf16 of the un-normalised attention sum: the attention LN folded
+      g.A = xs; g.B = m->ptr(Lw.f1_wf); g.bias = m->ptr<float>(Lw.f1_bf); g.acol = m->ptr<float>(Lw.f1_c);
       g.apart = p1; g.apart_nt = nt; g.ln_eps = eps;
     }
     RC(prof(m, s, "gemm:ffn1", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
@@ -820,12 +826,13 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     g.A = ff; g.B = m->ptr(Lw.f2_w); g.M = M; g.N = H; g.K = F; g.rows_per_seg = M; g.lda = F;
     g.bias = m->ptr<float>(Lw.f2_b); g.resid = x; g.Cf = x; g.ldc = H; g.zero = zero;
     if (lnfold) {
+      g.resid = nullptr; g.Cf = nullptr; g.resid_t = (const bf16*)xs;
       g.rpart = p1; g.rpart_nt = nt; g.ln_eps = eps; g.rln_w = m->ptr<float>(Lw.ln1_w); g.rln_b = m->ptr<float>(Lw.ln1_b);
       g.Ct = xb; g.opart = p2;
     }
     RC(prof(m, s, "gemm:ffn2", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     if (lnfold) {
-      RC(sink.emit_ln(l + 1, x, nullptr, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), eps, p2, nt));
+      RC(sink.emit_ln<T>(l + 1, xb, nullptr, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), eps, p2, nt));
       continue;
     }
     if (!c.stable_layer_norm) {
