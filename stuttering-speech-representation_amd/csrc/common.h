@@ -183,6 +183,9 @@ struct GemmArgs {
   // bf16 residual [M][ldc] (instead of resid; folded post-LN path: the residual stream is kept in
   // bf16 and the output is bf16 Ct only)
   const bf16* resid_t;
+  // split-bf16 output (SSE_DTYPE_BF16X3): Ct is the next GEMM's tripled operand [M][3N] (ldc = 3N),
+  // row = [hi | lo | hi] with hi = bf16(v), lo = bf16(v - hi)
+  int ct3;
 };
 
 // (mean, rstd) of a row of 256 * NT values from its per-tile partials (mean_t, M2_t), Chan's pairwise

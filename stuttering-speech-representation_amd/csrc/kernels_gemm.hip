@@ -333,7 +333,7 @@ int launch_any(const GemmArgs& a, int amode, int groups, hipStream_t s) {
   // Otherwise 128x128, 4 waves of 64x64, 2 stages (2 blocks/CU).  OPT_GEMM_CFG (tests, A/B):
   // 1 = never 256x256, 2 = 256x128 3-stage ring.
   const int force = sse_opt(OPT_GEMM_CFG);
-  if (a.apart || a.rpart || a.opart || a.resid_t) {   // folded-LayerNorm epilogues exist in the gemm8 kernels only
+  if (a.apart || a.rpart || a.opart || a.resid_t || a.ct3) {   // folded-LayerNorm epilogues exist in the gemm8 kernels only
     if constexpr (sizeof(T) == 2)
       if (amode == AMODE_SEG && groups == 1 && a.N % 256 == 0 && a.K % 64 == 0) return launch_gemm8_bf16(a, s);
     return -3;

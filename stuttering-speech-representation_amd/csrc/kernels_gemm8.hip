@@ -692,7 +692,7 @@ constexpr int G8P_SMEM = G8_OPS + 2 * G8P_EP;
 //   o = act(rstd_m * acc + (bias[n] - rstd_m mean_m acol[n]))   (folded LayerNorm of A, GemmArgs.apart)
 //   o = act(acc + bias[n])                                        (otherwise: rstd = 1 and the acol term
 //                                                                  is not formed, bit-identical to a plain add)
-template <int ACT>
+template <int ACT, bool CT3>
 SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, int n0, int wm, int wn, int q,
                           int r16, const char* ep, bool has_bias, bool fold) {
   f32x4 bv[2][2], ac[2][2];
@@ -760,9 +760,23 @@ SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, i
           const uint2 X = __builtin_bit_cast(uint2, x0), Y = __builtin_bit_cast(uint2, x1);
           const auto s0 = __builtin_amdgcn_permlane16_swap(X.x, Y.x, false, false);
           const auto s1 = __builtin_amdgcn_permlane16_swap(X.y, Y.y, false, false);
+          const long long c = n0 + ni * 128 + wn * 32 + (q & 1) * 16 + (q >> 1) * 8;
           if (ok) {
             const uint4 v = make_uint4(s0[0], s1[0], s0[1], s1[1]);
-            *(uint4*)((bf16*)g.Ct + row + n0 + ni * 128 + wn * 32 + (q & 1) * 16 + (q >> 1) * 8) = v;
+            *(uint4*)((bf16*)g.Ct + row + c) = v;
+            if constexpr (CT3) *(uint4*)((bf16*)g.Ct + row + 2 * g.N + c) = v;
+          }
+          if constexpr (CT3) {   // lo plane: bf16(v - hi)
+            bf16x4 l0, l1;
+            #pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              l0[e] = (bf16)(o0[e] - (float)x0[e]);
+              l1[e] = (bf16)(o1[e] - (float)x1[e]);
+            }
+            const uint2 LX = __builtin_bit_cast(uint2, l0), LY = __builtin_bit_cast(uint2, l1);
+            const auto t0 = __builtin_amdgcn_permlane16_swap(LX.x, LY.x, false, false);
+            const auto t1 = __builtin_amdgcn_permlane16_swap(LX.y, LY.y, false, false);
+            if (ok) *(uint4*)((bf16*)g.Ct + row + g.N + c) = make_uint4(t0[0], t1[0], t0[1], t1[1]);
           }
         }
       }
@@ -782,7 +796,7 @@ SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, i
 // flight -- the next tile's first K-tile waits vmcnt(2n + S) (S = store instructions issued after
 // its prologue), so it needs only the prologue loads and the stores drain under its MFMAs.
 // ======================================================================================
-template <int ACT>
+template <int ACT, bool CT3 = false>
 __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
   __shared__ __attribute__((aligned(16))) char smem[G8P_SMEM];   // operands | 2 epilogue slots: the ONLY shared object
   const int lane = threadIdx.x & 63;
@@ -795,7 +809,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
   const int G = gridDim.x, b = blockIdx.x;
   // stores per wave of one full tile (the count the next tile's first K-tile may leave in
   // flight); under-counting is safe, so it is capped to keep 2n + S within vmcnt's 6 bits
-  const int s_full = min(32 * (g.Cf ? 1 : 0) + 16 * (g.Ct ? 1 : 0), 54);   // 54 + 9 <= 63
+  const int s_full = min(32 * (g.Cf ? 1 : 0) + (CT3 ? 48 : 16) * (g.Ct ? 1 : 0), 54);   // 54 + 9 <= 63
   const bool has_bias = g.bias != nullptr, fold = g.apart != nullptr;
 
   int round = 0;
@@ -975,7 +989,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
       setup(next);
       for (int k = -6; k < 0; ++k) issue(k);
     }
-    g8p_epilogue<ACT>(g, acc, m0, n0, wm, wn, q, r16, smem + G8_OPS + slot * G8P_EP, has_bias, fold);
+    g8p_epilogue<ACT, CT3>(g, acc, m0, n0, wm, wn, q, r16, smem + G8_OPS + slot * G8P_EP, has_bias, fold);
     if (next < 0) break;
     slot ^= 1;
     S = m0 + 256 <= M ? s_full : 0;
@@ -1324,7 +1338,8 @@ int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
   if ((a.apart && a.apart_nt != 3) || (a.rpart && a.rpart_nt != 3) || (a.opart && a.N != 768)) return -3;
   dim3 grid((unsigned)(((a.M + 255) / 256) * (a.N / 256)));
   // OPT_GEMM_NONPERSIST (tests, A/B): the non-persistent LDS-staged kernel for every shape
-  if (sse_opt(OPT_GEMM_NONPERSIST) && !a.resid_t) {
+  if (a.ct3 && (a.resid || a.resid_t || !a.Ct)) return -3;   // split-bf16 output: persistent kernel only
+  if (sse_opt(OPT_GEMM_NONPERSIST) && !a.resid_t && !a.ct3) {
     hipLaunchKernelGGL((gemm8_kernel<0, false, false>), grid, dim3(512), 0, s, a);
   } else if (a.resid_t) {
     // bf16 residual stream (folded post-LN path): bf16 out only
@@ -1356,7 +1371,14 @@ int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
       return -2;
     const int n_tiles = (int)grid.x;
     const int G = n_tiles < cus[dev] ? n_tiles : cus[dev];
-    if (a.act == ACT_GELU)
+    if (a.ct3) {   // split-bf16 output (bf16x3 path): erf-GELU or none
+      if (a.act == ACT_GELU)
+        hipLaunchKernelGGL((gemm8p_kernel<ACT_GELU, true>), dim3(G), dim3(512), 0, s, a, n_tiles);
+      else if (a.act == ACT_NONE)
+        hipLaunchKernelGGL((gemm8p_kernel<ACT_NONE, true>), dim3(G), dim3(512), 0, s, a, n_tiles);
+      else
+        return -3;
+    } else if (a.act == ACT_GELU)
       hipLaunchKernelGGL(gemm8p_kernel<ACT_GELU>, dim3(G), dim3(512), 0, s, a, n_tiles);
     else if (a.act == ACT_GELU_FAST)
       hipLaunchKernelGGL(gemm8p_kernel<ACT_GELU_FAST>, dim3(G), dim3(512), 0, s, a, n_tiles);

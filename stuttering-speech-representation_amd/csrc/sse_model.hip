@@ -133,6 +133,27 @@ struct Arena {
     return off;
   }
   size_t put_f32(const float* src, size_t n) { return put(src, n * 4); }
+  // split-bf16 GEMM weight (SSE_DTYPE_BF16X3): rows of nblk blocks of blk values (a conv tap is a block)
+  // -> per block [hi | hi | lo], hi = bf16(w), lo = bf16(w - hi): matched to activation rows
+  // [hi | lo | hi], the K-sum is hi*hi + lo*hi + hi*lo
+  size_t put_x3(const std::vector<float>& v, size_t rows, int nblk, int blk) {
+    std::vector<uint16_t> h(v.size() * 3);
+    for (size_t r = 0; r < rows; ++r)
+      for (int j = 0; j < nblk; ++j)
+        for (int c = 0; c < blk; ++c) {
+          const float w = v[(r * nblk + j) * blk + c];
+          const uint16_t hi = f2bf_bits(w);
+          float hf;
+          const uint32_t u = (uint32_t)hi << 16;
+          std::memcpy(&hf, &u, 4);
+          const uint16_t lo = f2bf_bits(w - hf);
+          uint16_t* o = h.data() + (r * nblk + j) * 3 * (size_t)blk;
+          o[c] = hi;
+          o[blk + c] = hi;
+          o[2 * blk + c] = lo;
+        }
+    return put(h.data(), h.size() * 2);
+  }
   size_t put_elem(const std::vector<float>& v, bool bf) {
     if (!bf) return put(v.data(), v.size() * 4);
     std::vector<uint16_t> h(v.size());
@@ -219,6 +240,7 @@ struct sse_model {
 
   template <typename X = void> const X* ptr(size_t off) const { return (const X*)(dmem + off); }
   bool bf() const { return dtype == SSE_DTYPE_BF16 || dtype == SSE_DTYPE_FP8; }   // bf16 activations
+  bool x3() const { return dtype == SSE_DTYPE_BF16X3; }   // split-bf16 GEMMs, fp32 activations
   bool mx() const { return dtype == SSE_DTYPE_FP8; }   // MX-fp8 encoder-layer GEMMs (Whisper)
 };
 
@@ -261,7 +283,7 @@ int build_wavlm(sse_model* m, Blob& bl, Arena& ar) {
       for (int o = 0; o < co; ++o)
         for (int ci = 0; ci < cin; ++ci)
           for (int j = 0; j < k; ++j) t[((size_t)o * k + j) * cin + ci] = w[((size_t)o * cin + ci) * k + j];
-      m->conv_w[i] = ar.put_elem(t, BF);
+      m->conv_w[i] = m->x3() ? ar.put_x3(t, co, k, cin) : ar.put_elem(t, BF);
     }
     m->conv_b[i] = b ? ar.put_f32(b, co) : 0;
     m->has_conv_b = b != nullptr;
@@ -285,7 +307,8 @@ int build_wavlm(sse_model* m, Blob& bl, Arena& ar) {
   if (fplw) {
     m->fp_ln_w = ar.put_f32(fplw, C);
     m->fp_ln_b = ar.put_f32(fplb, C);
-    m->fp_w = ar.put_elem(std::vector<float>(fpw, fpw + (size_t)H * C), BF);
+    m->fp_w = m->x3() ? ar.put_x3(std::vector<float>(fpw, fpw + (size_t)H * C), H, 1, C)
+                      : ar.put_elem(std::vector<float>(fpw, fpw + (size_t)H * C), BF);
     m->fp_b = ar.put_f32(fpb, H);
     // weight_norm(dim=2): w[o][c][j] = g[j] * v[o][c][j] / ||v[:, :, j]||  (fp64 norm), then
     // per group [cg_out][j*cg + c_in]
@@ -338,18 +361,22 @@ int build_wavlm(sse_model* m, Blob& bl, Arena& ar) {
         for (int d = 0; d < 64; ++d) qkv[row * H + hh * 64 + d] = gw[o * 64 + d];
         qkvb[row] = gbb[o];
       }
-    L.qkv_w = ar.put_elem(qkv, BF);
+    const bool X3 = m->x3();
+    L.qkv_w = X3 ? ar.put_x3(qkv, ldq, 1, H) : ar.put_elem(qkv, BF);
     L.qkv_b = ar.put_f32(qkvb.data(), ldq);
-    L.o_w = ar.put_elem(std::vector<float>(ow, ow + (size_t)H * H), BF);
+    L.o_w = X3 ? ar.put_x3(std::vector<float>(ow, ow + (size_t)H * H), H, 1, H)
+               : ar.put_elem(std::vector<float>(ow, ow + (size_t)H * H), BF);
     L.o_b = ar.put_f32(ob, H);
     L.g_const = ar.put_f32(gc, nh);
     L.g_w = ar.put_f32(gw, 8 * 64);
     L.g_b = ar.put_f32(gbb, 8);
     L.ln1_w = ar.put_f32(l1w, H);
     L.ln1_b = ar.put_f32(l1b, H);
-    L.f1_w = ar.put_elem(std::vector<float>(f1w, f1w + (size_t)F * H), BF);
+    L.f1_w = X3 ? ar.put_x3(std::vector<float>(f1w, f1w + (size_t)F * H), F, 1, H)
+                : ar.put_elem(std::vector<float>(f1w, f1w + (size_t)F * H), BF);
     L.f1_b = ar.put_f32(f1b, F);
-    L.f2_w = ar.put_elem(std::vector<float>(f2w, f2w + (size_t)H * F), BF);
+    L.f2_w = X3 ? ar.put_x3(std::vector<float>(f2w, f2w + (size_t)H * F), H, 1, F)
+                : ar.put_elem(std::vector<float>(f2w, f2w + (size_t)H * F), BF);
     L.f2_b = ar.put_f32(f2b, H);
     L.ln2_w = ar.put_f32(l2w, H);
     L.ln2_b = ar.put_f32(l2b, H);
@@ -849,6 +876,152 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
   return 0;
 }
 
+// ---- SSE_DTYPE_BF16X3: the fp32 path with split-bf16 GEMMs ----------------------------------
+// Every GEMM operand is stored tripled, a row [hi | lo | hi] of 3K bf16 (hi = bf16(v), lo =
+// bf16(v - hi)); the weights [hi | hi | lo] per K-block (Arena::put_x3).  The bf16 8-phase kernels
+// then run unchanged on K' = 3K and accumulate hi*hi + lo*hi + hi*lo in fp32 (the dropped lo*lo is
+// ~2^-16 relative).  Strided convs keep their overlapping-row addressing: a frame is 3C values, a
+// window of k frames k*3C.  conv0 + GroupNorm + GELU, the positional conv and the attention core
+// (scores, softmax, P.V) run in exact fp32 as in the fp32 path; LayerNorms read / write fp32 and
+// tripled rows.
+struct X3Ws {
+  size_t zero, norm, part, ss, c0, bufA, bufB, x, xt, xb, qkv, ctx, ctx3, ff;
+};
+
+X3Ws x3_plan(const sse_model* m, int B, int L, Plan& p) {
+  const sse_cfg& c = m->cfg;
+  int Ts[8];
+  const int T = wavlm_frames(c, L, Ts);
+  const size_t M = (size_t)B * T;
+  const int H = c.hidden, C0 = c.conv_dim[0];
+  size_t maxA = 0, maxB = 0;
+  for (int i = 0; i < c.n_conv; ++i) {
+    const size_t sz = (size_t)B * Ts[i] * c.conv_dim[i] * 6;
+    if (i % 2 == 0) maxA = sz > maxA ? sz : maxA; else maxB = sz > maxB ? sz : maxB;
+  }
+  const int Cl = c.conv_dim[c.n_conv - 1];
+  X3Ws w;
+  w.zero = p.add(256);
+  w.norm = p.add((size_t)B * 8);
+  w.part = p.add(conv0_moments_bytes(B));
+  w.ss = p.add((size_t)B * C0 * 8);
+  w.c0 = p.add((size_t)B * Ts[0] * C0 * 4);
+  w.bufA = p.add(maxA);
+  w.bufB = p.add(maxB);
+  w.x = p.add(M * H * 4);
+  w.xt = p.add(M * H * 4);
+  w.xb = p.add(M * (size_t)(H > Cl ? H : Cl) * 6);
+  w.qkv = p.add(M * (size_t)(((3 * H + 8 * c.heads + 255) / 256) * 256) * 4);
+  w.ctx = p.add(M * H * 4);
+  w.ctx3 = p.add(M * H * 6);
+  w.ff = p.add(M * (size_t)c.ffn * 6);
+  return w;
+}
+
+int wavlm_forward_x3(sse_model* m, const float* wave, int B, int L, const Sink& sink, char* ws, hipStream_t s) {
+  const sse_cfg& c = m->cfg;
+  Plan p;
+  const X3Ws w = x3_plan(m, B, L, p);
+  int Ts[8];
+  const int Tf = wavlm_frames(c, L, Ts);
+  const int H = c.hidden, nh = c.heads, F = c.ffn;
+  const int M = B * Tf;
+  const float eps = c.ln_eps;
+  void* zero = ws + w.zero;
+  if (hipMemsetAsync(zero, 0, 256, s) != hipSuccess) return SSE_ERR_HIP;
+  const float* norm = nullptr;
+  if (c.do_normalize) {
+    RC(launch_wave_stats(wave, B, L, (float*)(ws + w.norm), s));
+    norm = (const float*)(ws + w.norm);
+  }
+  // split-bf16 GEMM: logical K (the FLOP count), physical operands K' = 3K
+  auto gemm3 = [&](const char* tag, GemmArgs& g, int Klog) {
+    g.zero = zero;
+    return prof(m, s, tag, 2.0 * g.M * (double)g.N * Klog, gbytes<bf16>(g), [&] { return launch_gemm8_bf16(g, s); });
+  };
+  // ---- conv feature encoder: conv0 + GroupNorm + GELU in fp32, then tripled ----
+  const int C0 = c.conv_dim[0];
+  float* c0 = (float*)(ws + w.c0);
+  const float* b0 = m->conv_b[0] ? m->ptr<float>(m->conv_b[0]) : nullptr;
+  bf16* bufs[2] = {(bf16*)(ws + w.bufA), (bf16*)(ws + w.bufB)};
+  RC(prof(m, s, "conv0_gn", 2.0 * B * (double)Ts[0] * C0 * c.conv_kernel[0], 0, [&] {
+    return launch_conv0_gn<float>(wave, B, L, norm, m->ptr<float>(m->conv_w[0]), b0, C0, c.conv_kernel[0],
+                                  c.conv_stride[0], Ts[0], m->ptr<float>(m->conv_ln_w[0]), m->ptr<float>(m->conv_ln_b[0]),
+                                  1e-5f, (double*)(ws + w.part), (float2*)(ws + w.ss), c0, s); }));
+  RC(launch_split3(c0, (long long)B * Ts[0], C0, bufs[0], s));
+  for (int i = 1; i < c.n_conv; ++i) {
+    const int cin = c.conv_dim[i - 1], co = c.conv_dim[i], k = c.conv_kernel[i], st = c.conv_stride[i];
+    GemmArgs g{};
+    g.A = bufs[(i - 1) & 1]; g.B = m->ptr(m->conv_w[i]);
+    g.M = B * Ts[i]; g.N = co; g.K = k * 3 * cin;
+    g.rows_per_seg = Ts[i]; g.seg_stride = (long long)Ts[i - 1] * 3 * cin; g.lda = (long long)st * 3 * cin;
+    g.bias = m->conv_b[i] ? m->ptr<float>(m->conv_b[i]) : nullptr;
+    g.Ct = bufs[i & 1]; g.ct3 = 1; g.ldc = 3 * co; g.act = ACT_GELU;
+    RC(gemm3("gemm:conv", g, k * cin));
+  }
+  const bf16* feat = bufs[(c.n_conv - 1) & 1];
+  const int C = c.conv_dim[c.n_conv - 1];
+  float* x = (float*)(ws + w.x);
+  float* xt = (float*)(ws + w.xt);
+  bf16* xb = (bf16*)(ws + w.xb);
+  // ---- feature projection ----
+  RC(launch_layernorm_x3(feat, true, m->ptr<float>(m->fp_ln_w), m->ptr<float>(m->fp_ln_b), M, C, eps, nullptr, xb, s));
+  {
+    GemmArgs g{};
+    g.A = xb; g.B = m->ptr(m->fp_w); g.M = M; g.N = H; g.K = 3 * C; g.rows_per_seg = M; g.lda = 3 * C;
+    g.bias = m->ptr<float>(m->fp_b); g.Cf = x; g.ldc = H;
+    RC(gemm3("gemm:proj", g, C));
+  }
+  if (hipMemcpyAsync(xt, x, (size_t)M * H * 4, hipMemcpyDeviceToDevice, s) != hipSuccess) return SSE_ERR_HIP;
+  // ---- positional conv embedding in exact fp32: x = x + gelu(conv(x) + b) ----
+  {
+    const int G = c.pos_groups, cg = H / G, K = c.pos_kernel;
+    GemmArgs g{};
+    g.A = xt; g.B = m->ptr(m->pos_w); g.M = M; g.N = cg; g.K = K * cg;
+    g.rows_per_seg = Tf; g.T_in = Tf; g.stride = 1; g.pad = K / 2; g.cin = cg; g.ld_in = H;
+    g.bias = m->ptr<float>(m->pos_b); g.resid = x; g.Cf = x; g.ldc = H; g.act = ACT_GELU; g.zero = zero;
+    RC(prof(m, s, "gemm_conv:posconv", gflops(g, G), gbytes<float>(g, AMODE_CONV, G),
+            [&] { return launch_gemm<float>(g, AMODE_CONV, G, s); }));
+  }
+  RC(launch_layernorm_x3(x, false, m->ptr<float>(m->enc_ln_w), m->ptr<float>(m->enc_ln_b), M, H, eps, x, xb, s));
+  RC(sink.emit(0, x));
+  float* qkv = (float*)(ws + w.qkv);
+  float* ctx = (float*)(ws + w.ctx);
+  bf16* ctx3 = (bf16*)(ws + w.ctx3);
+  bf16* ff = (bf16*)(ws + w.ff);
+  for (int l = 0; l < c.layers; ++l) {
+    const LayerW& Lw = m->layers[l];
+    GemmArgs g{};
+    g.A = xb; g.B = m->ptr(Lw.qkv_w); g.M = M; g.N = m->ldq; g.K = 3 * H;
+    g.rows_per_seg = M; g.lda = 3 * H; g.bias = m->ptr<float>(Lw.qkv_b); g.Cf = qkv; g.ldc = m->ldq;
+    g.zero = zero;
+    RC(prof(m, s, "gemm:qkv", 2.0 * M * (3.0 * H + 8.0 * nh) * H, gbytes<bf16>(g),
+            [&] { return launch_gemm8_bf16(g, s); }));
+    AttnArgs a{};
+    a.qkv = qkv; a.out = ctx; a.T = Tf; a.H = H; a.nh = nh; a.ldq = m->ldq; a.scale = 0.125f;
+    a.gconst = m->ptr<float>(Lw.g_const); a.relb = m->ptr<float>(m->relb); a.maxd = MAXD;
+    RC(prof(m, s, "attn", 4.0 * B * (double)Tf * Tf * H, (double)B * Tf * (4.0 * H + 8.0 * nh) * 4.0,
+            [&] { return launch_attention<float>(a, B, s); }));
+    RC(launch_split3(ctx, M, H, ctx3, s));
+    g = GemmArgs{};
+    g.A = ctx3; g.B = m->ptr(Lw.o_w); g.M = M; g.N = H; g.K = 3 * H; g.rows_per_seg = M; g.lda = 3 * H;
+    g.bias = m->ptr<float>(Lw.o_b); g.resid = x; g.Cf = x; g.ldc = H;
+    RC(gemm3("gemm:oproj", g, H));
+    RC(launch_layernorm_x3(x, false, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, x, xb, s));
+    g = GemmArgs{};
+    g.A = xb; g.B = m->ptr(Lw.f1_w); g.M = M; g.N = F; g.K = 3 * H; g.rows_per_seg = M; g.lda = 3 * H;
+    g.bias = m->ptr<float>(Lw.f1_b); g.Ct = ff; g.ct3 = 1; g.ldc = 3 * F; g.act = ACT_GELU;
+    RC(gemm3("gemm:ffn1", g, H));
+    g = GemmArgs{};
+    g.A = ff; g.B = m->ptr(Lw.f2_w); g.M = M; g.N = H; g.K = 3 * F; g.rows_per_seg = M; g.lda = 3 * F;
+    g.bias = m->ptr<float>(Lw.f2_b); g.resid = x; g.Cf = x; g.ldc = H;
+    RC(gemm3("gemm:ffn2", g, F));
+    RC(launch_layernorm_x3(x, false, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, H, eps, x, xb, s));
+    RC(sink.emit(l + 1, x));
+  }
+  return 0;
+}
+
 // The reference's 1-token decoder pass (REF/whisper_embeddings_large.py:257-262): input id 0 at
 // position 0, cross-attending to the encoder's last_hidden_state enc [B*Tq][D] (type T).  Rows
 // are clips (M = B); the K|V projection of the encoder output is the one large GEMM per layer.
@@ -1027,7 +1200,9 @@ int forward(sse_model* m, const float* d_in, int B, int L, const Sink& sink, voi
   if (hipGetDevice(&dev) != hipSuccess) return SSE_ERR_HIP;
   if (dev != m->device && hipSetDevice(m->device) != hipSuccess) return SSE_ERR_HIP;
   int rc;
-  if (m->cfg.kind == SSE_KIND_WAVLM)
+  if (m->cfg.kind == SSE_KIND_WAVLM && m->x3())
+    rc = wavlm_forward_x3(m, d_in, B, L, sink, (char*)d_ws, s);
+  else if (m->cfg.kind == SSE_KIND_WAVLM)
     rc = m->bf() ? wavlm_forward<bf16>(m, d_in, B, L, sink, (char*)d_ws, s)
                  : wavlm_forward<float>(m, d_in, B, L, sink, (char*)d_ws, s);
   else
@@ -1105,8 +1280,13 @@ size_t sse_weight_floats(const sse_cfg* cfg) {
 int sse_model_create(const sse_cfg* cfg, const float* host_weights, size_t nbytes, int device, int dtype,
                      sse_model** out) {
   if (!out || !host_weights || !cfg_valid(cfg) ||
-      (dtype != SSE_DTYPE_F32 && dtype != SSE_DTYPE_BF16 && dtype != SSE_DTYPE_FP8))
+      (dtype != SSE_DTYPE_F32 && dtype != SSE_DTYPE_BF16 && dtype != SSE_DTYPE_FP8 && dtype != SSE_DTYPE_BF16X3))
     return SSE_ERR_INVALID;
+  // split-bf16: WavLM "group" frontend + post-LN encoder (WavLM-base); every GEMM N % 256 == 0
+  if (dtype == SSE_DTYPE_BF16X3 &&
+      (cfg->kind != SSE_KIND_WAVLM || cfg->feat_norm_layer || cfg->stable_layer_norm || cfg->hidden % 256 ||
+       cfg->ffn % 256 || cfg->conv_dim[0] != 512 || cfg->conv_bias))
+    return SSE_ERR_UNSUPPORTED;
   // MX-fp8 GEMMs: N % 256 and K % 128 for QKV (3D x D), fc1 (F x D), fc2 (D x F)
   if (dtype == SSE_DTYPE_FP8 && (cfg->kind != SSE_KIND_WHISPER || cfg->hidden % 256 || cfg->ffn % 256))
     return SSE_ERR_UNSUPPORTED;
@@ -1163,7 +1343,7 @@ size_t sse_workspace_bytes(const sse_model* m, int B, int L) {
   Plan p;
   if (m->cfg.kind == SSE_KIND_WAVLM) {
     if (wavlm_frames(m->cfg, L, nullptr) <= 0) return 0;
-    wavlm_plan(m, B, L, p);
+    if (m->x3()) x3_plan(m, B, L, p); else wavlm_plan(m, B, L, p);
   } else {
     whisper_plan(m, B, p);
   }
