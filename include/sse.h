@@ -113,6 +113,17 @@ int sse_logmel(const float* d_wave, int B, int L, int n_mels, float* d_mel,
 int sse_embed(sse_model* m, const float* d_in, int B, int L, const int32_t* layer_ids,
               int n_layers, float* d_out, void* d_ws, size_t ws_bytes, void* stream);
 
+/* Ragged batch (REF/WavLM_embeddings.py:284-307 embeds every file at its own length): d_in [B][L]
+ * fp32 holds each clip in the first d_lengths[b] samples of its row (device int32 [B], 1..L; WavLM:
+ * >= 400 samples, the conv receptive field).  Each clip's embedding equals that clip run alone:
+ * WavLM's GroupNorm statistics, attention keys, positional-conv padding and time-means cover the
+ * clip's own frames; Whisper pads each clip with zeros to 30 s as the feature extractor does.
+ * Bit-identical to the per-clip call when the batch's longest clip selects the same attention
+ * kernel (WavLM: all clips <= 160 frames, or all > 160). */
+int sse_embed_ragged(sse_model* m, const float* d_in, const int32_t* d_lengths, int B, int L,
+                     const int32_t* layer_ids, int n_layers, float* d_out, void* d_ws, size_t ws_bytes,
+                     void* stream);
+
 /* Same forward, materialising every hidden state: d_hs [layers+1][B][T][hidden] fp32. */
 int sse_hidden_states(sse_model* m, const float* d_in, int B, int L, float* d_hs,
                       void* d_ws, size_t ws_bytes, void* stream);

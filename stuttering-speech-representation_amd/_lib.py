@@ -29,7 +29,7 @@ EXPORTED = ("sse_weight_floats", "sse_model_create", "sse_model_destroy", "sse_o
             "sse_whisper_decoder_hidden_states", "sse_mono", "sse_resample_length", "sse_resample_workspace_bytes",
             "sse_resample", "sse_augment", "sse_mx_scale_bytes", "sse_mx_scale_offset", "sse_mx_quantize",
             "sse_mx_quantize_host", "sse_gemm_mx", "sse_pitch_shift_workspace_bytes", "sse_pitch_shift",
-            "sse_set_option", "sse_get_option")
+            "sse_set_option", "sse_get_option", "sse_embed_ragged")
 
 
 class SSEError(RuntimeError):
@@ -119,6 +119,8 @@ def lib() -> ctypes.CDLL:
     L.sse_logmel.restype = i32
     L.sse_embed.argtypes = [vp, vp, i32, i32, vp, i32, vp, vp, sz, vp]
     L.sse_embed.restype = i32
+    L.sse_embed_ragged.argtypes = [vp, vp, vp, i32, i32, vp, i32, vp, vp, sz, vp]
+    L.sse_embed_ragged.restype = i32
     L.sse_hidden_states.argtypes = [vp, vp, i32, i32, vp, vp, sz, vp]
     L.sse_hidden_states.restype = i32
     L.sse_whisper_hidden_states_from_mel.argtypes = [vp, vp, i32, vp, vp, sz, vp]

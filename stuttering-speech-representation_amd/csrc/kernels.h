@@ -2,13 +2,25 @@
 #pragma once
 #include "common.h"
 
-int launch_wave_stats(const float* x, int B, int L, float* out, hipStream_t s);
+// lens (ragged batches, device, optional): samples of each clip [B]; L is the row stride
+int launch_wave_stats(const float* x, int B, int L, float* out, hipStream_t s, const int* lens = nullptr);
 
 size_t conv0_moments_bytes(int B);
+// t0len (ragged batches, device, optional): conv0 frames of each clip [B] (GroupNorm statistics
+// over the clip's own frames); T0 is the row stride
 template <typename TO>
 int launch_conv0_gn(const float* x, int B, int L, const float* norm, const float* w0, const float* b0, int C,
                     int k0, int s0, int T0, const float* gamma, const float* beta, float eps, double* mom,
-                    float2* ss, TO* out, hipStream_t s);
+                    float2* ss, TO* out, hipStream_t s, const int* t0len = nullptr);
+
+// ragged batches: per-clip frame counts after each conv layer, from the sample counts
+struct ClipFrames {
+  int n_conv, kernel[8], stride[8];
+};
+int launch_clip_frames(const int* lens, int B, ClipFrames cf, int* t0, int* tf, hipStream_t s);
+// zero rows t >= tlen[b] of x [B][T][H] (ragged batches: the padded positional conv must read zeros)
+template <typename TE>
+int launch_mask_rows(TE* x, int B, int T, int H, const int* tlen, hipStream_t s);
 
 template <typename TO>
 int launch_conv0_ln(const float* x, int B, int L, const float* norm, const float* w0, const float* b0, int C, int k0,
@@ -37,11 +49,12 @@ int launch_posconv_bf16(const bf16* xt, const bf16* W, const float* bias, float*
                         int pad, hipStream_t s);
 
 // st: per-row (mean, rstd), or part: per-256-column partials [rows][nt] (ln_part_stats): each element
-// is LayerNorm'd with (w, b) before the mean
+// is LayerNorm'd with (w, b) before the mean.  tlen (ragged batches): the mean runs over each clip's
+// own frames; T is the row stride.
 template <typename TI>
 int launch_pool_mean(const TI* x, int B, int T, int H, float* out, long long out_stride, hipStream_t s,
                      const float2* st = nullptr, const float* w = nullptr, const float* b = nullptr,
-                     const float2* part = nullptr, int nt = 0, float eps = 0.f);
+                     const float2* part = nullptr, int nt = 0, float eps = 0.f, const int* tlen = nullptr);
 
 struct AttnArgs {
   const void* qkv;       // [B*T][ldq]  (q | k | v | WavLM gate projection | pad), element type T
@@ -53,6 +66,7 @@ struct AttnArgs {
   const float* gconst;   // [nh]
   const float* relb;     // [nh][2*maxd+1], index d + maxd
   int maxd;
+  const int* tlen;       // ragged batch: frames of each clip [B] (T is then the per-clip row stride)
 };
 template <typename T>
 int launch_attention(const AttnArgs& a, int B, hipStream_t s);

@@ -4,10 +4,11 @@
 constexpr int LM_NB = 448;   // DFT basis rows: 201 cos + 201 sin, padded to a multiple of 64
 
 size_t logmel_workspace_bytes(int B, int n_mels);
-// x [B][L] fp32 -> out_hf [B][n_mels][3000] fp32 (optional) and out_cl [B][3000][n_mels] (optional)
+// x [B][L] fp32 -> out_hf [B][n_mels][3000] fp32 (optional) and out_cl [B][3000][n_mels] (optional);
+// lens (ragged batch, device, optional): samples of each clip, zeros after (the feature extractor's padding)
 template <typename TO>
 int launch_logmel(const float* x, int B, int L, int n_mels, float* out_hf, TO* out_cl, void* ws, size_t ws_bytes,
-                  hipStream_t s);
+                  hipStream_t s, const int* lens = nullptr);
 // HF-layout mel [B][n_mels][3000] fp32 -> channels-last [B][3000][n_mels]
 template <typename TO>
 int launch_mel_to_cl(const float* mel_hf, int B, int n_mels, TO* out_cl, hipStream_t s);

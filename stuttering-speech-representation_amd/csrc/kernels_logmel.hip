@@ -17,10 +17,12 @@ namespace {
 constexpr int N_FFT = 400, HOP = 160, PAD = 200, NS = 480000, NP = NS + 2 * PAD, NFR = 3000;
 constexpr int NF = N_FFT / 2 + 1;   // 201 bins
 
-__global__ void lm_pad_kernel(const float* __restrict__ x, int L, int Lv, float* __restrict__ xp) {
+__global__ void lm_pad_kernel(const float* __restrict__ x, int L, int Lv, float* __restrict__ xp,
+                              const int* __restrict__ lens) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int b = blockIdx.y;
   if (i >= NP) return;
+  if (lens) Lv = lens[b] < NS ? lens[b] : NS;   // ragged batch: the clip's own samples, zeros after
   int j = (int)i - PAD;
   if (j < 0) j = -j;
   if (j >= NS) j = 2 * (NS - 1) - j;
@@ -156,7 +158,7 @@ size_t logmel_workspace_bytes(int B, int n_mels) {
 
 template <typename TO>
 int launch_logmel(const float* x, int B, int L, int n_mels, float* out_hf, TO* out_cl, void* ws, size_t ws_bytes,
-                  hipStream_t s) {
+                  hipStream_t s, const int* lens) {
   if (B <= 0 || L <= 0 || n_mels <= 0 || n_mels > 256) return -1;
   if (ws_bytes < logmel_workspace_bytes(B, n_mels)) return -4;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -172,7 +174,7 @@ int launch_logmel(const float* x, int B, int L, int n_mels, float* out_hf, TO* o
   if (hipMemsetAsync(mx, 0, (size_t)B * 4, s) != hipSuccess) return -2;
   hipLaunchKernelGGL(lm_basis_kernel, dim3((LM_NB * N_FFT + 255) / 256), dim3(256), 0, s, basis);
   hipLaunchKernelGGL(lm_filters_kernel, dim3((NF * n_mels + 255) / 256), dim3(256), 0, s, fb, n_mels);
-  hipLaunchKernelGGL(lm_pad_kernel, dim3((NP + 255) / 256, B), dim3(256), 0, s, x, L, L < NS ? L : NS, xp);
+  hipLaunchKernelGGL(lm_pad_kernel, dim3((NP + 255) / 256, B), dim3(256), 0, s, x, L, L < NS ? L : NS, xp, lens);
   if (hipGetLastError() != hipSuccess) return -2;
   GemmArgs g{};
   g.A = xp; g.B = basis; g.M = B * NFR; g.N = LM_NB; g.K = N_FFT;
@@ -185,5 +187,6 @@ int launch_logmel(const float* x, int B, int L, int n_mels, float* out_hf, TO* o
                      out_hf, out_cl);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
-template int launch_logmel<float>(const float*, int, int, int, float*, float*, void*, size_t, hipStream_t);
-template int launch_logmel<bf16>(const float*, int, int, int, float*, bf16*, void*, size_t, hipStream_t);
+template int launch_logmel<float>(const float*, int, int, int, float*, float*, void*, size_t, hipStream_t,
+                                  const int*);
+template int launch_logmel<bf16>(const float*, int, int, int, float*, bf16*, void*, size_t, hipStream_t, const int*);

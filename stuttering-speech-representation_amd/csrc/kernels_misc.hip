@@ -9,9 +9,10 @@
 
 // ---------------------------------------------------------------------------------------
 // a2: per-clip mean / rstd for do_normalize (HF feature_extraction_wav2vec2.py:94).
-__global__ __launch_bounds__(256) void wave_stats_kernel(const float* __restrict__ x, int L,
-                                                         float* __restrict__ out) {
-  const float* xb = x + (long long)blockIdx.x * L;
+__global__ __launch_bounds__(256) void wave_stats_kernel(const float* __restrict__ x, int LS,
+                                                         float* __restrict__ out, const int* __restrict__ lens) {
+  const float* xb = x + (long long)blockIdx.x * LS;
+  const int L = lens ? lens[blockIdx.x] : LS;
   double s = 0.0, q = 0.0;
   for (int i = threadIdx.x; i < L; i += 256) {
     const double v = xb[i];
@@ -33,8 +34,8 @@ __global__ __launch_bounds__(256) void wave_stats_kernel(const float* __restrict
   }
 }
 
-int launch_wave_stats(const float* x, int B, int L, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(wave_stats_kernel, dim3(B), dim3(256), 0, s, x, L, out);
+int launch_wave_stats(const float* x, int B, int L, float* out, hipStream_t s, const int* lens) {
+  hipLaunchKernelGGL(wave_stats_kernel, dim3(B), dim3(256), 0, s, x, L, out, lens);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -54,9 +55,10 @@ constexpr int NG = K0 * (K0 + 1) / 2;    // unique Gram entries
 constexpr int NMOM = K0 + NG;            // 65 moments per clip
 
 __global__ __launch_bounds__(256) void conv0_moments_kernel(const float* __restrict__ x, int L,
-                                                            const float* __restrict__ norm, int s0, int T0,
-                                                            double* __restrict__ mom) {
+                                                            const float* __restrict__ norm, int s0, int T0S,
+                                                            double* __restrict__ mom, const int* __restrict__ t0len) {
   const int b = blockIdx.x;
+  const int T0 = t0len ? t0len[b] : T0S;
   const float* xb = x + (long long)b * L;
   float mu = 0.f, rs = 1.f;
   if (norm) { mu = norm[2 * b]; rs = norm[2 * b + 1]; }
@@ -92,13 +94,14 @@ __global__ __launch_bounds__(256) void conv0_moments_kernel(const float* __restr
         red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
 }
 
-__global__ void gn_finalize_kernel(const double* __restrict__ mom, int B, int C, int T0,
+__global__ void gn_finalize_kernel(const double* __restrict__ mom, int B, int C, int T0S,
                                    const float* __restrict__ w0, const float* __restrict__ b0,
                                    const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
-                                   float2* __restrict__ ss) {
+                                   float2* __restrict__ ss, const int* __restrict__ t0len) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B * C) return;
   const int b = i / C, c = i - b * C;
+  const int T0 = t0len ? t0len[b] : T0S;
   const double* S = mom + (long long)b * NMOM;
   const double* G = S + K0;
   double w[K0];
@@ -266,7 +269,8 @@ __global__ __launch_bounds__(256) void conv0_apply_kernel(const float* __restric
 //   q0: xh0-7 | wh0-7   q1: xh8,9 xl0-5 | wh8,9 wh0-5   q2: xl6-9 xh0-3 | wh6-9 wl0-3   q3: xh4-9 0 0 | wl4-9 0 0
 // MFMAs compute C^T (channels x frames), so a lane holds 4 consecutive channels of one frame; two
 // channel blocks per step and a v_permlane16_swap give every lane 8 consecutive bf16 = one 16-B store.
-constexpr int C0M_T = 32;                // frames per block (2 blocks of 16)
+constexpr int C0M_T = 32;
+constexpr int C0M_C = 512;               // channels of the matrix-core conv0 (conv0_wfrag_kernel fragments)                // frames per block (2 blocks of 16)
 
 SSE_DEV void c0m_split(float v, bf16& h, bf16& l) {
   h = (bf16)v;
@@ -371,26 +375,33 @@ __global__ __launch_bounds__(256) void conv0_mfma_kernel(const float* __restrict
   }
 }
 
-size_t conv0_moments_bytes(int B) { return ((size_t)B * NMOM * sizeof(double) + 255) / 256 * 256 + 512 / 16 * 1024; }
+// moments [B][NMOM] fp64 | the matrix-core conv0's weight fragments (C0M_C / 16 x 64 lanes x 16 B)
+size_t conv0_moments_bytes(int B) { return ((size_t)B * NMOM * sizeof(double) + 255) / 256 * 256 + C0M_C / 16 * 64 * 16; }
 
 
 template <typename TO>
 int launch_conv0_gn(const float* x, int B, int L, const float* norm, const float* w0, const float* b0,
                     int C, int k0, int s0, int T0, const float* gamma, const float* beta, float eps,
-                    double* mom, float2* ss, TO* out, hipStream_t s) {
+                    double* mom, float2* ss, TO* out, hipStream_t s, const int* t0len) {
   if (k0 != K0 || s0 != 5) return -3;
-  hipLaunchKernelGGL(conv0_moments_kernel, dim3(B), dim3(256), 0, s, x, L, norm, s0, T0, mom);
+  hipLaunchKernelGGL(conv0_moments_kernel, dim3(B), dim3(256), 0, s, x, L, norm, s0, T0, mom, t0len);
   hipLaunchKernelGGL(gn_finalize_kernel, dim3((B * C + 255) / 256), dim3(256), 0, s, mom, B, C, T0, w0, b0, gamma,
-                     beta, eps, ss);
+                     beta, eps, ss, t0len);
   if (C % 8) return -3;
   dim3 grid((T0 + C0_T - 1) / C0_T, B), block(256);
   const bool valu = sse_opt(OPT_CONV0_VALU) != 0;   // A/B and tests: the VALU kernel below
-  if (sizeof(TO) == 2 && !gelu_exact_env() && C == 512 && !valu) {   // matrix-core conv0
+  // matrix-core conv0: C == C0M_C channels, whose weight fragments conv0_moments_bytes reserves
+  if (sizeof(TO) == 2 && !gelu_exact_env() && C == C0M_C && !valu) {
     bf16x8* wf = (bf16x8*)((char*)mom + ((size_t)B * NMOM * sizeof(double) + 255) / 256 * 256);
     hipLaunchKernelGGL(conv0_wfrag_kernel, dim3((C / 16 * 64 + 255) / 256), dim3(256), 0, s, w0, C, wf);
-    // 3 resident blocks per CU (168 VGPRs): spread each clip's chunks over G blocks, G * B ~ 3 * 256
+    // 3 resident blocks per CU (168 VGPRs): spread each clip's chunks over G blocks, G * B ~ 3 * CUs
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -2;
+    if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return -2;
     const int nchunk = (T0 + C0M_T - 1) / C0M_T;
-    int G = (3 * 256 + B - 1) / B;
+    int G = (3 * cus[dev] + B - 1) / B;
     G = G < 1 ? 1 : (G > nchunk ? nchunk : G);
     hipLaunchKernelGGL(conv0_mfma_kernel, dim3(G, B), dim3(256), 0, s, x, L, norm, (const bf16x8*)wf, b0, T0,
                        (const float2*)ss, (bf16*)out);
@@ -437,10 +448,10 @@ template int launch_conv0_raw<bf16>(const float*, int, int, const float*, const 
                                     int, bf16*, hipStream_t);
 template int launch_conv0_gn<float>(const float*, int, int, const float*, const float*, const float*, int, int,
                                     int, int, const float*, const float*, float, double*, float2*, float*,
-                                    hipStream_t);
+                                    hipStream_t, const int*);
 template int launch_conv0_gn<bf16>(const float*, int, int, const float*, const float*, const float*, int, int,
                                    int, int, const float*, const float*, float, double*, float2*, bf16*,
-                                   hipStream_t);
+                                   hipStream_t, const int*);
 
 // ---------------------------------------------------------------------------------------
 // LayerNorm over rows of H (H % 4 == 0, H <= 2048).  One wave per row, 4 rows per block;
@@ -800,26 +811,28 @@ __global__ __launch_bounds__(256) void pool_mean_kernel(const TI* __restrict__ x
                                                         float* __restrict__ out, long long out_stride,
                                                         const float2* __restrict__ st, const float* __restrict__ w,
                                                         const float* __restrict__ bb, const float2* __restrict__ lpart,
-                                                        int nt, float eps) {
+                                                        int nt, float eps, const int* __restrict__ tlen) {
   __shared__ double part[4][256];
   __shared__ float2 fst[POOL_TMAX];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int n = blockIdx.x * 256 + lane * 4, b = blockIdx.y;
+  const int TS = T;   // row stride per clip; T: this clip's frames (ragged batches)
+  T = tlen ? tlen[b] : T;
   const bool ln = st || lpart;
   const bool tab = ln && T <= POOL_TMAX;
   if (tab) {
     for (int t = threadIdx.x; t < T; t += 256)
-      fst[t] = st ? st[(long long)b * T + t] : ln_part_stats(lpart, nt, (long long)b * T + t, eps);
+      fst[t] = st ? st[(long long)b * TS + t] : ln_part_stats(lpart, nt, (long long)b * TS + t, eps);
     __syncthreads();
   }
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   if (n < H) {
-    const TI* xb = x + (long long)b * T * H + n;
+    const TI* xb = x + (long long)b * TS * H + n;
     const f32x4 wn = ln ? *(const f32x4*)(w + n) : f32x4{1.f, 1.f, 1.f, 1.f};
     const f32x4 bn = ln ? *(const f32x4*)(bb + n) : f32x4{0.f, 0.f, 0.f, 0.f};
     auto add = [&](f32x4 v, int t) {
       if (ln) {
-        const float2 q = tab ? fst[t] : (st ? st[(long long)b * T + t] : ln_part_stats(lpart, nt, (long long)b * T + t, eps));
+        const float2 q = tab ? fst[t] : (st ? st[(long long)b * TS + t] : ln_part_stats(lpart, nt, (long long)b * TS + t, eps));
         #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = fmaf((v[e] - q.x) * q.y, wn[e], bn[e]);
       }
@@ -850,16 +863,55 @@ __global__ __launch_bounds__(256) void pool_mean_kernel(const TI* __restrict__ x
 
 template <typename TI>
 int launch_pool_mean(const TI* x, int B, int T, int H, float* out, long long out_stride, hipStream_t s,
-                     const float2* st, const float* w, const float* b, const float2* part, int nt, float eps) {
+                     const float2* st, const float* w, const float* b, const float2* part, int nt, float eps,
+                     const int* tlen) {
   if (H % 4) return -3;
   hipLaunchKernelGGL(pool_mean_kernel<TI>, dim3((H + 255) / 256, B), dim3(256), 0, s, x, T, H, out, out_stride, st, w,
-                     b, part, nt, eps);
+                     b, part, nt, eps, tlen);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 template int launch_pool_mean<float>(const float*, int, int, int, float*, long long, hipStream_t, const float2*,
-                                     const float*, const float*, const float2*, int, float);
+                                     const float*, const float*, const float2*, int, float, const int*);
 template int launch_pool_mean<bf16>(const bf16*, int, int, int, float*, long long, hipStream_t, const float2*,
-                                    const float*, const float*, const float2*, int, float);
+                                    const float*, const float*, const float2*, int, float, const int*);
+
+// ---------------------------------------------------------------------------------------
+// Ragged batches: per-clip frame counts after conv0 and after the last conv layer (the same
+// integer recurrence as wavlm_frames on the host); 0 for a clip shorter than the receptive field.
+__global__ void clip_frames_kernel(const int* __restrict__ lens, int B, ClipFrames cf, int* __restrict__ t0,
+                                   int* __restrict__ tf) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  int t = lens[b], f0 = 0;
+  for (int i = 0; i < cf.n_conv; ++i) {
+    t = t < cf.kernel[i] ? 0 : (t - cf.kernel[i]) / cf.stride[i] + 1;
+    if (i == 0) f0 = t;
+  }
+  t0[b] = f0;
+  tf[b] = t;
+}
+
+int launch_clip_frames(const int* lens, int B, ClipFrames cf, int* t0, int* tf, hipStream_t s) {
+  hipLaunchKernelGGL(clip_frames_kernel, dim3((B + 255) / 256), dim3(256), 0, s, lens, B, cf, t0, tf);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+template <typename TE>
+__global__ __launch_bounds__(256) void mask_rows_kernel(TE* __restrict__ x, int T, int H, const int* __restrict__ tlen) {
+  const int b = blockIdx.y;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= T || t < tlen[b]) return;
+  TE* row = x + ((long long)b * T + t) * H;
+  for (int c = (threadIdx.x & 63); c < H; c += 64) row[c] = (TE)0.f;
+}
+
+template <typename TE>
+int launch_mask_rows(TE* x, int B, int T, int H, const int* tlen, hipStream_t s) {
+  hipLaunchKernelGGL(mask_rows_kernel<TE>, dim3((T + 3) / 4, B), dim3(256), 0, s, x, T, H, tlen);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+template int launch_mask_rows<float>(float*, int, int, int, const int*, hipStream_t);
+template int launch_mask_rows<bf16>(bf16*, int, int, int, const int*, hipStream_t);
 
 // ---------------------------------------------------------------------------------------
 // K5/K6/K11: attention, flash style.  Block = (64 queries, head, clip), 4 waves x 16 queries.
@@ -929,14 +981,15 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
 
   int qc, h, b;
   attn_block_xcd(qc, h, b);
-  const int T = a.T, H = a.H, H3 = a.ldq;
+  // T: this clip's frames (ragged batches: a.tlen), TS: the batch's row stride per clip
+  const int TS = a.T, T = a.tlen ? a.tlen[b] : a.T, H = a.H, H3 = a.ldq;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
   const int q0 = qc * AT_Q;
   const int nkt = (T + AT_K - 1) / AT_K;
   const int Tk = nkt * AT_K;
-  const TE* qkv = (const TE*)a.qkv + (long long)b * T * H3;
+  const TE* qkv = (const TE*)a.qkv + (long long)b * TS * H3;
 
   if (BIAS) {
     // gate[q] = sigmoid(a) * (sigmoid(b) * const_h - 1) + 2 with a, b the pairwise sums of the
@@ -1104,7 +1157,7 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
   l_run += __shfl_xor(l_run, 32, 64);
   if (!qv) return;
   const float inv = 1.0f / l_run;
-  TE* orow = (TE*)a.out + ((long long)b * T + qi) * H + h * AT_HD;
+  TE* orow = (TE*)a.out + ((long long)b * TS + qi) * H + h * AT_HD;
   #pragma unroll
   for (int db = 0; db < 4; ++db) {
     if constexpr (BF) {
@@ -1150,13 +1203,13 @@ __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
   float* rb = gate + F2_Q;                         // [2*Tk]
   int qc, h, b;
   attn_block_xcd(qc, h, b);
-  const int T = a.T, H = a.H, LQ = a.ldq;
+  const int TS = a.T, T = a.tlen ? a.tlen[b] : a.T, H = a.H, LQ = a.ldq;   // frames of this clip / row stride
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
   const int q0 = qc * F2_Q;
   const int nkt = (T + F2_K - 1) / F2_K, Tk = nkt * F2_K;
-  const bf16* qkv = (const bf16*)a.qkv + (long long)b * T * LQ;
+  const bf16* qkv = (const bf16*)a.qkv + (long long)b * TS * LQ;
 
   if (BIAS) {
     if (tid < F2_Q)
@@ -1316,7 +1369,7 @@ __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
     l += __shfl_xor(l, 32, 64);
     if (qi[qq] < T) {
       const float inv = 1.0f / l;
-      bf16* orow = (bf16*)a.out + ((long long)b * T + qi[qq]) * H + h * AT_HD;
+      bf16* orow = (bf16*)a.out + ((long long)b * TS + qi[qq]) * H + h * AT_HD;
       #pragma unroll
       for (int db = 0; db < 4; ++db) {
         bf16x4 ov = {(bf16)(o[qq][db][0] * inv), (bf16)(o[qq][db][1] * inv), (bf16)(o[qq][db][2] * inv),
@@ -1348,11 +1401,11 @@ __global__ __launch_bounds__(640) void attention_full_kernel(AttnArgs a, int hpb
   // registers before this head's MFMAs and written to LDS after them (one LDS image, two
   // barriers per head), so a block pays one exposed HBM round trip, not one per head
   const int h0 = blockIdx.x * hpb, b = blockIdx.y;
-  const int T = a.T, H = a.H, H3 = a.ldq;
+  const int TS = a.T, T = a.tlen ? a.tlen[b] : a.T, H = a.H, H3 = a.ldq;   // frames of this clip / row stride
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
-  const bf16* qkv = (const bf16*)a.qkv + (long long)b * T * H3;
+  const bf16* qkv = (const bf16*)a.qkv + (long long)b * TS * H3;
   const int qb = wave;
   const int qi = qb * 16 + r16;
   const bool qv = qi < T;
@@ -1476,7 +1529,7 @@ __global__ __launch_bounds__(640) void attention_full_kernel(AttnArgs a, int hpb
   }
   if (qv) {
     const float inv = 1.0f / l;
-    bf16* orow = (bf16*)a.out + ((long long)b * T + qi) * H + h * AT_HD;
+    bf16* orow = (bf16*)a.out + ((long long)b * TS + qi) * H + h * AT_HD;
     #pragma unroll
     for (int db = 0; db < 4; ++db) {
       bf16x4 ov = {(bf16)(o[db][0] * inv), (bf16)(o[db][1] * inv), (bf16)(o[db][2] * inv),

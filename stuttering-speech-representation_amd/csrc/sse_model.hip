@@ -572,7 +572,7 @@ int wavlm_frames(const sse_cfg& c, int L, int* Ts) {
 }
 
 struct WavlmWs {
-  size_t zero, norm, part, ss, bufA, bufB, x, xt, xb, qkv, ctx, ff, hf, p1, p2;
+  size_t zero, norm, part, ss, bufA, bufB, x, xt, xb, qkv, ctx, ff, hf, p1, p2, fr;
 };
 
 WavlmWs wavlm_plan(const sse_model* m, int B, int L, Plan& p) {
@@ -605,6 +605,7 @@ WavlmWs wavlm_plan(const sse_model* m, int B, int L, Plan& p) {
   const size_t nt = H % 256 == 0 ? (size_t)H / 256 : 0;   // folded path: per-256-column partials
   w.p1 = p.add(M * nt * 8);
   w.p2 = p.add(M * nt * 8);
+  w.fr = p.add((size_t)B * 8);   // ragged batches: per-clip conv0 frames | final frames
   return w;
 }
 
@@ -655,9 +656,12 @@ struct Sink {
   float* hs;             // [n_hs][B][T][H]
   int B, T, H;
   hipStream_t s;
+  const int* tlen = nullptr;   // ragged batch: frames of each clip (the time-means run over those)
   int emit(int idx, const float* x) const {
     for (int i = 0; i < n_ids; ++i)
-      if (ids[i] == idx) RC(launch_pool_mean(x, B, T, H, pooled + (size_t)i * H, (long long)n_ids * H, s));
+      if (ids[i] == idx)
+        RC(launch_pool_mean(x, B, T, H, pooled + (size_t)i * H, (long long)n_ids * H, s, nullptr, nullptr, nullptr,
+                            nullptr, 0, 0.f, tlen));
     if (hs) {
       const size_t bytes = (size_t)B * T * H * 4;
       if (hipMemcpyAsync(hs + (size_t)idx * B * T * H, x, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
@@ -672,7 +676,8 @@ struct Sink {
               const float2* part = nullptr, int nt = 0) const {
     for (int i = 0; i < n_ids; ++i)
       if (ids[i] == idx)
-        RC(launch_pool_mean<TI>(x, B, T, H, pooled + (size_t)i * H, (long long)n_ids * H, s, st, w, b, part, nt, eps));
+        RC(launch_pool_mean<TI>(x, B, T, H, pooled + (size_t)i * H, (long long)n_ids * H, s, st, w, b, part, nt, eps,
+                                tlen));
     if (hs)
       RC((launch_layernorm<TI, float>(x, w, b, B * T, H, eps, ACT_NONE, hs + (size_t)idx * B * T * H,
                                       (float*)nullptr, s)));
@@ -691,11 +696,26 @@ int gelu_rounded_act() {
   }
 }
 
+// Ragged batches (lens: samples of each clip, device): the per-clip conv0 frame counts t0 and
+// final frame counts tf go to the workspace; the sink's means run over tf.
+int ragged_frames(const sse_model* m, const int* lens, int B, int* t0, int* tf, hipStream_t s) {
+  ClipFrames cf{};
+  cf.n_conv = m->cfg.n_conv;
+  for (int i = 0; i < cf.n_conv; ++i) { cf.kernel[i] = m->cfg.conv_kernel[i]; cf.stride[i] = m->cfg.conv_stride[i]; }
+  return launch_clip_frames(lens, B, cf, t0, tf, s);
+}
+
 template <typename T>
-int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sink, char* ws, hipStream_t s) {
+int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sink_in, char* ws, hipStream_t s,
+                  const int* lens = nullptr) {
   const sse_cfg& c = m->cfg;
   Plan p;
   const WavlmWs w = wavlm_plan(m, B, L, p);
+  int* t0len = lens ? (int*)(ws + w.fr) : nullptr;
+  int* tflen = lens ? t0len + B : nullptr;
+  Sink sink = sink_in;
+  sink.tlen = tflen;
+  if (lens) RC(ragged_frames(m, lens, B, t0len, tflen, s));
   int Ts[8];
   const int Tf = wavlm_frames(c, L, Ts);
   const int H = c.hidden, nh = c.heads, F = c.ffn;
@@ -705,7 +725,7 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
   if (hipMemsetAsync(zero, 0, 256, s) != hipSuccess) return SSE_ERR_HIP;
   const float* norm = nullptr;
   if (c.do_normalize) {
-    RC(launch_wave_stats(wave, B, L, (float*)(ws + w.norm), s));
+    RC(launch_wave_stats(wave, B, L, (float*)(ws + w.norm), s, lens));
     norm = (const float*)(ws + w.norm);
   }
   // ---- conv feature encoder ----
@@ -730,7 +750,7 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     RC(prof(m, s, "conv0_gn", 2.0 * B * (double)Ts[0] * C0 * c.conv_kernel[0], 0, [&] {
       return launch_conv0_gn<T>(wave, B, L, norm, m->ptr<float>(m->conv_w[0]), b0, C0, c.conv_kernel[0],
                                 c.conv_stride[0], Ts[0], m->ptr<float>(m->conv_ln_w[0]), m->ptr<float>(m->conv_ln_b[0]),
-                                1e-5f, (double*)(ws + w.part), (float2*)(ws + w.ss), bufs[0], s); }));
+                                1e-5f, (double*)(ws + w.part), (float2*)(ws + w.ss), bufs[0], s, t0len); }));
   }
   for (int i = 1; i < c.n_conv; ++i) {
     const int cin = c.conv_dim[i - 1], co = c.conv_dim[i], k = c.conv_kernel[i], st = c.conv_stride[i];
@@ -761,6 +781,7 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     RC(prof(m, s, "gemm:proj", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
   }
   // ---- positional conv embedding: x = x + gelu(conv(x) + b) ----
+  if (lens) RC(launch_mask_rows<T>(xt, B, Tf, H, tflen, s));   // frames past a clip read as the conv's zero padding
   {
     const int G = c.pos_groups, cg = H / G, K = c.pos_kernel;
     GemmArgs g{};
@@ -818,7 +839,7 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
             [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     AttnArgs a{};
     a.qkv = qkv; a.out = ctx; a.T = Tf; a.H = H; a.nh = nh; a.ldq = m->ldq; a.scale = 0.125f;
-    a.gconst = m->ptr<float>(Lw.g_const); a.relb = m->ptr<float>(m->relb); a.maxd = MAXD;
+    a.gconst = m->ptr<float>(Lw.g_const); a.relb = m->ptr<float>(m->relb); a.maxd = MAXD; a.tlen = tflen;
     RC(prof(m, s, "attn", 4.0 * B * (double)Tf * Tf * H, (double)B * Tf * (4.0 * H + 8.0 * nh) * sizeof(T),
             [&] { return launch_attention<T>(a, B, s); }));
     g = GemmArgs{};
@@ -885,7 +906,7 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
 // (scores, softmax, P.V) run in exact fp32 as in the fp32 path; LayerNorms read / write fp32 and
 // tripled rows.
 struct X3Ws {
-  size_t zero, norm, part, ss, c0, bufA, bufB, x, xt, xb, qkv, ctx, ctx3, ff;
+  size_t zero, norm, part, ss, c0, bufA, bufB, x, xt, xb, qkv, ctx, ctx3, ff, fr;
 };
 
 X3Ws x3_plan(const sse_model* m, int B, int L, Plan& p) {
@@ -915,13 +936,20 @@ X3Ws x3_plan(const sse_model* m, int B, int L, Plan& p) {
   w.ctx = p.add(M * H * 4);
   w.ctx3 = p.add(M * H * 6);
   w.ff = p.add(M * (size_t)c.ffn * 6);
+  w.fr = p.add((size_t)B * 8);
   return w;
 }
 
-int wavlm_forward_x3(sse_model* m, const float* wave, int B, int L, const Sink& sink, char* ws, hipStream_t s) {
+int wavlm_forward_x3(sse_model* m, const float* wave, int B, int L, const Sink& sink_in, char* ws, hipStream_t s,
+                     const int* lens = nullptr) {
   const sse_cfg& c = m->cfg;
   Plan p;
   const X3Ws w = x3_plan(m, B, L, p);
+  int* t0len = lens ? (int*)(ws + w.fr) : nullptr;
+  int* tflen = lens ? t0len + B : nullptr;
+  Sink sink = sink_in;
+  sink.tlen = tflen;
+  if (lens) RC(ragged_frames(m, lens, B, t0len, tflen, s));
   int Ts[8];
   const int Tf = wavlm_frames(c, L, Ts);
   const int H = c.hidden, nh = c.heads, F = c.ffn;
@@ -931,7 +959,7 @@ int wavlm_forward_x3(sse_model* m, const float* wave, int B, int L, const Sink& 
   if (hipMemsetAsync(zero, 0, 256, s) != hipSuccess) return SSE_ERR_HIP;
   const float* norm = nullptr;
   if (c.do_normalize) {
-    RC(launch_wave_stats(wave, B, L, (float*)(ws + w.norm), s));
+    RC(launch_wave_stats(wave, B, L, (float*)(ws + w.norm), s, lens));
     norm = (const float*)(ws + w.norm);
   }
   // split-bf16 GEMM: logical K (the FLOP count), physical operands K' = 3K
@@ -947,7 +975,7 @@ int wavlm_forward_x3(sse_model* m, const float* wave, int B, int L, const Sink& 
   RC(prof(m, s, "conv0_gn", 2.0 * B * (double)Ts[0] * C0 * c.conv_kernel[0], 0, [&] {
     return launch_conv0_gn<float>(wave, B, L, norm, m->ptr<float>(m->conv_w[0]), b0, C0, c.conv_kernel[0],
                                   c.conv_stride[0], Ts[0], m->ptr<float>(m->conv_ln_w[0]), m->ptr<float>(m->conv_ln_b[0]),
-                                  1e-5f, (double*)(ws + w.part), (float2*)(ws + w.ss), c0, s); }));
+                                  1e-5f, (double*)(ws + w.part), (float2*)(ws + w.ss), c0, s, t0len); }));
   RC(launch_split3(c0, (long long)B * Ts[0], C0, bufs[0], s));
   for (int i = 1; i < c.n_conv; ++i) {
     const int cin = c.conv_dim[i - 1], co = c.conv_dim[i], k = c.conv_kernel[i], st = c.conv_stride[i];
@@ -973,6 +1001,7 @@ int wavlm_forward_x3(sse_model* m, const float* wave, int B, int L, const Sink& 
     RC(gemm3("gemm:proj", g, C));
   }
   if (hipMemcpyAsync(xt, x, (size_t)M * H * 4, hipMemcpyDeviceToDevice, s) != hipSuccess) return SSE_ERR_HIP;
+  if (lens) RC(launch_mask_rows<float>(xt, B, Tf, H, tflen, s));
   // ---- positional conv embedding in exact fp32: x = x + gelu(conv(x) + b) ----
   {
     const int G = c.pos_groups, cg = H / G, K = c.pos_kernel;
@@ -999,7 +1028,7 @@ int wavlm_forward_x3(sse_model* m, const float* wave, int B, int L, const Sink& 
             [&] { return launch_gemm8_bf16(g, s); }));
     AttnArgs a{};
     a.qkv = qkv; a.out = ctx; a.T = Tf; a.H = H; a.nh = nh; a.ldq = m->ldq; a.scale = 0.125f;
-    a.gconst = m->ptr<float>(Lw.g_const); a.relb = m->ptr<float>(m->relb); a.maxd = MAXD;
+    a.gconst = m->ptr<float>(Lw.g_const); a.relb = m->ptr<float>(m->relb); a.maxd = MAXD; a.tlen = tflen;
     RC(prof(m, s, "attn", 4.0 * B * (double)Tf * Tf * H, (double)B * Tf * (4.0 * H + 8.0 * nh) * 4.0,
             [&] { return launch_attention<float>(a, B, s); }));
     RC(launch_split3(ctx, M, H, ctx3, s));
@@ -1085,7 +1114,7 @@ int whisper_decoder(sse_model* m, const T* enc, int B, const Sink& sink, char* w
 
 template <typename T>
 int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& sink, char* ws, hipStream_t s,
-                    const float* mel_hf = nullptr, const Sink* dsink = nullptr) {
+                    const float* mel_hf = nullptr, const Sink* dsink = nullptr, const int* lens = nullptr) {
   const sse_cfg& c = m->cfg;
   Plan p;
   const WhisperWs w = whisper_plan(m, B, p);
@@ -1099,7 +1128,8 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
     RC(launch_mel_to_cl<T>(mel_hf, B, nm, mel, s));
   else
     RC(prof(m, s, "logmel", 2.0 * B * 3000.0 * LM_NB * 400, (double)B * (480000.0 * 4 + 3000.0 * nm * sizeof(T)),
-            [&] { return launch_logmel<T>(wave, B, L, nm, nullptr, mel, ws + w.lm, logmel_workspace_bytes(B, nm), s); }));
+            [&] { return launch_logmel<T>(wave, B, L, nm, nullptr, mel, ws + w.lm, logmel_workspace_bytes(B, nm), s,
+                                          lens); }));
   T* h1 = (T*)(ws + w.h1);
   float* x = (float*)(ws + w.x);
   T* xb = (T*)(ws + w.xb);
@@ -1192,7 +1222,7 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
 }
 
 int forward(sse_model* m, const float* d_in, int B, int L, const Sink& sink, void* d_ws, size_t ws_bytes,
-            hipStream_t s, bool from_mel = false, const Sink* dsink = nullptr) {
+            hipStream_t s, bool from_mel = false, const Sink* dsink = nullptr, const int* lens = nullptr) {
   if (!m || !d_in || B <= 0 || L <= 0) return SSE_ERR_INVALID;
   if (ws_bytes < sse_workspace_bytes(m, B, L)) return SSE_ERR_WORKSPACE;
   if (m->cfg.kind == SSE_KIND_WAVLM && wavlm_frames(m->cfg, L, nullptr) <= 0) return SSE_ERR_INVALID;
@@ -1201,13 +1231,13 @@ int forward(sse_model* m, const float* d_in, int B, int L, const Sink& sink, voi
   if (dev != m->device && hipSetDevice(m->device) != hipSuccess) return SSE_ERR_HIP;
   int rc;
   if (m->cfg.kind == SSE_KIND_WAVLM && m->x3())
-    rc = wavlm_forward_x3(m, d_in, B, L, sink, (char*)d_ws, s);
+    rc = wavlm_forward_x3(m, d_in, B, L, sink, (char*)d_ws, s, lens);
   else if (m->cfg.kind == SSE_KIND_WAVLM)
-    rc = m->bf() ? wavlm_forward<bf16>(m, d_in, B, L, sink, (char*)d_ws, s)
-                 : wavlm_forward<float>(m, d_in, B, L, sink, (char*)d_ws, s);
+    rc = m->bf() ? wavlm_forward<bf16>(m, d_in, B, L, sink, (char*)d_ws, s, lens)
+                 : wavlm_forward<float>(m, d_in, B, L, sink, (char*)d_ws, s, lens);
   else
-    rc = m->bf() ? whisper_forward<bf16>(m, d_in, B, L, sink, (char*)d_ws, s, from_mel ? d_in : nullptr, dsink)
-                 : whisper_forward<float>(m, d_in, B, L, sink, (char*)d_ws, s, from_mel ? d_in : nullptr, dsink);
+    rc = m->bf() ? whisper_forward<bf16>(m, d_in, B, L, sink, (char*)d_ws, s, from_mel ? d_in : nullptr, dsink, lens)
+                 : whisper_forward<float>(m, d_in, B, L, sink, (char*)d_ws, s, from_mel ? d_in : nullptr, dsink, lens);
   if (dev != m->device) (void)hipSetDevice(dev);
   return rc;
 }
@@ -1365,6 +1395,15 @@ int sse_embed(sse_model* m, const float* d_in, int B, int L, const int32_t* laye
     if (layer_ids[i] < 0 || layer_ids[i] > m->cfg.layers) return SSE_ERR_INVALID;
   Sink sk{layer_ids, n_layers, d_out, nullptr, B, hs_frames(m, L), m->cfg.hidden, (hipStream_t)stream};
   return forward(m, d_in, B, L, sk, d_ws, ws_bytes, (hipStream_t)stream);
+}
+
+int sse_embed_ragged(sse_model* m, const float* d_in, const int32_t* d_lengths, int B, int L, const int32_t* layer_ids,
+                     int n_layers, float* d_out, void* d_ws, size_t ws_bytes, void* stream) {
+  if (!m || !d_lengths || !layer_ids || n_layers <= 0 || !d_out) return SSE_ERR_INVALID;
+  for (int i = 0; i < n_layers; ++i)
+    if (layer_ids[i] < 0 || layer_ids[i] > m->cfg.layers) return SSE_ERR_INVALID;
+  Sink sk{layer_ids, n_layers, d_out, nullptr, B, hs_frames(m, L), m->cfg.hidden, (hipStream_t)stream};
+  return forward(m, d_in, B, L, sk, d_ws, ws_bytes, (hipStream_t)stream, false, nullptr, (const int*)d_lengths);
 }
 
 int sse_hidden_states(sse_model* m, const float* d_in, int B, int L, float* d_hs, void* d_ws, size_t ws_bytes,

@@ -153,8 +153,11 @@ class SSEModel:
         _lib.check(_lib.lib().sse_profile_stop(self._h), "sse_profile_stop")
 
     # -- compute --------------------------------------------------------------------------
-    def embed(self, wave: torch.Tensor, layer_indices, out: torch.Tensor | None = None) -> torch.Tensor:
-        """[B, L] fp32 16 kHz waves -> [B, len(layer_indices), H] fp32 time-means of hidden states."""
+    def embed(self, wave: torch.Tensor, layer_indices, out: torch.Tensor | None = None,
+              lengths=None) -> torch.Tensor:
+        """[B, L] fp32 16 kHz waves -> [B, len(layer_indices), H] fp32 time-means of hidden states.
+        ``lengths`` (ragged batch): samples of each clip, its first lengths[b] samples of row b; each
+        clip is embedded at its own length (sse_embed_ragged)."""
         wave = self._check_wave(wave)
         B, L = wave.shape
         ids = torch.tensor([int(i) for i in layer_indices], dtype=torch.int32)
@@ -162,9 +165,30 @@ class SSEModel:
         if out is None:
             out = torch.empty((B, n, self.spec.hidden), dtype=torch.float32, device=self.device)
         ws = self.workspace(B, L)
-        _lib.check(_lib.lib().sse_embed(self._h, wave.data_ptr(), B, L, ids.data_ptr(), n, out.data_ptr(),
-                                        ws.data_ptr(), ws.numel(), self._stream()), "sse_embed")
+        if lengths is None:
+            _lib.check(_lib.lib().sse_embed(self._h, wave.data_ptr(), B, L, ids.data_ptr(), n, out.data_ptr(),
+                                            ws.data_ptr(), ws.numel(), self._stream()), "sse_embed")
+            return out
+        lens = [int(v) for v in (lengths.tolist() if isinstance(lengths, torch.Tensor) else lengths)]
+        if len(lens) != B or min(lens) < 1 or max(lens) > L:
+            raise ValueError(f"lengths must be {B} values in [1, {L}]")
+        if isinstance(self.spec, WavLMSpec) and min(self.spec.frames(v) for v in lens) <= 0:
+            raise _lib.SSEError(-1, "a clip is shorter than the conv receptive field")
+        d_len = torch.tensor(lens, dtype=torch.int32).to(self.device, non_blocking=False)
+        _lib.check(_lib.lib().sse_embed_ragged(self._h, wave.data_ptr(), d_len.data_ptr(), B, L, ids.data_ptr(), n,
+                                               out.data_ptr(), ws.data_ptr(), ws.numel(), self._stream()),
+                   "sse_embed_ragged")
         return out
+
+    def embed_clips(self, clips, layer_indices) -> torch.Tensor:
+        """A list of 1-D clips of any lengths -> [N, len(layer_indices), H]: one ragged batch
+        (zero-padded rows + lengths), every clip embedded at its own length."""
+        lens = [int(c.shape[-1]) for c in clips]
+        wave = torch.zeros((len(clips), max(lens)), dtype=torch.float32, device=self.device)
+        for i, c in enumerate(clips):
+            c = c if isinstance(c, torch.Tensor) else torch.from_numpy(np.asarray(c, dtype=np.float32))
+            wave[i, :lens[i]] = c.to(self.device, torch.float32)
+        return self.embed(wave, layer_indices, lengths=lens)
 
     def hidden_states(self, wave: torch.Tensor) -> tuple:
         """[B, L] -> tuple of layers+1 tensors [B, T, H] (HF ``output_hidden_states`` semantics)."""

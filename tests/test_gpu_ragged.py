@@ -1,0 +1,90 @@
+"""Ragged batches (sse_embed_ragged): clips of different lengths share one batch and each is
+embedded at its own length, exactly as the reference embeds every file alone
+(REF/WavLM_embeddings.py:284-307; REF/whisper_embeddings_large.py:242-254 pads to 30 s).
+
+Properties: every clip of a ragged batch equals that clip run alone -- bit for bit when the batch's
+longest clip selects the same WavLM attention kernel (all clips <= 160 frames, or all > 160), and
+whatever the padding rows hold (random values are written past each clip's end); the fp32 path
+matches the oracle at every length (rel-L2 <= 1e-4)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return np.linalg.norm(a - b, axis=-1) / np.linalg.norm(b, axis=-1)
+
+
+def _batch(lens, seed, garbage=True):
+    from ssr_amd import synth
+    L = max(lens)
+    rng = np.random.default_rng(seed)
+    wave = (rng.standard_normal((len(lens), L)).astype(np.float32) * 3.0) if garbage else np.zeros((len(lens), L), np.float32)
+    clips = [synth.synth_clips(1, n, seed=seed + i)[0] for i, n in enumerate(lens)]
+    for i, c in enumerate(clips):
+        wave[i, :len(c)] = c
+    return torch.from_numpy(wave).cuda(), clips
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "bf16x3"])
+@pytest.mark.parametrize("lens", [[48000, 400, 12345, 47999, 30000, 16000], [80000, 60000, 52000, 70001]])
+def test_wavlm_ragged_equals_per_clip(wavlm_sd, dtype, lens):
+    from ssr_amd import config as C
+    from ssr_amd.model import SSEModel
+    m = SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype=dtype)
+    idx = [12, 11, 10, 6, 0]
+    wave, clips = _batch(lens, 300)
+    got = m.embed(wave, idx, lengths=lens)
+    assert torch.isfinite(got).all()
+    for i, c in enumerate(clips):
+        one = m.embed(torch.from_numpy(c).cuda()[None], idx)
+        assert torch.equal(got[i:i + 1], one), (dtype, i, lens[i])
+    if dtype == "fp32":
+        from oracle.wavlm import WavLMOracle
+        o = WavLMOracle(C.WAVLM_BASE, wavlm_sd)
+        for i in (0, 1, len(lens) - 1):
+            ref = o.embed(clips[i], idx)
+            assert _rel(got[i:i + 1].cpu().numpy(), ref).max() <= 1e-4
+
+
+def test_wavlm_ragged_mixed_attention_paths(wavlm_sd):
+    """Clips on both sides of the 160-frame attention split: equal to per-clip runs within the
+    bf16 path's own noise (different attention kernels, same math)."""
+    from ssr_amd import config as C
+    from ssr_amd.model import SSEModel
+    m = SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype="bf16")
+    lens = [48000, 80000, 3000]
+    wave, clips = _batch(lens, 77)
+    got = m.embed(wave, [12, 6], lengths=lens).cpu().numpy()
+    for i, c in enumerate(clips):
+        one = m.embed(torch.from_numpy(c).cuda()[None], [12, 6]).cpu().numpy()
+        assert _rel(got[i:i + 1], one).max() <= 1e-2, (i, lens[i])
+
+
+def test_wavlm_ragged_normalize_and_embed_clips(wavlm_sd):
+    """do_normalize statistics over each clip's own samples; embed_clips builds the padded batch."""
+    from ssr_amd import config as C
+    from ssr_amd.model import SSEModel
+    m = SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype="fp32", do_normalize=True)
+    lens = [20000, 48000, 9000]
+    _, clips = _batch(lens, 12)
+    got = m.embed_clips([torch.from_numpy(c) for c in clips], [12, 3])
+    for i, c in enumerate(clips):
+        assert torch.equal(got[i:i + 1], m.embed(torch.from_numpy(c).cuda()[None], [12, 3]))
+    with pytest.raises(Exception):
+        m.embed_clips([torch.zeros(300)], [12])
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_whisper_ragged_equals_per_clip(dtype):
+    from ssr_amd import config as C, synth
+    from ssr_amd.model import SSEModel
+    m = SSEModel(C.WHISPER_TINY, synth.synth_whisper_state_dict(C.WHISPER_TINY, seed=11), device="cuda:0", dtype=dtype)
+    lens = [16000, 48000, 7000]
+    wave, clips = _batch(lens, 5)
+    idx = [4, 3, 0]
+    got = m.embed(wave, idx, lengths=lens)
+    for i, c in enumerate(clips):
+        assert torch.equal(got[i:i + 1], m.embed(torch.from_numpy(c).cuda()[None], idx)), i
