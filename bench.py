@@ -67,6 +67,9 @@ def parse():
     ap.add_argument("--no-profile", action="store_true", help="skip the per-launch event timing")
     ap.add_argument("--stream", action="store_true",
                     help="clips streamed from pinned host memory each step (double-buffered H2D on a side stream)")
+    ap.add_argument("--logmel", action="store_true",
+                    help="the Whisper log-mel front end alone (sse_logmel, K9): B x 30 s clips -> [B, 80, 3000], "
+                         "reported against the HBM roofline (1.92 MB in + 0.96 MB out per clip)")
     ap.add_argument("--lib", default=None, help="load this build of libsse.so instead of the in-tree one (A/B)")
     ap.add_argument("--corpus", type=int, default=0,
                     help="BASELINE configs[3] mode: embed a corpus of this many clips (e.g. 50000) sharded "
@@ -197,6 +200,43 @@ def roofline(records, dtype):
             "device_ms_per_step_sum": None, "breakdown": breakdown, "roles": roles}
 
 
+def logmel_run(a, dev):
+    """K9 alone: sse_logmel over a resident batch of 30 s clips (REF/whisper_embeddings_large.py:242-246,
+    HF WhisperFeatureExtractor).  Algorithmic HBM bytes per clip: 480000 fp32 samples in + 80 x 3000
+    fp32 log-mel out; time per call from torch events around the timed calls (one stream)."""
+    from ssr_amd.model import logmel
+    B = a.batch or 128
+    L = 480000
+    clips = torch.from_numpy(synth.synth_clips(B, L, seed=1234)).to(dev)
+    for _ in range(a.warmup):
+        logmel(clips)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(a.steps):
+        out = logmel(clips)
+    e1.record()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ms = e0.elapsed_time(e1) / a.steps
+    by = B * (L * 4.0 + 80 * 3000 * 4.0)
+    gbs = by / (ms * 1e-3) / 1e9
+    res = {"metric": "clips/sec (30 s) Whisper log-mel front end", "value": round(B * a.steps / el, 1), "unit": "clips/s",
+           "n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1e3 * el / a.steps, 3),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+           "data": "synthetic 16 kHz clips (splitmix64 Gaussian+tones)",
+           "config": {"workload": f"log-mel of {B} x 30 s clips -> [{B}, 80, 3000] fp32 (sse_logmel)", "global_batch": B},
+           "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None, "alg_bytes_per_call": by,
+                        "mean_call_ms": round(ms, 4),
+                        "note": "the exact-fp32 DFT-as-GEMM (1.07 GFLOP/clip on v_mfma_f32_16x16x4_f32) dominates "
+                                "the call: dft_tflops below is its rate against the 157.3 TF fp32 matrix peak"},
+           "finite": bool(torch.isfinite(out).all().item())}
+    res["roofline"]["dft_tflops"] = round(B * 1.07e9 / (ms * 1e-3) / 1e12, 1)
+    print(json.dumps(res), flush=True)
+
+
 def corpus_run(a, model, spec, idx, clips, B, L, world, rank, dev, dist):
     """configs[3]: the whole corpus through corpus.extract_corpus (rank r embeds its contiguous
     shard in batches of B, then ONE all-gather assembles [N, n_layers, H] in corpus order).  The
@@ -255,6 +295,8 @@ def main():
             raise SystemExit("for --gpus > 1 launch with torch.distributed.run (one process per GPU)")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if a.logmel:
+        return logmel_run(a, dev)
     dist = None
     if world > 1:
         import torch.distributed as dist

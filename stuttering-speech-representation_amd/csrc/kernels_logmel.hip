@@ -76,12 +76,27 @@ __device__ __forceinline__ float unord_f32(unsigned u) {
   return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
 }
 
+// support [first, last] of each mel filter's nonzero bins (triangular filters: contiguous)
+__global__ void lm_support_kernel(const float* __restrict__ fb, int n_mels, int2* __restrict__ sup) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= n_mels) return;
+  int lo = NF, hi = -1;
+  for (int f = 0; f < NF; ++f)
+    if (fb[f * n_mels + m] != 0.f) {
+      lo = f < lo ? f : lo;
+      hi = f;
+    }
+  sup[m] = make_int2(lo, hi);
+}
+
 constexpr int MEL_FR = 20;   // frames per block (3000 = 150 x 20)
 static_assert(NFR % MEL_FR == 0, "mel grid must cover every frame");
 
+// mel = fb^T . |X|^2 over each filter's support only: the in-order fma chain over the support is
+// bit-identical to the dense 201-bin chain (the other terms are fma(0, P, acc) = acc)
 __global__ __launch_bounds__(256) void lm_mel_kernel(const float* __restrict__ S, const float* __restrict__ fb,
-                                                     int n_mels, float* __restrict__ logv,
-                                                     unsigned* __restrict__ mx) {
+                                                     const int2* __restrict__ sup, int n_mels,
+                                                     float* __restrict__ logv, unsigned* __restrict__ mx) {
   __shared__ float P[MEL_FR][NF + 3];
   const int b = blockIdx.y, t0 = blockIdx.x * MEL_FR;
   for (int i = threadIdx.x; i < MEL_FR * NF; i += 256) {
@@ -95,7 +110,8 @@ __global__ __launch_bounds__(256) void lm_mel_kernel(const float* __restrict__ S
   for (int i = threadIdx.x; i < MEL_FR * n_mels; i += 256) {
     const int fr = i / n_mels, m = i - fr * n_mels;
     float acc = 0.f;
-    for (int f = 0; f < NF; ++f) acc = fmaf(fb[f * n_mels + m], P[fr][f], acc);
+    const int2 r = sup[m];
+    for (int f = r.x; f <= r.y; ++f) acc = fmaf(fb[f * n_mels + m], P[fr][f], acc);
     const float v = log10f(fmaxf(acc, 1e-10f));
     logv[((long long)b * NFR + t0 + fr) * n_mels + m] = v;
     lmax = fmaxf(lmax, v);
@@ -153,7 +169,8 @@ int launch_normalize_apply(const float* x, int B, int L, const float* st, float*
 size_t logmel_workspace_bytes(int B, int n_mels) {
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   return al((size_t)LM_NB * N_FFT * 4) + al((size_t)NF * n_mels * 4) + al((size_t)B * NP * 4) +
-         al((size_t)B * NFR * LM_NB * 4) + al((size_t)B * NFR * n_mels * 4) + al((size_t)B * 4) + 256;
+         al((size_t)B * NFR * LM_NB * 4) + al((size_t)B * NFR * n_mels * 4) + al((size_t)B * 4) + 256 +
+         al((size_t)n_mels * 8);
 }
 
 template <typename TO>
@@ -169,11 +186,13 @@ int launch_logmel(const float* x, int B, int L, int n_mels, float* out_hf, TO* o
   float* xp = (float*)p; p += al((size_t)B * NP * 4);
   float* S = (float*)p; p += al((size_t)B * NFR * LM_NB * 4);
   float* logv = (float*)p; p += al((size_t)B * NFR * n_mels * 4);
-  unsigned* mx = (unsigned*)p;
+  unsigned* mx = (unsigned*)p; p += al((size_t)B * 4);
+  int2* sup = (int2*)p;
   if (hipMemsetAsync(zero, 0, 256, s) != hipSuccess) return -2;
   if (hipMemsetAsync(mx, 0, (size_t)B * 4, s) != hipSuccess) return -2;
   hipLaunchKernelGGL(lm_basis_kernel, dim3((LM_NB * N_FFT + 255) / 256), dim3(256), 0, s, basis);
   hipLaunchKernelGGL(lm_filters_kernel, dim3((NF * n_mels + 255) / 256), dim3(256), 0, s, fb, n_mels);
+  hipLaunchKernelGGL(lm_support_kernel, dim3((n_mels + 63) / 64), dim3(64), 0, s, fb, n_mels, sup);
   hipLaunchKernelGGL(lm_pad_kernel, dim3((NP + 255) / 256, B), dim3(256), 0, s, x, L, L < NS ? L : NS, xp, lens);
   if (hipGetLastError() != hipSuccess) return -2;
   GemmArgs g{};
@@ -182,7 +201,7 @@ int launch_logmel(const float* x, int B, int L, int n_mels, float* out_hf, TO* o
   g.Cf = S; g.ldc = LM_NB; g.act = ACT_NONE; g.zero = zero;
   int rc = launch_gemm_f32(g, AMODE_SEG, 1, s);
   if (rc) return rc;
-  hipLaunchKernelGGL(lm_mel_kernel, dim3(NFR / MEL_FR, B), dim3(256), 0, s, S, fb, n_mels, logv, mx);
+  hipLaunchKernelGGL(lm_mel_kernel, dim3(NFR / MEL_FR, B), dim3(256), 0, s, S, fb, sup, n_mels, logv, mx);
   hipLaunchKernelGGL((lm_final_kernel<TO>), dim3((NFR * n_mels + 255) / 256, B), dim3(256), 0, s, logv, mx, n_mels,
                      out_hf, out_cl);
   return hipGetLastError() == hipSuccess ? 0 : -2;
