@@ -179,3 +179,41 @@ def synth_state_dict(spec, seed: int | None = None) -> dict[str, np.ndarray]:
     if isinstance(spec, WavLMSpec):
         return synth_wavlm_state_dict(spec, 7 if seed is None else seed)
     return synth_whisper_state_dict(spec, 11 if seed is None else seed)
+
+
+def outlier_weights(sd: dict, seed: int = 3, n_out: int = 4, gain: float = 30.0, dof: int = 3) -> dict:
+    """A heavy-tailed variant of a synthetic state dict, shaped like real checkpoints' outlier
+    features (stress fixtures for the bf16 / fp8 bars):
+
+    * every LayerNorm / GroupNorm gain gets ``n_out`` channels (picked per tensor by the counter
+      hash) multiplied by ``gain`` -- a few feature dimensions an order of magnitude above the rest;
+    * every projection / conv weight (not biases, embeddings, positions or the positional conv's
+      weight-norm factors) is redrawn Student-t with ``dof`` degrees of freedom, rescaled to the
+      uniform tensor's standard deviation (same scale, far heavier tails).
+
+    Deterministic per key (same transform for the HF-loadable and the packed dictionaries)."""
+    out = {}
+    for key, v in sd.items():
+        v = np.asarray(v)
+        if "layer_norm.weight" in key:
+            w = v.astype(np.float32).copy().reshape(-1)
+            u = uniform01(seed, _stream_of(key + "#out"), n_out)
+            ch = np.unique((u * w.size).astype(np.int64))
+            w[ch] *= np.float32(gain)
+            out[key] = w.reshape(v.shape)
+            continue
+        skip = (v.ndim < 2 or key.endswith(".bias") or "embed" in key or "parametrizations" in key
+                or key.endswith("[0]") or "rel_attn" in key or "gru_rel_pos" in key)
+        if skip:
+            out[key] = v
+            continue
+        n = v.size
+        st = _stream_of(key + "#t")
+        z = gaussian(seed, st, n)
+        chi = np.zeros(n)
+        for k in range(dof):
+            chi += gaussian(seed, st + 1 + k, n) ** 2
+        t = z / np.sqrt(chi / dof)                       # Student-t(dof), variance dof / (dof - 2)
+        t *= float(np.std(v)) / math.sqrt(dof / (dof - 2.0))
+        out[key] = t.astype(np.float32).reshape(v.shape)
+    return out

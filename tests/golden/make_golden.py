@@ -212,10 +212,63 @@ def whisper_golden(ref_h, manifest, spec, tag, n_clips, seed, durations):
                      "note": "decoder: input id 0 at position 0 (REF :257-262); synthetic full_hf decoder tables"}
 
 
+# the fp8 (MX) GEMMs need d_model and ffn multiples of 256: the smallest Whisper shape of the MX tests
+WHISPER_MX_DEC = C.WhisperSpec(d_model=512, layers=3, heads=8, ffn=2048, decoder_layers=1,
+                               name="whisper-mx-test+decoder")
+
+
+def outlier_golden(ref_w, ref_h, manifest):
+    """Stress fixtures: heavy-tailed weights with outlier feature channels (synth.outlier_weights)
+    through the reference's own glue -- WavLM-base (4 clips) and the MX-test Whisper shape (2 clips)."""
+    from transformers import Wav2Vec2FeatureExtractor, WavLMConfig, WavLMModel
+    from transformers import WhisperConfig, WhisperFeatureExtractor, WhisperModel
+    spec = C.WAVLM_BASE
+    sd = synth.outlier_weights(synth.synth_wavlm_state_dict(spec, seed=7))
+    model = WavLMModel(WavLMConfig())
+    missing, unexpected = model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=False)
+    assert not unexpected and set(missing) == {"masked_spec_embed"}, (missing, unexpected)
+    model.eval()
+    clips = synth.synth_clips(4, 48000, seed=1234)
+    paths = _register("wavlm_outlier", clips)
+    idx = spec.default_layer_indices()
+    fe = Wav2Vec2FeatureExtractor(do_normalize=False)
+    t0 = time.time()
+    emb = np.stack([np.stack([ref_w.extract_wavlm_embeddings(p, model, fe, "cpu", idx)[f"layer_{i}"] for i in idx])
+                    for p in paths]).astype(np.float32)
+    manifest["wavlm_outlier_s"] = time.time() - t0
+    spec_w = WHISPER_MX_DEC
+    sdw = synth.outlier_weights(synth.synth_whisper_state_dict(spec_w, seed=21, full_hf=True))
+    cfg = WhisperConfig(d_model=spec_w.d_model, encoder_layers=spec_w.layers, encoder_attention_heads=spec_w.heads,
+                        decoder_layers=spec_w.decoder_layers, decoder_attention_heads=spec_w.heads,
+                        encoder_ffn_dim=spec_w.ffn, decoder_ffn_dim=spec_w.dec_ffn_dim, num_mel_bins=spec_w.n_mels,
+                        vocab_size=spec_w.vocab_size, max_target_positions=spec_w.max_target_positions)
+    wm = WhisperModel(cfg)
+    missing, unexpected = wm.load_state_dict({k: torch.from_numpy(v) for k, v in sdw.items()}, strict=False)
+    assert not unexpected and not missing, (missing, unexpected)
+    wm.eval()
+    wclips = synth.synth_clips(2, 48000, seed=99)
+    wpaths = _register("whisper_outlier", wclips)
+    proc = WhisperFeatureExtractor(feature_size=spec_w.n_mels)
+    eidx = spec_w.default_layer_indices()
+    t0 = time.time()
+    wemb = np.stack([np.stack([ref_h.extract_whisper_embeddings_fixed(p, wm, proc, "cpu", eidx, [1, 0])[f"encoder_layer_{i}"]
+                               for i in eidx]) for p in wpaths]).astype(np.float32)
+    manifest["whisper_outlier_s"] = time.time() - t0
+    np.savez_compressed(os.path.join(HERE, "outlier.npz"), wavlm_emb=emb, wavlm_layer_indices=np.array(idx, np.int32),
+                        whisper_emb=wemb, whisper_layer_indices=np.array(eidx, np.int32))
+    manifest["outlier"] = {"transform": "synth.outlier_weights(seed=3, n_out=4, gain=30, dof=3)",
+                           "wavlm": {"spec": spec.name, "weight_seed": 7, "clip_seed": 1234, "n_clips": 4,
+                                     "weights_sha256": _sd_sha(sd), "clips_sha256": _sha(clips)},
+                           "whisper": {"spec": "d512/3 layers/8 heads/ffn 2048 (+1 decoder layer)", "weight_seed": 21,
+                                       "clip_seed": 99, "n_clips": 2, "clips_sha256": _sha(wclips)},
+                           "reference_fn": ["REF/WavLM_embeddings.py:extract_wavlm_embeddings",
+                                            "REF/whisper_embeddings_large.py:extract_whisper_embeddings_fixed"]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-large", action="store_true")
-    ap.add_argument("--only", default=None, help="wavlm | wavlm_large | whisper_tiny | whisper_large_v2")
+    ap.add_argument("--only", default=None, help="wavlm | wavlm_large | whisper_tiny | outlier | whisper_large_v2")
     args = ap.parse_args()
     torch.set_num_threads(os.cpu_count())
     manifest = {"transformers": transformers.__version__, "torch": torch.__version__, "numpy": np.__version__}
@@ -233,6 +286,8 @@ def main():
                 wavlm_large_golden(ref_w, manifest)
             if only in (None, "whisper_tiny"):
                 whisper_golden(ref_h, manifest, C.WHISPER_TINY_DEC, "whisper_tiny", 2, 11, [3.0, 30.0])
+            if only in (None, "outlier"):
+                outlier_golden(ref_w, ref_h, manifest)
             if not args.skip_large and only in (None, "whisper_large_v2"):
                 whisper_golden(ref_h, manifest, C.WHISPER_LARGE_V2_DEC, "whisper_large_v2", 1, 11, [3.0])
         finally:
