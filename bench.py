@@ -44,9 +44,9 @@ from ssr_amd.model import SSEModel  # noqa: E402
 
 # Algorithmic FLOPs per clip: 2 x MACs of every GEMM/conv + QK^T, AV.
 FLOP_PER_CLIP = {"wavlm-base": 42.39e9, "wavlm-large": 109.6e9, "whisper-large-v2": 2272.67e9}
-# MI355X dense MFMA peaks (MI355X_MICROARCH.md); bf16x3 runs three bf16 products per logical
-# multiply-add, so its model-level peak is the bf16 peak / 3 (its GEMM roofline counts the MFMA work)
-PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3, "fp8": 5000.0, "bf16x3": 2500.0 / 3}
+# MI355X dense MFMA peaks (MI355X_MICROARCH.md); fp16x3 runs three fp16 products per logical
+# multiply-add, so its model-level peak is the fp16 (= bf16) peak / 3 (its GEMM roofline counts the MFMA work)
+PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3, "fp8": 5000.0, "fp16x3": 2500.0 / 3}
 HBM_PEAK_GBS = 8000.0
 
 
@@ -60,8 +60,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=None,
                     help="clips per rank per step (default 256 WavLM / 64 Whisper bf16 / 128 Whisper fp8)")
     ap.add_argument("--seconds", type=float, default=None, help="clip length (default 3 s / 30 s)")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8", "bf16x3"],
-                    help="fp8: Whisper only, MX-fp8 QKV / fc1 / fc2 GEMMs (BASELINE configs[4]); bf16x3: "
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8", "fp16x3"],
+                    help="fp8: Whisper only, MX-fp8 QKV / fc1 / fc2 GEMMs (BASELINE configs[4]); fp16x3: "
                          "WavLM-base, split-bf16 GEMMs, fp32-class (<= 1e-4) embeddings")
     ap.add_argument("--cpu-sample", type=int, default=None, help="clips for the CPU baseline (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-launch event timing")
@@ -181,7 +181,7 @@ def roofline(records, dtype):
     # the MX-fp8 GEMM is priced at the dense fp8 peak, every other kernel at the bf16 (fp32) one
     peak = PEAK_TFLOPS["fp8"] if name == "gemm_mx" else PEAK_TFLOPS["fp32" if dtype == "fp32" else "bf16"]
     mfma_work = 1.0
-    if dtype == "bf16x3" and name == "gemm":   # split-bf16: three bf16 products per logical multiply-add
+    if dtype == "fp16x3" and name == "gemm":   # split-fp16: three fp16 products per logical multiply-add
         mfma_work = 3.0
         achieved *= 3.0
     breakdown = {k: {"ms": round(v[0], 3), "launches": v[3], "share": round(v[0] / total, 4),

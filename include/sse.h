@@ -36,12 +36,14 @@ extern "C" {
 enum sse_kind { SSE_KIND_WAVLM = 0, SSE_KIND_WHISPER = 1 };
 /* SSE_DTYPE_FP8 (Whisper): bf16 activations, the encoder layers' QKV / fc1 / fc2 GEMMs in MX-fp8
  * (OCP e4m3 operands, one E8M0 scale per 32 K-elements, BASELINE configs[4] "fp8 MFMA encoder"). */
-/* SSE_DTYPE_BF16X3 (WavLM with the "group" frontend and post-LN encoder, i.e. WavLM-base): the
- * fp32 path with every dense GEMM / strided conv on the bf16 matrix cores in split form: operands
- * x = hi + lo (two bf16), products hi*hi + lo*hi + hi*lo accumulated in fp32 (the dropped lo*lo term
- * is ~2^-16 relative) -- fp32-class embeddings (<= 1e-4 rel-L2) at ~1/3 of the bf16 GEMM rate, with
- * conv0, the positional conv and the attention core in exact fp32. */
-enum sse_dtype { SSE_DTYPE_F32 = 0, SSE_DTYPE_BF16 = 1, SSE_DTYPE_FP8 = 2, SSE_DTYPE_BF16X3 = 3 };
+/* SSE_DTYPE_FP16X3 (WavLM with the "group" frontend and post-LN encoder, i.e. WavLM-base): the
+ * fp32 path with every dense GEMM / strided conv on the fp16 matrix cores in split form: operands
+ * x = hi + lo (two fp16, the lo plane carried scaled by 2^11 and the weights by a power of two so no
+ * operand is an fp16 subnormal), products hi*hi + lo*hi + hi*lo accumulated in fp32 (~22 significant
+ * bits per operand) -- fp32-class embeddings (<= 1e-4 rel-L2, also with outlier-channel weights) at
+ * ~1/3 of the bf16 GEMM rate, with conv0, the positional conv and the attention core in exact fp32.
+ * Activations must stay inside the fp16 range (|x| < 65504); an overflow shows as non-finite output. */
+enum sse_dtype { SSE_DTYPE_F32 = 0, SSE_DTYPE_BF16 = 1, SSE_DTYPE_FP8 = 2, SSE_DTYPE_FP16X3 = 3 };
 enum sse_err {
   SSE_OK = 0,
   SSE_ERR_INVALID = -1,      /* bad argument / null pointer / bad layer index         */

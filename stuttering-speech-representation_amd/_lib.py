@@ -19,7 +19,7 @@ LIB_PATH = os.path.join(_HERE, "libsse.so")
 SSE_DTYPE_F32 = 0
 SSE_DTYPE_BF16 = 1
 SSE_DTYPE_FP8 = 2   # bf16 activations + MX-fp8 encoder-layer GEMMs (Whisper)
-SSE_DTYPE_BF16X3 = 3   # fp32 activations, split-bf16 (hi/lo) GEMMs: fp32-class results (WavLM-base)
+SSE_DTYPE_FP16X3 = 3   # fp32 activations, split-fp16 (hi/lo) GEMMs: fp32-class results (WavLM-base)
 
 EXPORTED = ("sse_weight_floats", "sse_model_create", "sse_model_destroy", "sse_output_frames",
             "sse_workspace_bytes", "sse_logmel_workspace_bytes", "sse_logmel", "sse_embed",

@@ -9,6 +9,24 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef _Float16 f16;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
+
+// Split-fp16 operands (SSE_DTYPE_FP16X3).  A value v is carried as hi = f16(v) and lo' = f16((v - hi)
+// * 2^11): lo' keeps the magnitude of v, so it stays a normal fp16 for every v the fp16 range holds
+// (an unscaled lo would fall into fp16 subnormals for |v| < 2^-3).  Activation rows are [hi | lo' | hi]
+// and weight rows (pre-scaled by 2^s) [hi | hi * 2^-11 | lo] per K-block, so one f16 MFMA over
+// K' = 3K accumulates hi*hi + lo*hi + hi*lo: about 22 significant bits per operand (the dropped
+// lo*lo term is ~2^-22 relative).
+constexpr float X3_LO_SCALE = 2048.f;
+__host__ __device__ inline void x3_split4(const f32x4& v, f16x4& hi, f16x4& lo) {
+  #pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    hi[e] = (f16)v[e];
+    lo[e] = (f16)((v[e] - (float)hi[e]) * X3_LO_SCALE);
+  }
+}
 
 #define SSE_DEV __device__ __forceinline__
 
@@ -183,8 +201,11 @@ struct GemmArgs {
   // bf16 residual [M][ldc] (instead of resid; folded post-LN path: the residual stream is kept in
   // bf16 and the output is bf16 Ct only)
   const bf16* resid_t;
-  // split-bf16 output (SSE_DTYPE_BF16X3): Ct is the next GEMM's tripled operand [M][3N] (ldc = 3N),
-  // row = [hi | lo | hi] with hi = bf16(v), lo = bf16(v - hi)
+  // split-fp16 GEMM (SSE_DTYPE_FP16X3): A / B are fp16 planes (x3_split4), the MFMA is the f16 one and
+  // the epilogue scales the accumulator by alpha (the weights' power-of-two scale undone).  ct3: Ct is
+  // the next GEMM's tripled operand [M][3N] (ldc = 3N), row = [hi | lo' | hi].
+  int f16;
+  float alpha;
   int ct3;
 };
 

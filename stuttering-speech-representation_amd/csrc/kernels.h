@@ -34,10 +34,10 @@ template <typename TI, typename TO>
 int launch_layernorm(const TI* in, const float* w, const float* b, int rows, int H, float eps, int act,
                      float* out_f, TO* out_t, hipStream_t s, float2* stats = nullptr);
 
-// split-bf16 (SSE_DTYPE_BF16X3) operands: tripled rows [hi | lo | hi] (common.h GemmArgs.ct3)
+// split-fp16 (SSE_DTYPE_FP16X3) operands: tripled rows [hi | lo' | hi] (common.h x3_split4)
 int launch_layernorm_x3(const void* in, bool in3, const float* w, const float* b, int rows, int H, float eps,
-                        float* out_f, bf16* out3, hipStream_t s);
-int launch_split3(const float* x, long long rows, int C, bf16* y, hipStream_t s);
+                        float* out_f, f16* out3, hipStream_t s);
+int launch_split3(const float* x, long long rows, int C, f16* y, hipStream_t s);
 
 // MX-fp8 (e4m3 + E8M0 per 32 K-elements) GEMM operands, layouts in common.h
 int launch_layernorm_mx(const float* in, const float* w, const float* b, int rows, int H, float eps,

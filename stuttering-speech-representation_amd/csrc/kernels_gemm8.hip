@@ -130,6 +130,14 @@ template <int OA, int OB>
 SSE_DEV f32x4 g8_mx(i32x8 a, i32x8 b, f32x4 c, int sa, int sb) {
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, OA, sa, OB, sb);
 }
+// 16x16x32 MFMA on bf16 or (split-fp16 path) fp16 operands; the 16-B fragments are the same bytes
+template <bool F16>
+SSE_DEV f32x4 g8_mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
 template <int I, int N, typename F>
 SSE_DEV void g8_sfor(F&& f) {   // f(integral_constant<int, I>) for I .. N-1, compile-time indices
   if constexpr (I < N) {
@@ -692,9 +700,10 @@ constexpr int G8P_SMEM = G8_OPS + 2 * G8P_EP;
 //   o = act(rstd_m * acc + (bias[n] - rstd_m mean_m acol[n]))   (folded LayerNorm of A, GemmArgs.apart)
 //   o = act(acc + bias[n])                                        (otherwise: rstd = 1 and the acol term
 //                                                                  is not formed, bit-identical to a plain add)
-template <int ACT, bool CT3>
+template <int ACT, bool CT3, bool F16>
 SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, int n0, int wm, int wn, int q,
                           int r16, const char* ep, bool has_bias, bool fold) {
+  const float alpha = F16 ? g.alpha : 1.f;   // split-fp16: the weights' 2^s undone (exact)
   f32x4 bv[2][2], ac[2][2];
   #pragma unroll
   for (int ni = 0; ni < 2; ++ni)
@@ -714,7 +723,7 @@ SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, i
       const float2* p = (const float2*)(ep + 2048) + (mi * 128 + wm * 64 + i * 16 + r16) * 3;
       const float2 v[3] = {p[0], p[1], p[2]};
       const float2 st = ln_part_combine<3>(v, g.ln_eps);
-      ast[mi][i] = fold ? st : make_float2(0.f, 1.f);
+      ast[mi][i] = fold ? st : make_float2(0.f, alpha);
     }
   auto finish_half = [&](int mi) {
     #pragma unroll
@@ -755,9 +764,22 @@ SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, i
         }
         if (g.Ct) {
           const f32x4 o0 = acc[mi][ni][i][0], o1 = acc[mi][ni][i][1];
-          const bf16x4 x0 = {(bf16)o0[0], (bf16)o0[1], (bf16)o0[2], (bf16)o0[3]};
-          const bf16x4 x1 = {(bf16)o1[0], (bf16)o1[1], (bf16)o1[2], (bf16)o1[3]};
-          const uint2 X = __builtin_bit_cast(uint2, x0), Y = __builtin_bit_cast(uint2, x1);
+          uint2 X, Y, LX, LY;   // hi (and, CT3, the lo' plane) of the two j blocks
+          if constexpr (F16) {
+            f16x4 h0, h1, l0, l1;
+            x3_split4(o0, h0, l0);
+            x3_split4(o1, h1, l1);
+            X = __builtin_bit_cast(uint2, h0);
+            Y = __builtin_bit_cast(uint2, h1);
+            LX = __builtin_bit_cast(uint2, l0);
+            LY = __builtin_bit_cast(uint2, l1);
+          } else {
+            const bf16x4 x0 = {(bf16)o0[0], (bf16)o0[1], (bf16)o0[2], (bf16)o0[3]};
+            const bf16x4 x1 = {(bf16)o1[0], (bf16)o1[1], (bf16)o1[2], (bf16)o1[3]};
+            X = __builtin_bit_cast(uint2, x0);
+            Y = __builtin_bit_cast(uint2, x1);
+            LX = LY = make_uint2(0u, 0u);
+          }
           const auto s0 = __builtin_amdgcn_permlane16_swap(X.x, Y.x, false, false);
           const auto s1 = __builtin_amdgcn_permlane16_swap(X.y, Y.y, false, false);
           const long long c = n0 + ni * 128 + wn * 32 + (q & 1) * 16 + (q >> 1) * 8;
@@ -766,14 +788,7 @@ SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, i
             *(uint4*)((bf16*)g.Ct + row + c) = v;
             if constexpr (CT3) *(uint4*)((bf16*)g.Ct + row + 2 * g.N + c) = v;
           }
-          if constexpr (CT3) {   // lo plane: bf16(v - hi)
-            bf16x4 l0, l1;
-            #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              l0[e] = (bf16)(o0[e] - (float)x0[e]);
-              l1[e] = (bf16)(o1[e] - (float)x1[e]);
-            }
-            const uint2 LX = __builtin_bit_cast(uint2, l0), LY = __builtin_bit_cast(uint2, l1);
+          if constexpr (CT3) {   // lo' plane
             const auto t0 = __builtin_amdgcn_permlane16_swap(LX.x, LY.x, false, false);
             const auto t1 = __builtin_amdgcn_permlane16_swap(LX.y, LY.y, false, false);
             if (ok) *(uint4*)((bf16*)g.Ct + row + g.N + c) = make_uint4(t0[0], t1[0], t0[1], t1[1]);
@@ -796,7 +811,7 @@ SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, i
 // flight -- the next tile's first K-tile waits vmcnt(2n + S) (S = store instructions issued after
 // its prologue), so it needs only the prologue loads and the stores drain under its MFMAs.
 // ======================================================================================
-template <int ACT, bool CT3 = false>
+template <int ACT, bool CT3 = false, bool F16 = false>
 __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
   __shared__ __attribute__((aligned(16))) char smem[G8P_SMEM];   // operands | 2 epilogue slots: the ONLY shared object
   const int lane = threadIdx.x & 63;
@@ -914,7 +929,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
       #pragma unroll
       for (int i = 0; i < 4; ++i)
         #pragma unroll
-        for (int j = 0; j < 2; ++j) c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][ks], af[i][ks], c[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) c[i][j] = g8_mfma<F16>(bf[j][ks], af[i][ks], c[i][j]);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -989,7 +1004,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
       setup(next);
       for (int k = -6; k < 0; ++k) issue(k);
     }
-    g8p_epilogue<ACT, CT3>(g, acc, m0, n0, wm, wn, q, r16, smem + G8_OPS + slot * G8P_EP, has_bias, fold);
+    g8p_epilogue<ACT, CT3, F16>(g, acc, m0, n0, wm, wn, q, r16, smem + G8_OPS + slot * G8P_EP, has_bias, fold);
     if (next < 0) break;
     slot ^= 1;
     S = m0 + 256 <= M ? s_full : 0;
@@ -1010,7 +1025,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
 // reduces its 64 columns (16 in-lane values, lanes q = 0..3) to (mean_c, M2_c), the 4 waves' chunks
 // meet in LDS and one thread per row combines them (Chan) into the 256-column (mean_t, M2_t).
 // ======================================================================================
-template <bool LN, bool OPART, bool RB>
+template <bool LN, bool OPART, bool RB, bool F16 = false>
 __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[G8_OPS];   // the ONLY shared object
   const int lane = threadIdx.x & 63;
@@ -1104,7 +1119,7 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
       #pragma unroll
       for (int i = 0; i < 4; ++i)
         #pragma unroll
-        for (int j = 0; j < 2; ++j) c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][ks], af[i][ks], c[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) c[i][j] = g8_mfma<F16>(bf[j][ks], af[i][ks], c[i][j]);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -1227,6 +1242,9 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
   // column parameters are read from LDS where they are used (registers hold acc + one half's rows)
   float2* cst = (float2*)(smem + 16384);
   auto finish_half = [&](int mi) {
+    // compiler memory barrier: the column parameters are re-read from LDS per half (without it the
+    // second half's reads are merged with the first's and held live across the stores: spills)
+    asm volatile("" ::: "memory");
     unpack_half();
     #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1250,7 +1268,7 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
           }
           const f32x4 bvv = *(const f32x4*)(smem + c * 4);
           const f32x4 bv = has_bias ? bvv : f32x4{0.f, 0.f, 0.f, 0.f};
-          f32x4 o = (acc[mi][ni][i][j] + bv) + r;
+          f32x4 o = ((F16 ? acc[mi][ni][i][j] * g.alpha : acc[mi][ni][i][j]) + bv) + r;
           if constexpr (RB) {   // bf16 output: the statistics describe the rounded values
             #pragma unroll
             for (int e = 0; e < 4; ++e) o[e] = (float)(bf16)o[e];
@@ -1338,8 +1356,18 @@ int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
   if ((a.apart && a.apart_nt != 3) || (a.rpart && a.rpart_nt != 3) || (a.opart && a.N != 768)) return -3;
   dim3 grid((unsigned)(((a.M + 255) / 256) * (a.N / 256)));
   // OPT_GEMM_NONPERSIST (tests, A/B): the non-persistent LDS-staged kernel for every shape
-  if (a.ct3 && (a.resid || a.resid_t || !a.Ct)) return -3;   // split-bf16 output: persistent kernel only
-  if (sse_opt(OPT_GEMM_NONPERSIST) && !a.resid_t && !a.ct3) {
+  if (a.ct3 && (a.resid || a.resid_t || !a.Ct || !a.f16)) return -3;   // split output: persistent kernel only
+  if (a.f16) {
+    // split-fp16 (SSE_DTYPE_FP16X3): residual GEMMs (fp32 out), ct3 + GELU, or plain fp32 out
+    if (a.resid_t || a.rstats || a.rpart || a.opart || a.apart || a.resid_rows || a.alpha == 0.f) return -3;
+    if (a.resid) {
+      if (!a.Cf || a.Ct) return -3;
+      hipLaunchKernelGGL((gemm8r_kernel<false, false, false, true>), grid, dim3(512), 0, s, a);
+      return hipGetLastError() == hipSuccess ? 0 : -2;
+    }
+    if (a.ct3 ? (a.act != ACT_GELU || a.Cf) : (a.act != ACT_NONE || !a.Cf || a.Ct)) return -3;
+  }
+  if (sse_opt(OPT_GEMM_NONPERSIST) && !a.resid_t && !a.f16) {
     hipLaunchKernelGGL((gemm8_kernel<0, false, false>), grid, dim3(512), 0, s, a);
   } else if (a.resid_t) {
     // bf16 residual stream (folded post-LN path): bf16 out only
@@ -1371,13 +1399,11 @@ int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
       return -2;
     const int n_tiles = (int)grid.x;
     const int G = n_tiles < cus[dev] ? n_tiles : cus[dev];
-    if (a.ct3) {   // split-bf16 output (bf16x3 path): erf-GELU or none
-      if (a.act == ACT_GELU)
-        hipLaunchKernelGGL((gemm8p_kernel<ACT_GELU, true>), dim3(G), dim3(512), 0, s, a, n_tiles);
-      else if (a.act == ACT_NONE)
-        hipLaunchKernelGGL((gemm8p_kernel<ACT_NONE, true>), dim3(G), dim3(512), 0, s, a, n_tiles);
+    if (a.f16) {   // split-fp16: ct3 + erf-GELU (conv layers, ffn1) or fp32 out (proj, qkv)
+      if (a.ct3)
+        hipLaunchKernelGGL((gemm8p_kernel<ACT_GELU, true, true>), dim3(G), dim3(512), 0, s, a, n_tiles);
       else
-        return -3;
+        hipLaunchKernelGGL((gemm8p_kernel<ACT_NONE, false, true>), dim3(G), dim3(512), 0, s, a, n_tiles);
     } else if (a.act == ACT_GELU)
       hipLaunchKernelGGL(gemm8p_kernel<ACT_GELU>, dim3(G), dim3(512), 0, s, a, n_tiles);
     else if (a.act == ACT_GELU_FAST)

@@ -462,6 +462,14 @@ template <> SSE_DEV f32x4 load4<bf16>(const bf16* p) {
   const bf16x4 v = *(const bf16x4*)p;
   return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
 }
+// a split-fp16 value from its hi plane (p) and lo' plane (p + H): hi + lo' * 2^-11
+SSE_DEV f32x4 load4_x3(const f16* p, int H) {
+  const f16x4 h = *(const f16x4*)p, l = *(const f16x4*)(p + H);
+  f32x4 o;
+  #pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = fmaf((float)l[e], 1.f / X3_LO_SCALE, (float)h[e]);
+  return o;
+}
 
 // MX-fp8 quantisation of 4 consecutive values (columns c..c+3 of row `row`, K = H) held by a lane
 // whose 7 neighbours (lane ^ 1, 2, 4) hold the rest of the 32-column block: amax, E8M0 exponent
@@ -476,8 +484,8 @@ SSE_DEV void mx_quant4(f32x4 o, unsigned char* dst, unsigned char* scale, long l
   if ((lane & 7) == 0) scale[mx_a_scale_off(row, c >> 5, K >> 7)] = (unsigned char)e;
 }
 
-// IN3 / OUT3 (split-bf16 bf16x3 path, TI / TO = bf16): rows are tripled [hi | lo | hi] of 3H; the
-// input value is hi + lo, the output writes hi = bf16(y), lo = bf16(y - hi), hi.
+// IN3 / OUT3 (split-fp16 path, TI / TO = f16): rows are tripled [hi | lo' | hi] of 3H (x3_split4);
+// the input value is hi + lo' 2^-11.
 template <typename TI, typename TO, bool IN3 = false, bool OUT3 = false>
 __global__ __launch_bounds__(256) void layernorm_kernel(const TI* __restrict__ in, const float* __restrict__ w,
                                                         const float* __restrict__ bta, int rows, int H,
@@ -494,8 +502,8 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TI* __restrict__ i
   for (int i = 0; i < 8; ++i) {
     const int g = lane + 64 * i;
     if (g < n4) {
-      v[i] = load4<TI>(x + 4 * g);
-      if constexpr (IN3) v[i] += load4<TI>(x + H + 4 * g);
+      if constexpr (IN3) v[i] = load4_x3(x + 4 * g, H);
+      else v[i] = load4<TI>(x + 4 * g);
       s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
     }
   }
@@ -528,12 +536,11 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TI* __restrict__ i
       if (out_f) *(f32x4*)(out_f + off) = o;
       if constexpr (OUT3) {
         const long long o3 = (long long)row * 3 * H + c;
-        const bf16x4 hi = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
-        const bf16x4 lo = {(bf16)(o[0] - (float)hi[0]), (bf16)(o[1] - (float)hi[1]), (bf16)(o[2] - (float)hi[2]),
-                           (bf16)(o[3] - (float)hi[3])};
-        *(bf16x4*)((bf16*)out_t + o3) = hi;
-        *(bf16x4*)((bf16*)out_t + o3 + H) = lo;
-        *(bf16x4*)((bf16*)out_t + o3 + 2 * H) = hi;
+        f16x4 hi, lo;
+        x3_split4(o, hi, lo);
+        *(f16x4*)((f16*)out_t + o3) = hi;
+        *(f16x4*)((f16*)out_t + o3 + H) = lo;
+        *(f16x4*)((f16*)out_t + o3 + 2 * H) = hi;
       } else if constexpr (sizeof(TO) == 1) {
         // MX-fp8 GEMM operand (A layout): 8 lanes = one 32-column block (H % 32 == 0, so a block's
         // lanes are active together); out_t is e4m3 bytes, stats carries the scale tensor
@@ -644,37 +651,35 @@ int launch_layernorm(const TI* in, const float* w, const float* b, int rows, int
 template int launch_layernorm<float, float>(const float*, const float*, const float*, int, int, float, int,
                                             float*, float*, hipStream_t, float2*);
 
-// split-bf16 (bf16x3) LayerNorm: input fp32 [rows][H] or tripled bf16 [rows][3H] (in3), output fp32
-// (optional) and tripled bf16 [rows][3H]
+// split-fp16 LayerNorm: input fp32 [rows][H] or tripled f16 [rows][3H] (in3), output fp32 (optional)
+// and tripled f16 [rows][3H]
 int launch_layernorm_x3(const void* in, bool in3, const float* w, const float* b, int rows, int H, float eps,
-                        float* out_f, bf16* out3, hipStream_t s) {
+                        float* out_f, f16* out3, hipStream_t s) {
   if (H % 4 || H > 2048 || !out3) return -3;
   if (in3)
-    hipLaunchKernelGGL((layernorm_kernel<bf16, bf16, true, true>), dim3((rows + 3) / 4), dim3(256), 0, s,
-                       (const bf16*)in, w, b, rows, H, eps, (int)ACT_NONE, out_f, out3, (float2*)nullptr);
+    hipLaunchKernelGGL((layernorm_kernel<f16, f16, true, true>), dim3((rows + 3) / 4), dim3(256), 0, s,
+                       (const f16*)in, w, b, rows, H, eps, (int)ACT_NONE, out_f, out3, (float2*)nullptr);
   else
-    hipLaunchKernelGGL((layernorm_kernel<float, bf16, false, true>), dim3((rows + 3) / 4), dim3(256), 0, s,
+    hipLaunchKernelGGL((layernorm_kernel<float, f16, false, true>), dim3((rows + 3) / 4), dim3(256), 0, s,
                        (const float*)in, w, b, rows, H, eps, (int)ACT_NONE, out_f, out3, (float2*)nullptr);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-// fp32 [rows][C] -> tripled bf16 [rows][3C] ([hi | lo | hi]), 4 values per thread
+// fp32 [rows][C] -> tripled f16 [rows][3C] ([hi | lo' | hi], x3_split4), 4 values per thread
 __global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ x, long long n4, int C,
-                                                     bf16* __restrict__ y) {
+                                                     f16* __restrict__ y) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= n4) return;
   const long long e = i * 4, r = e / C, c = e - r * C;
-  const f32x4 v = *(const f32x4*)(x + e);
-  const bf16x4 hi = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-  const bf16x4 lo = {(bf16)(v[0] - (float)hi[0]), (bf16)(v[1] - (float)hi[1]), (bf16)(v[2] - (float)hi[2]),
-                     (bf16)(v[3] - (float)hi[3])};
-  bf16* o = y + r * 3 * C + c;
-  *(bf16x4*)o = hi;
-  *(bf16x4*)(o + C) = lo;
-  *(bf16x4*)(o + 2 * C) = hi;
+  f16x4 hi, lo;
+  x3_split4(*(const f32x4*)(x + e), hi, lo);
+  f16* o = y + r * 3 * C + c;
+  *(f16x4*)o = hi;
+  *(f16x4*)(o + C) = lo;
+  *(f16x4*)(o + 2 * C) = hi;
 }
 
-int launch_split3(const float* x, long long rows, int C, bf16* y, hipStream_t s) {
+int launch_split3(const float* x, long long rows, int C, f16* y, hipStream_t s) {
   if (C % 4) return -3;
   const long long n4 = rows * C / 4;
   hipLaunchKernelGGL(split3_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, n4, C, y);

@@ -16,6 +16,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <algorithm>
 #include <mutex>
 #include <new>
 #include <string>
@@ -133,26 +135,32 @@ struct Arena {
     return off;
   }
   size_t put_f32(const float* src, size_t n) { return put(src, n * 4); }
-  // split-bf16 GEMM weight (SSE_DTYPE_BF16X3): rows of nblk blocks of blk values (a conv tap is a block)
-  // -> per block [hi | hi | lo], hi = bf16(w), lo = bf16(w - hi): matched to activation rows
-  // [hi | lo | hi], the K-sum is hi*hi + lo*hi + hi*lo
+  // split-fp16 GEMM weight (SSE_DTYPE_FP16X3, common.h x3_split4): rows of nblk blocks of blk values
+  // (a conv tap is a block), scaled by 2^e so that max |w| 2^e <= 2^14, -> per block
+  // [hi | hi * 2^-11 | lo], hi = f16(w 2^e), lo = f16(w 2^e - hi): matched to activation rows
+  // [hi | lo' | hi] the K-sum is 2^e (hi*hi + lo*hi + hi*lo); alpha[offset] = 2^-e undoes the scale in
+  // the GEMM epilogue (powers of two: exact)
+  std::map<size_t, float> alpha;
   size_t put_x3(const std::vector<float>& v, size_t rows, int nblk, int blk) {
-    std::vector<uint16_t> h(v.size() * 3);
+    float amax = 0.f;
+    for (float w : v) amax = std::fmax(amax, std::fabs(w));
+    int e = 0;
+    if (amax > 0.f && std::isfinite(amax)) e = std::min(60, std::max(-60, (int)std::floor(std::log2(16384.0 / amax))));
+    const float sc = std::ldexp(1.f, e);
+    std::vector<f16> h(v.size() * 3);
     for (size_t r = 0; r < rows; ++r)
       for (int j = 0; j < nblk; ++j)
         for (int c = 0; c < blk; ++c) {
-          const float w = v[(r * nblk + j) * blk + c];
-          const uint16_t hi = f2bf_bits(w);
-          float hf;
-          const uint32_t u = (uint32_t)hi << 16;
-          std::memcpy(&hf, &u, 4);
-          const uint16_t lo = f2bf_bits(w - hf);
-          uint16_t* o = h.data() + (r * nblk + j) * 3 * (size_t)blk;
+          const float w = v[(r * nblk + j) * blk + c] * sc;
+          const f16 hi = (f16)w;
+          f16* o = h.data() + (r * nblk + j) * 3 * (size_t)blk;
           o[c] = hi;
-          o[blk + c] = hi;
-          o[2 * blk + c] = lo;
+          o[blk + c] = (f16)((float)hi * (1.f / X3_LO_SCALE));
+          o[2 * blk + c] = (f16)(w - (float)hi);
         }
-    return put(h.data(), h.size() * 2);
+    const size_t off = put(h.data(), h.size() * 2);
+    alpha[off] = std::ldexp(1.f, -e);
+    return off;
   }
   size_t put_elem(const std::vector<float>& v, bool bf) {
     if (!bf) return put(v.data(), v.size() * 4);
@@ -240,7 +248,12 @@ struct sse_model {
 
   template <typename X = void> const X* ptr(size_t off) const { return (const X*)(dmem + off); }
   bool bf() const { return dtype == SSE_DTYPE_BF16 || dtype == SSE_DTYPE_FP8; }   // bf16 activations
-  bool x3() const { return dtype == SSE_DTYPE_BF16X3; }   // split-bf16 GEMMs, fp32 activations
+  bool x3() const { return dtype == SSE_DTYPE_FP16X3; }   // split-fp16 GEMMs, fp32 activations
+  std::map<size_t, float> x3_alpha;   // split-fp16 weight offset -> epilogue scale (Arena::put_x3)
+  float alpha(size_t off) const {
+    const auto it = x3_alpha.find(off);
+    return it == x3_alpha.end() ? 0.f : it->second;   // 0: the GEMM launcher rejects the call
+  }
   bool mx() const { return dtype == SSE_DTYPE_FP8; }   // MX-fp8 encoder-layer GEMMs (Whisper)
 };
 
@@ -897,14 +910,15 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
   return 0;
 }
 
-// ---- SSE_DTYPE_BF16X3: the fp32 path with split-bf16 GEMMs ----------------------------------
-// Every GEMM operand is stored tripled, a row [hi | lo | hi] of 3K bf16 (hi = bf16(v), lo =
-// bf16(v - hi)); the weights [hi | hi | lo] per K-block (Arena::put_x3).  The bf16 8-phase kernels
-// then run unchanged on K' = 3K and accumulate hi*hi + lo*hi + hi*lo in fp32 (the dropped lo*lo is
-// ~2^-16 relative).  Strided convs keep their overlapping-row addressing: a frame is 3C values, a
-// window of k frames k*3C.  conv0 + GroupNorm + GELU, the positional conv and the attention core
-// (scores, softmax, P.V) run in exact fp32 as in the fp32 path; LayerNorms read / write fp32 and
-// tripled rows.
+// ---- SSE_DTYPE_FP16X3: the fp32 path with split-fp16 GEMMs ----------------------------------
+// Every GEMM operand is stored tripled (common.h x3_split4): an activation row [hi | lo' | hi] of 3K
+// fp16 (hi = f16(v), lo' = f16((v - hi) 2^11)), the weights 2^e-scaled [hi | hi 2^-11 | lo] per
+// K-block (Arena::put_x3).  The 8-phase kernels run on K' = 3K with the f16 MFMA and accumulate
+// hi*hi + lo*hi + hi*lo in fp32 (~22 significant bits per operand; the dropped lo*lo is ~2^-22
+// relative); the epilogue scales by alpha = 2^-e.  Strided convs keep their overlapping-row
+// addressing: a frame is 3C values, a window of k frames k*3C.  conv0 + GroupNorm + GELU, the
+// positional conv and the attention core (scores, softmax, P.V) run in exact fp32 as in the fp32
+// path; LayerNorms read / write fp32 and tripled rows.
 struct X3Ws {
   size_t zero, norm, part, ss, c0, bufA, bufB, x, xt, xb, qkv, ctx, ctx3, ff, fr;
 };
@@ -962,16 +976,18 @@ int wavlm_forward_x3(sse_model* m, const float* wave, int B, int L, const Sink& 
     RC(launch_wave_stats(wave, B, L, (float*)(ws + w.norm), s, lens));
     norm = (const float*)(ws + w.norm);
   }
-  // split-bf16 GEMM: logical K (the FLOP count), physical operands K' = 3K
+  // split-fp16 GEMM: logical K (the FLOP count), physical operands K' = 3K
   auto gemm3 = [&](const char* tag, GemmArgs& g, int Klog) {
     g.zero = zero;
+    g.f16 = 1;
+    g.alpha = m->alpha((size_t)((const char*)g.B - m->dmem));
     return prof(m, s, tag, 2.0 * g.M * (double)g.N * Klog, gbytes<bf16>(g), [&] { return launch_gemm8_bf16(g, s); });
   };
   // ---- conv feature encoder: conv0 + GroupNorm + GELU in fp32, then tripled ----
   const int C0 = c.conv_dim[0];
   float* c0 = (float*)(ws + w.c0);
   const float* b0 = m->conv_b[0] ? m->ptr<float>(m->conv_b[0]) : nullptr;
-  bf16* bufs[2] = {(bf16*)(ws + w.bufA), (bf16*)(ws + w.bufB)};
+  f16* bufs[2] = {(f16*)(ws + w.bufA), (f16*)(ws + w.bufB)};
   RC(prof(m, s, "conv0_gn", 2.0 * B * (double)Ts[0] * C0 * c.conv_kernel[0], 0, [&] {
     return launch_conv0_gn<float>(wave, B, L, norm, m->ptr<float>(m->conv_w[0]), b0, C0, c.conv_kernel[0],
                                   c.conv_stride[0], Ts[0], m->ptr<float>(m->conv_ln_w[0]), m->ptr<float>(m->conv_ln_b[0]),
@@ -987,11 +1003,11 @@ int wavlm_forward_x3(sse_model* m, const float* wave, int B, int L, const Sink& 
     g.Ct = bufs[i & 1]; g.ct3 = 1; g.ldc = 3 * co; g.act = ACT_GELU;
     RC(gemm3("gemm:conv", g, k * cin));
   }
-  const bf16* feat = bufs[(c.n_conv - 1) & 1];
+  const f16* feat = bufs[(c.n_conv - 1) & 1];
   const int C = c.conv_dim[c.n_conv - 1];
   float* x = (float*)(ws + w.x);
   float* xt = (float*)(ws + w.xt);
-  bf16* xb = (bf16*)(ws + w.xb);
+  f16* xb = (f16*)(ws + w.xb);
   // ---- feature projection ----
   RC(launch_layernorm_x3(feat, true, m->ptr<float>(m->fp_ln_w), m->ptr<float>(m->fp_ln_b), M, C, eps, nullptr, xb, s));
   {
@@ -1016,14 +1032,16 @@ int wavlm_forward_x3(sse_model* m, const float* wave, int B, int L, const Sink& 
   RC(sink.emit(0, x));
   float* qkv = (float*)(ws + w.qkv);
   float* ctx = (float*)(ws + w.ctx);
-  bf16* ctx3 = (bf16*)(ws + w.ctx3);
-  bf16* ff = (bf16*)(ws + w.ff);
+  f16* ctx3 = (f16*)(ws + w.ctx3);
+  f16* ff = (f16*)(ws + w.ff);
   for (int l = 0; l < c.layers; ++l) {
     const LayerW& Lw = m->layers[l];
     GemmArgs g{};
     g.A = xb; g.B = m->ptr(Lw.qkv_w); g.M = M; g.N = m->ldq; g.K = 3 * H;
     g.rows_per_seg = M; g.lda = 3 * H; g.bias = m->ptr<float>(Lw.qkv_b); g.Cf = qkv; g.ldc = m->ldq;
     g.zero = zero;
+    g.f16 = 1;
+    g.alpha = m->alpha(Lw.qkv_w);
     RC(prof(m, s, "gemm:qkv", 2.0 * M * (3.0 * H + 8.0 * nh) * H, gbytes<bf16>(g),
             [&] { return launch_gemm8_bf16(g, s); }));
     AttnArgs a{};
@@ -1310,10 +1328,10 @@ size_t sse_weight_floats(const sse_cfg* cfg) {
 int sse_model_create(const sse_cfg* cfg, const float* host_weights, size_t nbytes, int device, int dtype,
                      sse_model** out) {
   if (!out || !host_weights || !cfg_valid(cfg) ||
-      (dtype != SSE_DTYPE_F32 && dtype != SSE_DTYPE_BF16 && dtype != SSE_DTYPE_FP8 && dtype != SSE_DTYPE_BF16X3))
+      (dtype != SSE_DTYPE_F32 && dtype != SSE_DTYPE_BF16 && dtype != SSE_DTYPE_FP8 && dtype != SSE_DTYPE_FP16X3))
     return SSE_ERR_INVALID;
-  // split-bf16: WavLM "group" frontend + post-LN encoder (WavLM-base); every GEMM N % 256 == 0
-  if (dtype == SSE_DTYPE_BF16X3 &&
+  // split-fp16: WavLM "group" frontend + post-LN encoder (WavLM-base); every GEMM N % 256 == 0
+  if (dtype == SSE_DTYPE_FP16X3 &&
       (cfg->kind != SSE_KIND_WAVLM || cfg->feat_norm_layer || cfg->stable_layer_norm || cfg->hidden % 256 ||
        cfg->ffn % 256 || cfg->conv_dim[0] != 512 || cfg->conv_bias))
     return SSE_ERR_UNSUPPORTED;
@@ -1333,6 +1351,7 @@ int sse_model_create(const sse_cfg* cfg, const float* host_weights, size_t nbyte
   const int rc = cfg->kind == SSE_KIND_WAVLM ? build_wavlm(m, bl, ar) : build_whisper(m, bl, ar);
   if (rc != SSE_OK || bl.off != need) { delete m; return SSE_ERR_WEIGHTS; }
   m->zero = ar.put(nullptr, 256);
+  m->x3_alpha = ar.alpha;
   int prev = -1;
   if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) { delete m; return SSE_ERR_HIP; }
   m->dbytes = ar.size;

@@ -20,7 +20,7 @@ from .config import WavLMSpec, WhisperSpec, param_specs
 
 DTYPES = {"fp32": _lib.SSE_DTYPE_F32, "float32": _lib.SSE_DTYPE_F32, "f32": _lib.SSE_DTYPE_F32,
           "bf16": _lib.SSE_DTYPE_BF16, "bfloat16": _lib.SSE_DTYPE_BF16,
-          "fp8": _lib.SSE_DTYPE_FP8, "mxfp8": _lib.SSE_DTYPE_FP8, "bf16x3": _lib.SSE_DTYPE_BF16X3}
+          "fp8": _lib.SSE_DTYPE_FP8, "mxfp8": _lib.SSE_DTYPE_FP8, "fp16x3": _lib.SSE_DTYPE_FP16X3}
 
 
 def _as_numpy(v) -> np.ndarray:
@@ -61,8 +61,8 @@ def pack_weights(spec, state_dict: dict) -> np.ndarray:
 
 
 class SSEModel:
-    """One model on one GPU.  ``dtype``: "bf16" (throughput path), "fp32" (parity path), "bf16x3"
-    (WavLM-base: fp32 activations, split-bf16 GEMMs -- fp32-class parity at ~3x the fp32 path's
+    """One model on one GPU.  ``dtype``: "bf16" (throughput path), "fp32" (parity path), "fp16x3"
+    (WavLM-base: fp32 activations, split-fp16 GEMMs -- fp32-class parity at ~3x the fp32 path's
     throughput) or "fp8" (Whisper only: bf16 activations, MX-fp8 QKV / fc1 / fc2 GEMMs, BASELINE
     configs[4])."""
 

@@ -242,17 +242,17 @@ def test_clip_longer_than_bias_table(dtype, tol, wavlm_sd):
 def mx3(wavlm_sd):
     from ssr_amd import config as C
     from ssr_amd.model import SSEModel
-    return SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype="bf16x3")
+    return SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype="fp16x3")
 
 
-def test_bf16x3_embed_matches_reference(mx3, wavlm_clips, golden_wavlm):
-    """Split-bf16 GEMMs (operands hi + lo, three bf16 products accumulated in fp32): the north star's
+def test_fp16x3_embed_matches_reference(mx3, wavlm_clips, golden_wavlm):
+    """Split-fp16 GEMMs (operands hi + lo, three fp16 products accumulated in fp32): the north star's
     fp32 bar, pooled rel-L2 <= 1e-4 against the reference's own fixture, with and without the
     feature extractor's normalisation; every hidden state of one clip too."""
     idx = [int(i) for i in golden_wavlm["layer_indices"]]
     got = mx3.embed(torch.from_numpy(wavlm_clips).cuda(), idx).cpu().numpy()
     rel = _rel(got, golden_wavlm["emb_norm0"])
-    print("bf16x3 max rel-L2", rel.max())
+    print("fp16x3 max rel-L2", rel.max())
     assert rel.max() <= FP32_TOL
     hs = mx3.hidden_states(torch.from_numpy(wavlm_clips[:2]).cuda())
     pooled = torch.stack([h.mean(dim=1) for h in hs], dim=1).cpu().numpy()
@@ -261,10 +261,10 @@ def test_bf16x3_embed_matches_reference(mx3, wavlm_clips, golden_wavlm):
     assert np.linalg.norm(h1 - golden_wavlm["hs1_clip0"]) / np.linalg.norm(golden_wavlm["hs1_clip0"]) <= FP32_TOL
 
 
-def test_bf16x3_normalize_and_batch_invariance(wavlm_sd, golden_wavlm):
+def test_fp16x3_normalize_and_batch_invariance(wavlm_sd, golden_wavlm):
     from ssr_amd import config as C, synth
     from ssr_amd.model import SSEModel
-    m = SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype="bf16x3", do_normalize=True)
+    m = SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype="fp16x3", do_normalize=True)
     idx = [int(i) for i in golden_wavlm["layer_indices"]]
     clips = synth.synth_clips(16, 48000, seed=1234)
     got = m.embed(torch.from_numpy(clips[:4]).cuda(), idx).cpu().numpy()
