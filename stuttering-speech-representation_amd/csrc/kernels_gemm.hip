@@ -286,7 +286,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
           o = f32x4{lo.x, lo.y, hi.x, hi.y};
         }
         if (gelu_fast) {
-          const f32x2 lo = gelu_sig2(f32x2{o[0], o[1]}), hi = gelu_sig2(f32x2{o[2], o[3]});
+          const f32x2 lo = gelu_fast2(f32x2{o[0], o[1]}), hi = gelu_fast2(f32x2{o[2], o[3]});
           o = f32x4{lo.x, lo.y, hi.x, hi.y};
         }
         o += rv[u];

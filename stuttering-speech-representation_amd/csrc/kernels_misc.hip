@@ -217,7 +217,7 @@ __global__ __launch_bounds__(256) void conv0_apply_kernel(const float* __restric
           for (int p = 0; p < 4; ++p) {
             const f32x2 z = {fmaf((y[f][p].x - mean[f]) * rstd[f], gw[p].x, gb[p].x),
                              fmaf((y[f][p].y - mean[f]) * rstd[f], gw[p].y, gb[p].y)};
-            o[p] = FAST ? gelu_sig2(z) : gelu_erf2(z);
+            o[p] = FAST ? gelu_fast2(z) : gelu_erf2(z);
           }
           const long long row = (long long)(t + 4 * f) * C;
           if constexpr (sizeof(TO) == 2) {
@@ -244,7 +244,7 @@ __global__ __launch_bounds__(256) void conv0_apply_kernel(const float* __restric
         #pragma unroll
         for (int p = 0; p < 4; ++p) {
           const f32x2 z = __builtin_elementwise_fma(y[p], sc[p], sh[p]);
-          y[p] = FAST ? gelu_sig2(z) : gelu_erf2(z);
+          y[p] = FAST ? gelu_fast2(z) : gelu_erf2(z);
         }
       }
       if constexpr (sizeof(TO) == 2) {
@@ -364,8 +364,8 @@ __global__ __launch_bounds__(256) void conv0_mfma_kernel(const float* __restrict
       #pragma unroll
       for (int fb = 0; fb < C0M_T / 16; ++fb) {
         const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[i], xf[fb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        const f32x2 o0 = gelu_sig2(__builtin_elementwise_fma(f32x2{acc[0], acc[1]}, sc0[i], sh0[i]));
-        const f32x2 o1 = gelu_sig2(__builtin_elementwise_fma(f32x2{acc[2], acc[3]}, sc1[i], sh1[i]));
+        const f32x2 o0 = gelu_fast2(__builtin_elementwise_fma(f32x2{acc[0], acc[1]}, sc0[i], sh0[i]));
+        const f32x2 o1 = gelu_fast2(__builtin_elementwise_fma(f32x2{acc[2], acc[3]}, sc1[i], sh1[i]));
         *(bf16x4*)&tile[fb * 16 + r16][c] = bf16x4{(bf16)o0.x, (bf16)o0.y, (bf16)o1.x, (bf16)o1.y};
       }
     }
@@ -405,7 +405,7 @@ int launch_conv0_gn(const float* x, int B, int L, const float* norm, const float
     G = G < 1 ? 1 : (G > nchunk ? nchunk : G);
     hipLaunchKernelGGL(conv0_mfma_kernel, dim3(G, B), dim3(256), 0, s, x, L, norm, (const bf16x8*)wf, b0, T0,
                        (const float2*)ss, (bf16*)out);
-  } else if (sizeof(TO) == 2 && !gelu_exact_env())   // bf16 output: gelu_sig2 (common.h)
+  } else if (sizeof(TO) == 2 && !gelu_exact_env())   // bf16 output: gelu_fast2 (common.h)
     hipLaunchKernelGGL((conv0_apply_kernel<TO, false, true>), grid, block, 0, s, x, L, norm, w0, b0, C, T0, ss, out);
   else
     hipLaunchKernelGGL((conv0_apply_kernel<TO, false, false>), grid, block, 0, s, x, L, norm, w0, b0, C, T0, ss, out);
@@ -430,7 +430,7 @@ int launch_conv0_ln(const float* x, int B, int L, const float* norm, const float
                     int s0, int T0, const float* lnw, const float* lnb, float eps, TO* out, hipStream_t s) {
   if (k0 != K0 || s0 != 5 || C != 512) return -3;
   dim3 grid((T0 + C0_T - 1) / C0_T, B), block(256);
-  if (sizeof(TO) == 2 && !gelu_exact_env())   // bf16 output: gelu_sig2 (common.h)
+  if (sizeof(TO) == 2 && !gelu_exact_env())   // bf16 output: gelu_fast2 (common.h)
     hipLaunchKernelGGL((conv0_apply_kernel<TO, true, true, true>), grid, block, 0, s, x, L, norm, w0, b0, C, T0,
                        (const float2*)nullptr, out, lnw, lnb, eps);
   else
@@ -560,7 +560,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TI* __restrict__ i
 // bf16 -> bf16 LayerNorm of narrow rows (H <= 512: the WavLM conv frontend's per-layer LN + GELU
 // and the feature projection's LN): one 16-B load per lane per row, R rows per wave with every load
 // issued first (the one-row-per-wave kernel keeps only 1 KiB in flight per wave: ~2.4 TB/s on these
-// rows), DPP/permlane reductions for the R rows interleaved.  GELU: the bf16 path's gelu_sig2.
+// rows), DPP/permlane reductions for the R rows interleaved.  GELU: the bf16 path's gelu_fast2.
 template <int R>
 __global__ __launch_bounds__(256) void layernorm_bf16_rows_kernel(const bf16* __restrict__ in, const float* __restrict__ w,
                                                                   const float* __restrict__ bta, int rows, int H,
@@ -619,7 +619,7 @@ __global__ __launch_bounds__(256) void layernorm_bf16_rows_kernel(const bf16* __
     if (act != ACT_NONE) {
       #pragma unroll
       for (int e = 0; e < 8; e += 2) {
-        const f32x2 g2 = act == ACT_GELU ? gelu_erf2(f32x2{y[e], y[e + 1]}) : gelu_sig2(f32x2{y[e], y[e + 1]});
+        const f32x2 g2 = act == ACT_GELU ? gelu_erf2(f32x2{y[e], y[e + 1]}) : gelu_fast2(f32x2{y[e], y[e + 1]});
         y[e] = g2.x;
         y[e + 1] = g2.y;
       }

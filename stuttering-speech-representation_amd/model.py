@@ -299,7 +299,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, bias=None, resid=None, act: str | Non
          out_dtype=torch.float32) -> torch.Tensor:
     """The path's MFMA GEMM on its own: a [M, K] @ b[N, K]^T (+bias) (gelu) (+resid).
     a, b both bf16 (bf16 MFMA) or both fp32 (exact-f32 MFMA).  act: None | "gelu" (erf form) |
-    "gelu_fast" (the bf16 path's gelu_sig2 epilogue, common.h)."""
+    "gelu_fast" (the bf16 path's gelu_fast2 epilogue, common.h)."""
     if a.dtype != b.dtype or a.dtype not in (torch.bfloat16, torch.float32):
         raise TypeError("a and b must both be bf16 or both fp32")
     M, K = a.shape

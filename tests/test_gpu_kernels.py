@@ -74,9 +74,10 @@ def test_gemm_tile_configs_agree(M, N, K):
 
 @pytest.mark.parametrize("M,N,K", [(149, 768, 768), (4099, 3072, 768), (1000, 512, 1536)])
 def test_gemm_fast_gelu_epilogue(M, N, K):
-    """The bf16 path's GELU (gelu_sig2: sigmoid form with a degree-6 minimax exponent) in the
-    GEMM epilogue against torch's exact erf-GELU: fp32 output within 1e-5 rel-L2 (the erf form's
-    own bar), bf16 output within the bf16 rounding bar."""
+    """The bf16 path's GELU (gelu_fast2: clamped odd minimax polynomial for Phi, no transcendental)
+    in the GEMM epilogue against torch's exact erf-GELU: fp32 output within 5e-5 rel-L2 on N(0, 4)
+    pre-activations (the fp32 restatement tools/fit_gelu.py gives 1.7e-5), bf16 output within the
+    bf16 rounding bar."""
     from ssr_amd.model import gemm
     g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
     a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
@@ -84,14 +85,15 @@ def test_gemm_fast_gelu_epilogue(M, N, K):
     bias = torch.randn(N, device="cuda", generator=g)
     ref = _ref(a, b, bias, None, "gelu")
     got = gemm(a, b, bias, None, "gelu_fast")
-    assert ((got - ref).norm() / ref.norm()).item() <= 1e-5
+    assert ((got - ref).norm() / ref.norm()).item() <= 5e-5
     gt = gemm(a, b, bias, None, "gelu_fast", out_dtype=torch.bfloat16)
     assert ((gt.float() - ref).norm() / ref.norm()).item() <= 5e-3
 
 
 def test_fast_gelu_pointwise():
-    """gelu_sig2 over a dense grid through the GEMM (a = x, b = 1, K = 64 with one non-zero
-    column): max abs error <= 1e-6 and relative <= 1e-4 where |gelu| > 1e-3, against fp64 erf."""
+    """gelu_fast2 over a dense grid through the GEMM (a = x, b = 1, K = 64 with one non-zero
+    column) against fp64 erf: max abs error <= 1e-4 (fit: 7.3e-5, tools/fit_gelu.py), relative
+    <= 1e-4 for x >= 0.5, relu beyond the clamp (Phi(4.5) = 1 exactly, Phi(-4.5) = 3e-8)."""
     from ssr_amd.model import gemm
     x = torch.linspace(-12, 12, 256 * 1024, dtype=torch.float64)
     a = torch.zeros(x.numel(), 64, dtype=torch.float32)
@@ -103,9 +105,12 @@ def test_fast_gelu_pointwise():
     xe = a[:, 0].double()
     ref = xe * 0.5 * (1.0 + torch.erf(xe / 2 ** 0.5))
     err = (got - ref).abs()
-    assert err.max().item() <= 1e-6, err.max().item()
-    m = ref.abs() > 1e-3
+    assert err.max().item() <= 1e-4, err.max().item()
+    m = xe >= 0.5
     assert (err[m] / ref[m].abs()).max().item() <= 1e-4
+    assert torch.equal(got[xe > 4.5], xe[xe > 4.5].float().double())   # Phi(4.5) = 1 exactly
+    neg = xe < -4.5
+    assert (got[neg].abs() <= 1e-7 * xe[neg].abs()).all()              # Phi(-4.5) = 3e-8
 
 
 @pytest.mark.parametrize("M,N,K", [(16421, 1024, 64), (16421, 1024, 128), (16421, 768, 192), (16384, 1024, 256),

@@ -7,7 +7,8 @@ importlib.import_module("stuttering-speech-representation_amd")
 from ssr_amd import _lib
 from ssr_amd.model import gemm
 
-SHAPES = {"qkv": (38144, 2432, 768, None), "oproj": (38144, 768, 768, "res"), "ffn1": (38144, 3072, 768, "gelu"),
+SHAPES = {"qkv": (38144, 2432, 768, None), "oproj": (38144, 768, 768, "res"), "ffn1": (38144, 3072, 768, "gelu"), "ffn1_noact": (38144, 3072, 768, None),
+          "conv1": (1228544, 512, 1536, "gelu"), "conv1_noact": (1228544, 512, 1536, None),
           "ffn2": (38144, 768, 3072, "res"), "proj": (38144, 768, 512, None), "sq4096": (4096, 4096, 4096, None)}
 cfgs = sys.argv[1:] or ["0"]
 res = {}
