@@ -71,6 +71,8 @@ def parse():
                     help="the Whisper log-mel front end alone (sse_logmel, K9): B x 30 s clips -> [B, 80, 3000], "
                          "reported against the HBM roofline (1.92 MB in + 0.96 MB out per clip)")
     ap.add_argument("--lib", default=None, help="load this build of libsse.so instead of the in-tree one (A/B)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="sse_set_option A/B kernel switch (repeatable)")
     ap.add_argument("--corpus", type=int, default=0,
                     help="BASELINE configs[3] mode: embed a corpus of this many clips (e.g. 50000) sharded "
                          "across the ranks with corpus.extract_corpus (tail batch + one all-gather timed)")
@@ -287,6 +289,10 @@ def main():
     if a.lib:
         from ssr_amd import _lib
         _lib.use_library(a.lib)
+    for kv in a.opt:
+        from ssr_amd import _lib
+        name, val = kv.split("=")
+        _lib.check(_lib.lib().sse_set_option(name.encode(), int(val)), "sse_set_option " + name)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -1385,26 +1385,36 @@ __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
   }
 }
 
-// Short-sequence bf16 attention (T <= 160, WavLM 3 s clips: T = 149): one block per (head,
-// clip), one wave per 16-query block, the whole padded key row (NKB x 16 keys) in LDS.
-// Staging issues every global load of the block first (K: 2 chunks/thread, V: 4 rows for half
-// the threads, the gate's 8 projections, one relative-bias entry) and only then writes LDS, so
-// a block pays one HBM round trip before its MFMA work instead of one per loop trip.
-template <bool BIAS, int NKB>
-__global__ __launch_bounds__(640) void attention_full_kernel(AttnArgs a, int hpb) {
+// Short-sequence bf16 attention (T <= 160, WavLM 3 s clips: T = 149): block = (clip, hpb heads),
+// one wave per 16-query block, the whole padded key row (NKB x 16 keys) of one head in LDS.
+// K and V go HBM -> LDS by LDS-DMA (buffer_load ... lds, 16 B per lane, XOR-swizzled 16-B chunks
+// like the GEMM's operand tiles), from a buffer resource that covers only the clip's T valid rows,
+// so padded keys read as zeros (a padded V row must be finite: its probability is exactly 0).
+// No register staging and a lean register budget (<= 96 VGPRs): two or three blocks share a CU,
+// so one block's loads overlap another's MFMA / softmax work.
+SSE_DEV bf16x8 v_frag_sw(const char* Vs, int k0, int d0, int g, int r16) {
+  // V^T fragment from swizzled row-major V (row = key, 128 B): lane reads 8 B of row k, columns
+  // d0 + 4 (r16 & 3) .. +3; the transpose read gathers the 16-bit elements across lanes
+  auto addr = [&](int row) {
+    const int byte = d0 * 2 + 8 * (r16 & 3);
+    return Vs + row * 128 + (((byte >> 4) ^ ((row >> 1) & 7)) << 4) + (byte & 15);
+  };
+  const int row = k0 + 4 * g + (r16 >> 2);
+  const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)addr(row));
+  const bf16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)addr(row + 16));
+  return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+template <bool BIAS, int NKB, bool RAG>
+__global__ __launch_bounds__(64 * NKB, 2) void attention_full_kernel(AttnArgs a, int hpb) {
   constexpr int TP = NKB * 16;                                   // padded keys
-  constexpr int NT = 64 * NKB;                                   // threads (one wave per query block)
   constexpr int KS_BYTES = TP * 128;
-  constexpr int VS_BYTES = TP * VR_STRIDE;                        // V row-major, read transposed
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ks = smem;
   char* Vs = smem + KS_BYTES;
-  float* gate = (float*)(Vs + VS_BYTES);                          // [TP]
+  float* gate = (float*)(Vs + KS_BYTES);                          // [TP]
   float* rb = gate + TP;                                          // [2*TP]
 
-  // block = (clip, hpb consecutive heads): the next head's K/V/Q/gate/bias loads are issued into
-  // registers before this head's MFMAs and written to LDS after them (one LDS image, two
-  // barriers per head), so a block pays one exposed HBM round trip, not one per head
   const int h0 = blockIdx.x * hpb, b = blockIdx.y;
   const int TS = a.T, T = a.tlen ? a.tlen[b] : a.T, H = a.H, H3 = a.ldq;   // frames of this clip / row stride
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1415,51 +1425,52 @@ __global__ __launch_bounds__(640) void attention_full_kernel(AttnArgs a, int hpb
   const int qi = qb * 16 + r16;
   const bool qv = qi < T;
   const float LOG2E = 1.4426950408889634f;
+  // rows >= T of this clip are out of range: the DMA writes zeros
+  const __amdgpu_buffer_rsrc_t clip =
+      __builtin_amdgcn_make_buffer_rsrc((void*)qkv, (short)0, T * H3 * 2, 0x00020000);
+  // wave-instruction u (= wave, wave + NKB) stages rows [8u, 8u + 8): lane -> row 8u + lane/8, LDS
+  // chunk lane%8 holding source chunk (lane%8) ^ ((row >> 1) & 7)
+  unsigned voff[2];
+  #pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int row = 8 * (wave + NKB * u) + (lane >> 3);
+    voff[u] = (unsigned)(row * H3 * 2 + (((lane & 7) ^ ((row >> 1) & 7)) << 4));
+  }
 
-  bf16x8 kreg[2], vreg[2], greg = bf16x8{}, qreg[2];
-  float rbv = 0.f, gc = 0.f;
-  auto prefetch = [&](int h) {
-    const bf16* qrow = qkv + (long long)(qv ? qi : 0) * H3 + h * AT_HD;
-    #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) qreg[ks] = qv ? *(const bf16x8*)(qrow + ks * 32 + g * 8) : bf16x8{};
+  for (int hh = 0; hh < hpb; ++hh) {
+    const int h = h0 + hh;
+    if (hh) __syncthreads();   // every wave is done reading the previous head's LDS image
     #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int i = tid + u * NT, kr = i >> 3, ch = i & 7;
-      const bf16* row = qkv + (long long)kr * H3 + h * AT_HD + ch * 8;
-      kreg[u] = kr < T ? *(const bf16x8*)(row + H) : bf16x8{};
-      vreg[u] = kr < T ? *(const bf16x8*)(row + 2 * H) : bf16x8{};
+      const int off = (wave + NKB * u) * 1024;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(clip, LPTR(Ks + off), 16, voff[u] + (unsigned)((H + h * AT_HD) * 2), 0, 0,
+                                               0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(clip, LPTR(Vs + off), 16,
+                                               voff[u] + (unsigned)((2 * H + h * AT_HD) * 2), 0, 0, 0);
+    }
+    bf16x8 qf[2];
+    {
+      const bf16* qrow = qkv + (long long)(qv ? qi : 0) * H3 + h * AT_HD;
+      #pragma unroll
+      for (int ks = 0; ks < 2; ++ks) qf[ks] = qv ? *(const bf16x8*)(qrow + ks * 32 + g * 8) : bf16x8{};
     }
     if (BIAS) {
+      bf16x8 greg = bf16x8{};
+      float rbv = 0.f;
       if (tid < T) greg = *(const bf16x8*)(qkv + (long long)tid * H3 + 3 * H + 8 * h);
-      gc = a.gconst[h];
       if (tid < 2 * TP - 1) {
         int d = tid - (TP - 1);
         d = d < -a.maxd ? -a.maxd : (d > a.maxd ? a.maxd : d);
         rbv = a.relb[(long long)h * (2 * a.maxd + 1) + a.maxd + d];
       }
-    }
-  };
-  prefetch(h0);
-  for (int hh = 0; hh < hpb; ++hh) {
-    const int h = h0 + hh;
-    if (hh) __syncthreads();   // every wave is done reading the previous head's LDS image
-    // write LDS: K swizzled rows, V plain rows (read transposed), gate, bias
-    #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int i = tid + u * NT, kr = i >> 3, ch = i & 7;
-      *(bf16x8*)(Ks + kr * 128 + ((ch ^ ((kr >> 1) & 7)) * 16)) = kreg[u];
-      *(bf16x8*)(Vs + kr * VR_STRIDE + ch * 16) = vreg[u];
-    }
-    if (BIAS) {
+      const float gc = a.gconst[h];
       if (tid < TP) gate[tid] = tid < T ? wavlm_gate_v(greg, gc) : 0.f;
       if (tid < 2 * TP - 1) rb[tid] = rbv;
     }
-    const bf16x8 qf[2] = {qreg[0], qreg[1]};
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (hh + 1 < hpb) prefetch(h + 1);   // in flight during this head's MFMAs
-    if (qb * 16 < T) {
-  f32x4 s[NKB];
-  {
+    if (qb * 16 >= T) continue;
+    f32x4 s[NKB];
     #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1471,99 +1482,119 @@ __global__ __launch_bounds__(640) void attention_full_kernel(AttnArgs a, int hpb
       }
       s[kb] = acc;
     }
-  }
-  // exact softmax over the whole (padded) row (lane holds keys kb*16 + 4g + r), log2 domain:
-  // v = s * scale * log2(e) (+ gate * log2(e) * bias) in packed fp32, p = 2^(v - max) with the raw
-  // v_exp_f32, cross-lane max / sum over the 4 key groups by v_permlane16/32_swap
-  const float gq2 = BIAS ? gate[qb * 16 + r16] * LOG2E : 0.f;
-  const float sl2 = a.scale * LOG2E;
-  f32x2 v2[NKB * 2];
-  #pragma unroll
-  for (int kb = 0; kb < NKB; ++kb)
+    // exact softmax over the whole (padded) row (lane holds keys kb*16 + 4g + r), log2 domain:
+    // v = s * scale * log2(e) (+ gate * log2(e) * bias) in packed fp32, p = 2^(v - max) with the raw
+    // v_exp_f32, cross-lane max / sum over the 4 key groups by v_permlane16/32_swap.  Keys >= T can
+    // only fall in the last two key blocks (dispatch: T > (NKB - 2) * 16) unless the batch is ragged.
+    const float gq2 = BIAS ? gate[qb * 16 + r16] * LOG2E : 0.f;
+    const float sl2 = a.scale * LOG2E;
+    f32x2 v2[NKB * 2];
     #pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      const int key = kb * 16 + 4 * g + 2 * hh;
-      f32x2 v = f32x2{s[kb][2 * hh], s[kb][2 * hh + 1]} * sl2;
-      if (BIAS) {
-        const int d = key - qi + (TP - 1);
-        v = __builtin_elementwise_fma(f32x2{gq2, gq2}, f32x2{rb[d], rb[d + 1]}, v);
+    for (int kb = 0; kb < NKB; ++kb)
+      #pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const int key = kb * 16 + 4 * g + 2 * hf;
+        f32x2 v = f32x2{s[kb][2 * hf], s[kb][2 * hf + 1]} * sl2;
+        if (BIAS) {
+          const int d = key - qi + (TP - 1);
+          v = __builtin_elementwise_fma(f32x2{gq2, gq2}, f32x2{rb[d], rb[d + 1]}, v);
+        }
+        if (RAG || kb >= NKB - 2) v = f32x2{key < T ? v.x : -INFINITY, key + 1 < T ? v.y : -INFINITY};
+        v2[kb * 2 + hf] = v;
       }
-      if (kb * 16 + 16 > T) v = f32x2{key < T ? v.x : -INFINITY, key + 1 < T ? v.y : -INFINITY};   // ragged block
-      v2[kb * 2 + hh] = v;
-    }
-  float mx = fmaxf(v2[0].x, v2[0].y);
-  #pragma unroll
-  for (int e = 1; e < NKB * 2; ++e) mx = fmaxf(fmaxf(mx, v2[e].x), v2[e].y);
-  {
-    const auto t16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-    mx = fmaxf(__uint_as_float(t16[0]), __uint_as_float(t16[1]));
-    const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-    mx = fmaxf(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
-  }
-  f32x2 l2 = {0.f, 0.f};
-  const f32x2 mm = {-mx, -mx};
-  #pragma unroll
-  for (int e = 0; e < NKB * 2; ++e) {
-    const f32x2 d = v2[e] + mm;
-    const f32x2 p = {__builtin_amdgcn_exp2f(d.x), __builtin_amdgcn_exp2f(d.y)};
-    l2 += p;
-    s[e >> 1][(e & 1) * 2] = p.x;
-    s[e >> 1][(e & 1) * 2 + 1] = p.y;
-  }
-  float l = l2.x + l2.y;
-  {
-    const auto t16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(l), __float_as_uint(l), false, false);
-    l = __uint_as_float(t16[0]) + __uint_as_float(t16[1]);
-    const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(l), __float_as_uint(l), false, false);
-    l = __uint_as_float(t32[0]) + __uint_as_float(t32[1]);
-  }
-  // O^T = V^T . P^T
-  f32x4 o[4];
-  #pragma unroll
-  for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  #pragma unroll
-  for (int ks = 0; ks < NKB / 2; ++ks) {
-    bf16x8 pf;
+    float mx = fmaxf(v2[0].x, v2[0].y);
     #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      pf[r] = (bf16)s[2 * ks][r];
-      pf[4 + r] = (bf16)s[2 * ks + 1][r];
+    for (int e = 1; e < NKB * 2; ++e) mx = fmaxf(fmaxf(mx, v2[e].x), v2[e].y);
+    {
+      const auto t16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = fmaxf(__uint_as_float(t16[0]), __uint_as_float(t16[1]));
+      const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = fmaxf(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
     }
+    f32x2 l2 = {0.f, 0.f};
+    const f32x2 mm = {-mx, -mx};
     #pragma unroll
-    for (int db = 0; db < 4; ++db) o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v_frag_tr(Vs, ks * 32, db * 16, g, r16), pf, o[db], 0, 0, 0);
-  }
-  if (qv) {
-    const float inv = 1.0f / l;
-    bf16* orow = (bf16*)a.out + ((long long)b * TS + qi) * H + h * AT_HD;
-    #pragma unroll
-    for (int db = 0; db < 4; ++db) {
-      bf16x4 ov = {(bf16)(o[db][0] * inv), (bf16)(o[db][1] * inv), (bf16)(o[db][2] * inv),
-                   (bf16)(o[db][3] * inv)};
-      *(bf16x4*)(orow + db * 16 + 4 * g) = ov;
+    for (int e = 0; e < NKB * 2; ++e) {
+      const f32x2 d = v2[e] + mm;
+      const f32x2 p = {__builtin_amdgcn_exp2f(d.x), __builtin_amdgcn_exp2f(d.y)};
+      l2 += p;
+      s[e >> 1][(e & 1) * 2] = p.x;
+      s[e >> 1][(e & 1) * 2 + 1] = p.y;
     }
-  }
+    float l = l2.x + l2.y;
+    {
+      const auto t16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(l), __float_as_uint(l), false, false);
+      l = __uint_as_float(t16[0]) + __uint_as_float(t16[1]);
+      const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(l), __float_as_uint(l), false, false);
+      l = __uint_as_float(t32[0]) + __uint_as_float(t32[1]);
+    }
+    // O^T = V^T . P^T
+    f32x4 o[4];
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    #pragma unroll
+    for (int ks = 0; ks < NKB / 2; ++ks) {
+      bf16x8 pf;
+      #pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pf[r] = (bf16)s[2 * ks][r];
+        pf[4 + r] = (bf16)s[2 * ks + 1][r];
+      }
+      #pragma unroll
+      for (int db = 0; db < 4; ++db)
+        o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v_frag_sw(Vs, ks * 32, db * 16, g, r16), pf, o[db], 0, 0, 0);
+    }
+    if (qv) {
+      const float inv = 1.0f / l;
+      bf16* orow = (bf16*)a.out + ((long long)b * TS + qi) * H + h * AT_HD;
+      #pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        bf16x4 ov = {(bf16)(o[db][0] * inv), (bf16)(o[db][1] * inv), (bf16)(o[db][2] * inv),
+                     (bf16)(o[db][3] * inv)};
+        *(bf16x4*)(orow + db * 16 + 4 * g) = ov;
+      }
     }
   }
 }
 
-template <bool BIAS, int NKB>
+template <bool BIAS, int NKB, bool RAG>
 int launch_attention_full(const AttnArgs& a, int B, hipStream_t s) {
   constexpr int TP = NKB * 16;
-  const size_t lds = (size_t)TP * 128 + (size_t)TP * VR_STRIDE + (size_t)TP * 4 + (size_t)2 * TP * 4;
-  const int hpb = a.nh % 4 == 0 ? 4 : (a.nh % 3 == 0 ? 3 : (a.nh % 2 == 0 ? 2 : 1));   // heads per block
-  hipLaunchKernelGGL((attention_full_kernel<BIAS, NKB>), dim3(a.nh / hpb, B), dim3(64 * NKB), lds, s, a, hpb);
+  const size_t lds = (size_t)2 * TP * 128 + (size_t)TP * 4 + (size_t)2 * TP * 4;
+  // heads per block: resident blocks per device x rounds should cover nh / hpb * B evenly
+  static int per_cu[64] = {0}, cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -2;
+  if (!cus[dev]) {
+    if (hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu[dev], attention_full_kernel<BIAS, NKB, RAG>, 64 * NKB, lds) !=
+            hipSuccess)
+      return -2;
+    if (per_cu[dev] < 1) per_cu[dev] = 1;
+  }
+  const long long slots = (long long)cus[dev] * per_cu[dev];
+  int hpb = 1;
+  double best = 1e30;
+  for (int c = 1; c <= a.nh; ++c) {   // fewest block rounds, then fewest blocks
+    if (a.nh % c) continue;
+    const long long nb = (long long)(a.nh / c) * B;
+    const long long rounds = (nb + slots - 1) / slots;
+    const double cost = (double)rounds * c + 1e-3 * c;
+    if (cost < best) best = cost, hpb = c;
+  }
+  hipLaunchKernelGGL((attention_full_kernel<BIAS, NKB, RAG>), dim3(a.nh / hpb, B), dim3(64 * NKB), lds, s, a, hpb);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-template <bool BIAS>
+template <bool BIAS, bool RAG>
 int dispatch_full(const AttnArgs& a, int B, hipStream_t s) {
   const int nkb = ((a.T + 31) / 32) * 2;
   switch (nkb) {
-    case 2: return launch_attention_full<BIAS, 2>(a, B, s);
-    case 4: return launch_attention_full<BIAS, 4>(a, B, s);
-    case 6: return launch_attention_full<BIAS, 6>(a, B, s);
-    case 8: return launch_attention_full<BIAS, 8>(a, B, s);
-    case 10: return launch_attention_full<BIAS, 10>(a, B, s);
+    case 2: return launch_attention_full<BIAS, 2, RAG>(a, B, s);
+    case 4: return launch_attention_full<BIAS, 4, RAG>(a, B, s);
+    case 6: return launch_attention_full<BIAS, 6, RAG>(a, B, s);
+    case 8: return launch_attention_full<BIAS, 8, RAG>(a, B, s);
+    case 10: return launch_attention_full<BIAS, 10, RAG>(a, B, s);
     default: return -3;
   }
 }
@@ -1579,8 +1610,10 @@ int launch_attention(const AttnArgs& a, int B, hipStream_t s) {
   if (a.relb) lds += (size_t)(2 * nkt * AT_K) * 4;
   if (lds > 160 * 1024) return -3;
   if constexpr (BF) {   // fp32 (parity) path keeps the flash kernel: its full-row form spills
-    if (a.T <= 160 && a.relb) return dispatch_full<true>(a, B, s);   // <= 10 key blocks: no spills
-    if (a.T <= 160) return dispatch_full<false>(a, B, s);
+    if (a.T <= 160) {   // <= 10 key blocks: the whole row in registers
+      if (a.relb) return a.tlen ? dispatch_full<true, true>(a, B, s) : dispatch_full<true, false>(a, B, s);
+      return a.tlen ? dispatch_full<false, true>(a, B, s) : dispatch_full<false, false>(a, B, s);
+    }
     const int Tk = ((a.T + F2_K - 1) / F2_K) * F2_K;
     const size_t lds2 = 2 * F2_BUF + F2_Q * 4 + (a.relb ? (size_t)2 * Tk * 4 : 0);
     if (lds2 > 160 * 1024) return -3;
