@@ -698,6 +698,11 @@ template int launch_layernorm<bf16, float>(const bf16*, const float*, const floa
 // go to LDS and leave as one dword store per (r16, block) instead of one byte store per
 // (row, block).  Data: e4m3 dwords (4 columns per lane).
 constexpr int LNMX_MAXB = 2048 / 32;
+// One wave per row, 16 rows per wave walked with the NEXT row's loads issued before this row's
+// math (two rows in flight per wave), lane-sliced 16-B loads, DPP / permlane reductions (no LDS
+// round trips): the kernel streams the fp32 residual at HBM rate instead of paying one exposed
+// round trip per row.
+template <int NI>
 __global__ __launch_bounds__(256) void layernorm_mx_kernel(const float* __restrict__ in, const float* __restrict__ w,
                                                            const float* __restrict__ bta, int rows, int H, float eps,
                                                            unsigned char* __restrict__ q, unsigned char* __restrict__ scale) {
@@ -705,40 +710,44 @@ __global__ __launch_bounds__(256) void layernorm_mx_kernel(const float* __restri
   const int r0 = blockIdx.x * 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n4 = H >> 2, nb = H >> 5;
+  const float inv_h = 1.0f / (float)H;
+  f32x4 cur[NI], nxt[NI];
+  auto load = [&](f32x4 (&v)[NI], int row) {
+    const float* x = in + (long long)(row < rows ? row : rows - 1) * H;
+    #pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int g = lane + 64 * i;
+      v[i] = g < n4 ? *(const f32x4*)(x + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  load(cur, r0 + wave);
   for (int rr = wave; rr < 64; rr += 4) {
     const int row = r0 + rr;
     if (row >= rows) break;
-    const float* x = in + (long long)row * H;
-    f32x4 v[8];
+    if (rr + 4 < 64) load(nxt, row + 4);
     float s = 0.f;
     #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int g = lane + 64 * i;
-      if (g < n4) {
-        v[i] = *(const f32x4*)(x + 4 * g);
-        s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
-      }
-    }
-    const float mean = wave_sum(s) / H;
+    for (int i = 0; i < NI; ++i) s += (cur[i][0] + cur[i][1]) + (cur[i][2] + cur[i][3]);
+    const float mean = wave_sum_fast(s) * inv_h;
     float qs = 0.f;
     #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < NI; ++i)
       if (lane + 64 * i < n4)
         #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float d = v[i][e] - mean;
+          const float d = cur[i][e] - mean;
           qs = fmaf(d, d, qs);
         }
-    const float rstd = 1.0f / sqrtf(wave_sum(qs) / H + eps);
+    const float rstd = 1.0f / sqrtf(wave_sum_fast(qs) * inv_h + eps);
     #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < NI; ++i) {
       const int g = lane + 64 * i;
       if (g < n4) {
         const int c = 4 * g;
         const f32x4 wv = *(const f32x4*)(w + c), bv = *(const f32x4*)(bta + c);
         f32x4 o;
         #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = fmaf((v[i][e] - mean) * rstd, wv[e], bv[e]);   // = ln_apply4
+        for (int e = 0; e < 4; ++e) o[e] = fmaf((cur[i][e] - mean) * rstd, wv[e], bv[e]);   // = ln_apply4
         const float a = max8_dpp(fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
         const int e8 = mx_scale_exp(a);
         const float inv = mx_inv_scale(e8);
@@ -748,6 +757,8 @@ __global__ __launch_bounds__(256) void layernorm_mx_kernel(const float* __restri
         if ((lane & 7) == 0) sc[rr * LNMX_MAXB + (c >> 5)] = (unsigned char)e8;
       }
     }
+    #pragma unroll
+    for (int i = 0; i < NI; ++i) cur[i] = nxt[i];
   }
   __syncthreads();
   // scale dwords of this 64-row group: (r16, block) -> bytes i = 0..3 of rows r16 + 16i
@@ -764,7 +775,17 @@ __global__ __launch_bounds__(256) void layernorm_mx_kernel(const float* __restri
 int launch_layernorm_mx(const float* in, const float* w, const float* b, int rows, int H, float eps,
                         unsigned char* q, unsigned char* scale, hipStream_t s) {
   if (H % 128 || H > 2048) return -3;
-  hipLaunchKernelGGL(layernorm_mx_kernel, dim3((rows + 63) / 64), dim3(256), 0, s, in, w, b, rows, H, eps, q, scale);
+  const dim3 grid((rows + 63) / 64);
+  switch ((H + 255) / 256) {   // 16-B pieces per lane
+    case 1: hipLaunchKernelGGL(layernorm_mx_kernel<1>, grid, dim3(256), 0, s, in, w, b, rows, H, eps, q, scale); break;
+    case 2: hipLaunchKernelGGL(layernorm_mx_kernel<2>, grid, dim3(256), 0, s, in, w, b, rows, H, eps, q, scale); break;
+    case 3: hipLaunchKernelGGL(layernorm_mx_kernel<3>, grid, dim3(256), 0, s, in, w, b, rows, H, eps, q, scale); break;
+    case 4: hipLaunchKernelGGL(layernorm_mx_kernel<4>, grid, dim3(256), 0, s, in, w, b, rows, H, eps, q, scale); break;
+    case 5: hipLaunchKernelGGL(layernorm_mx_kernel<5>, grid, dim3(256), 0, s, in, w, b, rows, H, eps, q, scale); break;
+    case 6: hipLaunchKernelGGL(layernorm_mx_kernel<6>, grid, dim3(256), 0, s, in, w, b, rows, H, eps, q, scale); break;
+    case 7: hipLaunchKernelGGL(layernorm_mx_kernel<7>, grid, dim3(256), 0, s, in, w, b, rows, H, eps, q, scale); break;
+    default: hipLaunchKernelGGL(layernorm_mx_kernel<8>, grid, dim3(256), 0, s, in, w, b, rows, H, eps, q, scale); break;
+  }
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
