@@ -1415,10 +1415,13 @@ __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
 // so one block's loads overlap another's MFMA / softmax work.
 SSE_DEV bf16x8 v_frag_sw(const char* Vs, int k0, int d0, int g, int r16) {
   // V^T fragment from swizzled row-major V (row = key, 128 B): lane reads 8 B of row k, columns
-  // d0 + 4 (r16 & 3) .. +3; the transpose read gathers the 16-bit elements across lanes
+  // d0 + 4 (r16 & 3) .. +3; the transpose read gathers the 16-bit elements across lanes.  V's 16-B
+  // chunks are XOR-swizzled by 2 ((row >> 1) & 3): the 32 lanes of one LDS pass read 8 rows x 32 B
+  // and every row pair lands on its own 8 banks of each half (the K swizzle, (row >> 1) & 7, maps
+  // chunk pairs {c, c+1} onto each other and conflicts here)
   auto addr = [&](int row) {
     const int byte = d0 * 2 + 8 * (r16 & 3);
-    return Vs + row * 128 + (((byte >> 4) ^ ((row >> 1) & 7)) << 4) + (byte & 15);
+    return Vs + row * 128 + (((byte >> 4) ^ (((row >> 1) & 3) << 1)) << 4) + (byte & 15);
   };
   const int row = k0 + 4 * g + (r16 >> 2);
   const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)addr(row));
@@ -1427,8 +1430,10 @@ SSE_DEV bf16x8 v_frag_sw(const char* Vs, int k0, int d0, int g, int r16) {
 }
 
 template <bool BIAS, int NKB, bool RAG>
-__global__ __launch_bounds__(64 * NKB, 2) void attention_full_kernel(AttnArgs a, int hpb) {
+__global__ __launch_bounds__(32 * NKB, 3) void attention_full_kernel(AttnArgs a, int hpb) {
   constexpr int TP = NKB * 16;                                   // padded keys
+  constexpr int QPW = 2;                                         // query blocks per wave (NKB is even)
+  constexpr int NW = NKB / QPW;                                  // waves per block
   constexpr int KS_BYTES = TP * 128;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ks = smem;
@@ -1442,40 +1447,38 @@ __global__ __launch_bounds__(64 * NKB, 2) void attention_full_kernel(AttnArgs a,
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
   const bf16* qkv = (const bf16*)a.qkv + (long long)b * TS * H3;
-  const int qb = wave;
-  const int qi = qb * 16 + r16;
-  const bool qv = qi < T;
   const float LOG2E = 1.4426950408889634f;
   // rows >= T of this clip are out of range: the DMA writes zeros
   const __amdgpu_buffer_rsrc_t clip =
       __builtin_amdgcn_make_buffer_rsrc((void*)qkv, (short)0, T * H3 * 2, 0x00020000);
-  // wave-instruction u (= wave, wave + NKB) stages rows [8u, 8u + 8): lane -> row 8u + lane/8, LDS
-  // chunk lane%8 holding source chunk (lane%8) ^ ((row >> 1) & 7)
-  unsigned voff[2];
-  #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int row = 8 * (wave + NKB * u) + (lane >> 3);
-    voff[u] = (unsigned)(row * H3 * 2 + (((lane & 7) ^ ((row >> 1) & 7)) << 4));
-  }
+  // wave-instruction u (u = wave + NW * i) stages rows [8u, 8u + 8): lane -> row 8u + lane/8, LDS
+  // chunk lane%8 holding source chunk (lane%8) ^ swizzle(row) (K: (row >> 1) & 7, V: v_frag_sw's)
+  constexpr int NU = 2 * NKB / NW;   // wave-instructions per wave for each of K and V
 
   for (int hh = 0; hh < hpb; ++hh) {
     const int h = h0 + hh;
     if (hh) __syncthreads();   // every wave is done reading the previous head's LDS image
     #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int off = (wave + NKB * u) * 1024;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(clip, LPTR(Ks + off), 16, voff[u] + (unsigned)((H + h * AT_HD) * 2), 0, 0,
-                                               0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(clip, LPTR(Vs + off), 16,
-                                               voff[u] + (unsigned)((2 * H + h * AT_HD) * 2), 0, 0, 0);
+    for (int u = 0; u < NU; ++u) {
+      const int row = 8 * (wave + NW * u) + (lane >> 3);
+      const unsigned rbase = (unsigned)(row * H3 * 2);
+      const unsigned kch = (unsigned)(((lane & 7) ^ ((row >> 1) & 7)) << 4);
+      const unsigned vch = (unsigned)(((lane & 7) ^ (((row >> 1) & 3) << 1)) << 4);
+      char* kdst = Ks + (wave + NW * u) * 1024;
+      char* vdst = Vs + (wave + NW * u) * 1024;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(clip, LPTR(kdst), 16, rbase + kch + (unsigned)((H + h * AT_HD) * 2), 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(clip, LPTR(vdst), 16, rbase + vch + (unsigned)((2 * H + h * AT_HD) * 2), 0,
+                                               0, 0);
     }
-    bf16x8 qf[2];
-    {
-      const bf16* qrow = qkv + (long long)(qv ? qi : 0) * H3 + h * AT_HD;
+    bf16x8 qf[QPW][2];
+    #pragma unroll
+    for (int qq = 0; qq < QPW; ++qq) {
+      const int qi = (wave + NW * qq) * 16 + r16;
+      const bf16* qrow = qkv + (long long)(qi < T ? qi : 0) * H3 + h * AT_HD;
       #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) qf[ks] = qv ? *(const bf16x8*)(qrow + ks * 32 + g * 8) : bf16x8{};
+      for (int ks = 0; ks < 2; ++ks) qf[qq][ks] = qi < T ? *(const bf16x8*)(qrow + ks * 32 + g * 8) : bf16x8{};
     }
-    if (BIAS) {
+    if (BIAS) {   // 64 * NW = 2 * TP threads: one gate entry and one bias entry per thread
       bf16x8 greg = bf16x8{};
       float rbv = 0.f;
       if (tid < T) greg = *(const bf16x8*)(qkv + (long long)tid * H3 + 3 * H + 8 * h);
@@ -1490,6 +1493,11 @@ __global__ __launch_bounds__(64 * NKB, 2) void attention_full_kernel(AttnArgs a,
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    #pragma unroll
+    for (int qq = 0; qq < QPW; ++qq) {
+    const int qb = wave + NW * qq;
+    const int qi = qb * 16 + r16;
+    const bool qv = qi < T;
     if (qb * 16 >= T) continue;
     f32x4 s[NKB];
     #pragma unroll
@@ -1499,7 +1507,7 @@ __global__ __launch_bounds__(64 * NKB, 2) void attention_full_kernel(AttnArgs a,
       #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const bf16x8 kf = *(const bf16x8*)(Ks + kr * 128 + (((g + 4 * ks) ^ ((kr >> 1) & 7)) * 16));
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qq][ks], acc, 0, 0, 0);
       }
       s[kb] = acc;
     }
@@ -1509,7 +1517,8 @@ __global__ __launch_bounds__(64 * NKB, 2) void attention_full_kernel(AttnArgs a,
     // only fall in the last two key blocks (dispatch: T > (NKB - 2) * 16) unless the batch is ragged.
     const float gq2 = BIAS ? gate[qb * 16 + r16] * LOG2E : 0.f;
     const float sl2 = a.scale * LOG2E;
-    f32x2 v2[NKB * 2];
+    // scores are rewritten in place (one live copy of the row: the kernel stays at <= 96 VGPRs, two
+    // 640-thread blocks per CU)
     #pragma unroll
     for (int kb = 0; kb < NKB; ++kb)
       #pragma unroll
@@ -1521,11 +1530,12 @@ __global__ __launch_bounds__(64 * NKB, 2) void attention_full_kernel(AttnArgs a,
           v = __builtin_elementwise_fma(f32x2{gq2, gq2}, f32x2{rb[d], rb[d + 1]}, v);
         }
         if (RAG || kb >= NKB - 2) v = f32x2{key < T ? v.x : -INFINITY, key + 1 < T ? v.y : -INFINITY};
-        v2[kb * 2 + hf] = v;
+        s[kb][2 * hf] = v.x;
+        s[kb][2 * hf + 1] = v.y;
       }
-    float mx = fmaxf(v2[0].x, v2[0].y);
+    float mx = fmaxf(s[0][0], s[0][1]);
     #pragma unroll
-    for (int e = 1; e < NKB * 2; ++e) mx = fmaxf(fmaxf(mx, v2[e].x), v2[e].y);
+    for (int kb = 0; kb < NKB; ++kb) mx = fmaxf(fmaxf(mx, fmaxf(s[kb][0], s[kb][1])), fmaxf(s[kb][2], s[kb][3]));
     {
       const auto t16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
       mx = fmaxf(__uint_as_float(t16[0]), __uint_as_float(t16[1]));
@@ -1535,13 +1545,15 @@ __global__ __launch_bounds__(64 * NKB, 2) void attention_full_kernel(AttnArgs a,
     f32x2 l2 = {0.f, 0.f};
     const f32x2 mm = {-mx, -mx};
     #pragma unroll
-    for (int e = 0; e < NKB * 2; ++e) {
-      const f32x2 d = v2[e] + mm;
-      const f32x2 p = {__builtin_amdgcn_exp2f(d.x), __builtin_amdgcn_exp2f(d.y)};
-      l2 += p;
-      s[e >> 1][(e & 1) * 2] = p.x;
-      s[e >> 1][(e & 1) * 2 + 1] = p.y;
-    }
+    for (int kb = 0; kb < NKB; ++kb)
+      #pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const f32x2 d = f32x2{s[kb][2 * hf], s[kb][2 * hf + 1]} + mm;
+        const f32x2 p = {__builtin_amdgcn_exp2f(d.x), __builtin_amdgcn_exp2f(d.y)};
+        l2 += p;
+        s[kb][2 * hf] = p.x;
+        s[kb][2 * hf + 1] = p.y;
+      }
     float l = l2.x + l2.y;
     {
       const auto t16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(l), __float_as_uint(l), false, false);
@@ -1575,6 +1587,7 @@ __global__ __launch_bounds__(64 * NKB, 2) void attention_full_kernel(AttnArgs a,
         *(bf16x4*)(orow + db * 16 + 4 * g) = ov;
       }
     }
+    }
   }
 }
 
@@ -1582,13 +1595,14 @@ template <bool BIAS, int NKB, bool RAG>
 int launch_attention_full(const AttnArgs& a, int B, hipStream_t s) {
   constexpr int TP = NKB * 16;
   const size_t lds = (size_t)2 * TP * 128 + (size_t)TP * 4 + (size_t)2 * TP * 4;
+  constexpr int NT = 32 * NKB;   // NKB / 2 waves, two query blocks each
   // heads per block: resident blocks per device x rounds should cover nh / hpb * B evenly
   static int per_cu[64] = {0}, cus[64] = {0};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -2;
   if (!cus[dev]) {
     if (hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu[dev], attention_full_kernel<BIAS, NKB, RAG>, 64 * NKB, lds) !=
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu[dev], attention_full_kernel<BIAS, NKB, RAG>, NT, lds) !=
             hipSuccess)
       return -2;
     if (per_cu[dev] < 1) per_cu[dev] = 1;
@@ -1603,7 +1617,7 @@ int launch_attention_full(const AttnArgs& a, int B, hipStream_t s) {
     const double cost = (double)rounds * c + 1e-3 * c;
     if (cost < best) best = cost, hpb = c;
   }
-  hipLaunchKernelGGL((attention_full_kernel<BIAS, NKB, RAG>), dim3(a.nh / hpb, B), dim3(64 * NKB), lds, s, a, hpb);
+  hipLaunchKernelGGL((attention_full_kernel<BIAS, NKB, RAG>), dim3(a.nh / hpb, B), dim3(NT), lds, s, a, hpb);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
