@@ -40,7 +40,8 @@ int launch_layernorm_x3(const void* in, bool in3, const float* w, const float* b
 int launch_split3(const float* x, long long rows, int C, f16* y, hipStream_t s);
 
 // MX-fp8 (e4m3 + E8M0 per 32 K-elements) GEMM operands, layouts in common.h
-int launch_layernorm_mx(const float* in, const float* w, const float* b, int rows, int H, float eps,
+template <typename TI>
+int launch_layernorm_mx(const TI* in, const float* w, const float* b, int rows, int H, float eps,
                         unsigned char* q, unsigned char* scale, hipStream_t s);
 int launch_mx_quantize(const float* x, int R, int K, int role, unsigned char* q, unsigned char* scale, hipStream_t s);
 
@@ -74,8 +75,8 @@ int launch_attention(const AttnArgs& a, int B, hipStream_t s);
 template <typename TE>
 int launch_xattn1(const TE* q, const TE* kv, int B, int T, int D, int nh, TE* out, hipStream_t s);
 int launch_bcast_rows(const float* v, int D, int B, float* out, hipStream_t s);
-template <typename TO>
-int launch_cast(const float* x, long long n, TO* y, hipStream_t s);
+template <typename TO, typename TI = float>
+int launch_cast(const TI* x, long long n, TO* y, hipStream_t s);
 
 // kernels_ingest.hip
 int resample_length(int L, int orig_freq, int new_freq);

@@ -243,7 +243,9 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
   constexpr int CH = EPI_ROWS * BN / 4;       // 16-B chunks per epilogue chunk
   constexpr int UNR = 4;
   const int col0 = grp * N;
-  const bool has_bias = g.bias != nullptr, has_res = g.resid != nullptr, gelu = g.act == ACT_GELU, gelu_fast = g.act == ACT_GELU_FAST;
+  // residual: fp32 (resid) or a bf16 residual stream (resid_t, read in place)
+  const bool has_bias = g.bias != nullptr, has_res = g.resid != nullptr || g.resid_t != nullptr;
+  const bool gelu = g.act == ACT_GELU, gelu_fast = g.act == ACT_GELU_FAST;
   #pragma unroll
   for (int half = 0; half < BM / EPI_ROWS; ++half) {
     __syncthreads();                          // operand stages (or the previous chunk) fully consumed
@@ -274,7 +276,12 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
         rv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (has_res) {
           const long long ro = g.resid_rows ? (long long)((ok[u] ? m : 0) % g.resid_rows) * g.ldc + col0 + n : off[u];
-          rv[u] = *(const f32x4*)(g.resid + ro);
+          if (g.resid_t) {
+            const bf16x4 rb = *(const bf16x4*)(g.resid_t + ro);
+            rv[u] = f32x4{(float)rb[0], (float)rb[1], (float)rb[2], (float)rb[3]};
+          } else {
+            rv[u] = *(const f32x4*)(g.resid + ro);
+          }
           if (g.rstats) rv[u] = ln_apply4(rv[u], g.rstats[ok[u] ? m : 0], g.rln_w, g.rln_b, col0 + n);
         }
       }
@@ -336,7 +343,9 @@ int launch_any(const GemmArgs& a, int amode, int groups, hipStream_t s) {
   if (a.apart || a.rpart || a.opart || a.resid_t || a.ct3) {   // folded-LayerNorm epilogues exist in the gemm8 kernels only
     if constexpr (sizeof(T) == 2)
       if (amode == AMODE_SEG && groups == 1 && a.N % 256 == 0 && a.K % 64 == 0) return launch_gemm8_bf16(a, s);
-    return -3;
+    // a plain bf16 residual stream (Whisper shapes with N % 256 != 0): this file's epilogue reads it
+    if (!(a.resid_t && !a.apart && !a.rpart && !a.opart && !a.ct3 && !a.resid && !a.Cf && a.Ct && sizeof(T) == 2))
+      return -3;
   }
   if (a.N % 128 == 0 && a.M >= 2048 && force == 2) return launch_cfg<T, 256, 128, 4, 2, 3>(a, amode, groups, s);
   if constexpr (sizeof(T) == 2) {

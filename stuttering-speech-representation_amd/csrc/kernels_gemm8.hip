@@ -397,7 +397,9 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
   float* Cs = (float*)smem;
   constexpr int CH = 128 * 256 / 4;
   constexpr int UNR = 4;
-  const bool has_bias = g.bias != nullptr, has_res = g.resid != nullptr, gelu = g.act == ACT_GELU, gelu_fast = g.act == ACT_GELU_FAST;
+  // residual: fp32 (resid) or the bf16 residual stream (resid_t)
+  const bool has_bias = g.bias != nullptr, has_res = g.resid != nullptr || g.resid_t != nullptr;
+  const bool gelu = g.act == ACT_GELU, gelu_fast = g.act == ACT_GELU_FAST;
   // compile-time mi / it (g8_sfor): acc[mi] and the MX scale words must stay in registers
   g8_sfor<0, 2>([&](auto mic) {
     constexpr int mi = decltype(mic)::value;
@@ -448,7 +450,12 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
         ast[u] = make_float2(0.f, 1.f);
         if (has_res) {
           const long long ro = g.resid_rows ? (long long)(mc % g.resid_rows) * g.ldc + n : off[u];
-          rv[u] = g8_ld<NT>((const f32x4*)(g.resid + ro));
+          if (g.resid_t) {
+            const bf16x4 rb = *(const bf16x4*)(g.resid_t + ro);
+            rv[u] = f32x4{(float)rb[0], (float)rb[1], (float)rb[2], (float)rb[3]};
+          } else {
+            rv[u] = g8_ld<NT>((const f32x4*)(g.resid + ro));
+          }
           if (g.rstats) st[u] = g.rstats[mc];
           else if (g.rpart) st[u] = ln_part_stats_n<3>(g.rpart, mc, g.ln_eps);
         }
@@ -1440,7 +1447,8 @@ int launch_gemm8_mx(const GemmArgs& a, hipStream_t s) {
   // tuples and would spill inside the counted-vmcnt main loop.  Without a residual the MFMAs
   // compute C^T and the epilogue stores from registers (no LDS round trip; OPT_GEMM_MX_STAGED
   // keeps the LDS-staged epilogue for A/B runs); residual GEMMs take the staged epilogue.
-  if (!a.resid && !sse_opt(OPT_GEMM_MX_STAGED))
+  if (a.resid && a.resid_t) return -3;
+  if (!a.resid && !a.resid_t && !sse_opt(OPT_GEMM_MX_STAGED))
     hipLaunchKernelGGL((gemm8_kernel<0, true, false, true>), grid, dim3(512), 0, s, a);
   else
     hipLaunchKernelGGL((gemm8_kernel<0, false, false, true>), grid, dim3(512), 0, s, a);

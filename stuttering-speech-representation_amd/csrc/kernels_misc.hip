@@ -702,8 +702,8 @@ constexpr int LNMX_MAXB = 2048 / 32;
 // math (two rows in flight per wave), lane-sliced 16-B loads, DPP / permlane reductions (no LDS
 // round trips): the kernel streams the fp32 residual at HBM rate instead of paying one exposed
 // round trip per row.
-template <int NI>
-__global__ __launch_bounds__(256) void layernorm_mx_kernel(const float* __restrict__ in, const float* __restrict__ w,
+template <typename TI, int NI>
+__global__ __launch_bounds__(256) void layernorm_mx_kernel(const TI* __restrict__ in, const float* __restrict__ w,
                                                            const float* __restrict__ bta, int rows, int H, float eps,
                                                            unsigned char* __restrict__ q, unsigned char* __restrict__ scale) {
   __shared__ unsigned char sc[64 * LNMX_MAXB];
@@ -713,11 +713,11 @@ __global__ __launch_bounds__(256) void layernorm_mx_kernel(const float* __restri
   const float inv_h = 1.0f / (float)H;
   f32x4 cur[NI], nxt[NI];
   auto load = [&](f32x4 (&v)[NI], int row) {
-    const float* x = in + (long long)(row < rows ? row : rows - 1) * H;
+    const TI* x = in + (long long)(row < rows ? row : rows - 1) * H;
     #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int g = lane + 64 * i;
-      v[i] = g < n4 ? *(const f32x4*)(x + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
+      v[i] = g < n4 ? load4<TI>(x + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
   load(cur, r0 + wave);
@@ -772,22 +772,31 @@ __global__ __launch_bounds__(256) void layernorm_mx_kernel(const float* __restri
   }
 }
 
-int launch_layernorm_mx(const float* in, const float* w, const float* b, int rows, int H, float eps,
-                        unsigned char* q, unsigned char* scale, hipStream_t s) {
+template <typename TI>
+int launch_layernorm_mx(const TI* in, const float* w, const float* b, int rows, int H, float eps, unsigned char* q,
+                        unsigned char* scale, hipStream_t s) {
   if (H % 128 || H > 2048) return -3;
   const dim3 grid((rows + 63) / 64);
+  auto go = [&](auto nic) {
+    constexpr int NI = decltype(nic)::value;
+    hipLaunchKernelGGL((layernorm_mx_kernel<TI, NI>), grid, dim3(256), 0, s, in, w, b, rows, H, eps, q, scale);
+  };
   switch ((H + 255) / 256) {   // 16-B pieces per lane
-    case 1: hipLaunchKernelGGL(layernorm_mx_kernel<1>, grid, dim3(256), 0, s, in, w, b, rows, H, eps, q, scale); break;
-    case 2: hipLaunchKernelGGL(layernorm_mx_kernel<2>, grid, dim3(256), 0, s, in, w, b, rows, H, eps, q, scale); break;
-    case 3: hipLaunchKernelGGL(layernorm_mx_kernel<3>, grid, dim3(256), 0, s, in, w, b, rows, H, eps, q, scale); break;
-    case 4: hipLaunchKernelGGL(layernorm_mx_kernel<4>, grid, dim3(256), 0, s, in, w, b, rows, H, eps, q, scale); break;
-    case 5: hipLaunchKernelGGL(layernorm_mx_kernel<5>, grid, dim3(256), 0, s, in, w, b, rows, H, eps, q, scale); break;
-    case 6: hipLaunchKernelGGL(layernorm_mx_kernel<6>, grid, dim3(256), 0, s, in, w, b, rows, H, eps, q, scale); break;
-    case 7: hipLaunchKernelGGL(layernorm_mx_kernel<7>, grid, dim3(256), 0, s, in, w, b, rows, H, eps, q, scale); break;
-    default: hipLaunchKernelGGL(layernorm_mx_kernel<8>, grid, dim3(256), 0, s, in, w, b, rows, H, eps, q, scale); break;
+    case 1: go(std::integral_constant<int, 1>{}); break;
+    case 2: go(std::integral_constant<int, 2>{}); break;
+    case 3: go(std::integral_constant<int, 3>{}); break;
+    case 4: go(std::integral_constant<int, 4>{}); break;
+    case 5: go(std::integral_constant<int, 5>{}); break;
+    case 6: go(std::integral_constant<int, 6>{}); break;
+    case 7: go(std::integral_constant<int, 7>{}); break;
+    default: go(std::integral_constant<int, 8>{}); break;
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+template int launch_layernorm_mx<float>(const float*, const float*, const float*, int, int, float, unsigned char*,
+                                        unsigned char*, hipStream_t);
+template int launch_layernorm_mx<bf16>(const bf16*, const float*, const float*, int, int, float, unsigned char*,
+                                       unsigned char*, hipStream_t);
 
 // ---------------------------------------------------------------------------------------
 // MX-fp8 quantisation of a row-major fp32 [R][K] tensor (K % 128 == 0) into e4m3 bytes [R][K]
@@ -1740,15 +1749,16 @@ int launch_bcast_rows(const float* v, int D, int B, float* out, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-template <typename TO>
-__global__ void cast_kernel(const float* __restrict__ x, long long n, TO* __restrict__ y) {
+template <typename TI, typename TO>
+__global__ void cast_kernel(const TI* __restrict__ x, long long n, TO* __restrict__ y) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i < n) y[i] = from_f32<TO>(x[i]);
+  if (i < n) y[i] = from_f32<TO>(to_f32(x[i]));
 }
-template <typename TO>
-int launch_cast(const float* x, long long n, TO* y, hipStream_t s) {
-  hipLaunchKernelGGL((cast_kernel<TO>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, n, y);
+template <typename TO, typename TI>
+int launch_cast(const TI* x, long long n, TO* y, hipStream_t s) {
+  hipLaunchKernelGGL((cast_kernel<TI, TO>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, n, y);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
-template int launch_cast<float>(const float*, long long, float*, hipStream_t);
-template int launch_cast<bf16>(const float*, long long, bf16*, hipStream_t);
+template int launch_cast<float, float>(const float*, long long, float*, hipStream_t);
+template int launch_cast<bf16, float>(const float*, long long, bf16*, hipStream_t);
+template int launch_cast<float, bf16>(const bf16*, long long, float*, hipStream_t);

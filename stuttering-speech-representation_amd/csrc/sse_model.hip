@@ -637,7 +637,7 @@ WhisperWs whisper_plan(const sse_model* m, int B, Plan& p) {
   w.lm = p.add(logmel_workspace_bytes(B, c.n_mels));
   w.mel = p.add((size_t)B * T2 * c.n_mels * es);
   w.h1 = p.add((size_t)B * T2 * D * es);
-  w.x = p.add(M * D * 4);
+  w.x = p.add(M * D * es);   // residual stream: bf16 on the bf16 / MX-fp8 paths, fp32 on the fp32 path
   w.xb = p.add(M * D * es);
   w.qkv = p.add(M * 3 * D * es);
   w.ctx = p.add(M * D * es);
@@ -670,15 +670,20 @@ struct Sink {
   int B, T, H;
   hipStream_t s;
   const int* tlen = nullptr;   // ragged batch: frames of each clip (the time-means run over those)
-  int emit(int idx, const float* x) const {
+  template <typename TI>
+  int emit(int idx, const TI* x) const {   // fp32 or the bf16 residual stream
     for (int i = 0; i < n_ids; ++i)
       if (ids[i] == idx)
-        RC(launch_pool_mean(x, B, T, H, pooled + (size_t)i * H, (long long)n_ids * H, s, nullptr, nullptr, nullptr,
-                            nullptr, 0, 0.f, tlen));
+        RC(launch_pool_mean<TI>(x, B, T, H, pooled + (size_t)i * H, (long long)n_ids * H, s, nullptr, nullptr, nullptr,
+                                nullptr, 0, 0.f, tlen));
     if (hs) {
-      const size_t bytes = (size_t)B * T * H * 4;
-      if (hipMemcpyAsync(hs + (size_t)idx * B * T * H, x, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
-        return SSE_ERR_HIP;
+      if constexpr (sizeof(TI) == 4) {
+        const size_t bytes = (size_t)B * T * H * 4;
+        if (hipMemcpyAsync(hs + (size_t)idx * B * T * H, x, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
+          return SSE_ERR_HIP;
+      } else {
+        RC((launch_cast<float, TI>(x, (long long)B * T * H, hs + (size_t)idx * B * T * H, s)));
+      }
     }
     return 0;
   }
@@ -1150,8 +1155,19 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
             [&] { return launch_logmel<T>(wave, B, L, nm, nullptr, mel, ws + w.lm, logmel_workspace_bytes(B, nm), s,
                                           lens); }));
   T* h1 = (T*)(ws + w.h1);
-  float* x = (float*)(ws + w.x);
+  // residual stream in the path's element type: the bf16 / MX-fp8 paths keep it in bf16 (the residual
+  // GEMMs read and write half the bytes, LayerNorm reads half; adds ~1e-3 rel-L2 against a ~6e-3 bf16
+  // path error), the fp32 path in fp32
+  using R = std::conditional_t<sizeof(T) == 2, bf16, float>;
+  R* x = (R*)(ws + w.x);
   T* xb = (T*)(ws + w.xb);
+  auto set_out = [&](GemmArgs& g) {   // C = x (+ residual x): bf16 stream or fp32
+    if constexpr (sizeof(R) == 2) g.Ct = x; else g.Cf = x;
+  };
+  auto set_resid = [&](GemmArgs& g) {
+    if constexpr (sizeof(R) == 2) g.resid_t = x; else g.resid = x;
+    set_out(g);
+  };
   {
     GemmArgs g{};   // conv1: k3 pad1, 80 -> D, GELU
     g.A = mel; g.B = m->ptr(m->c1_w); g.M = B * T2; g.N = D; g.K = 3 * nm;
@@ -1162,7 +1178,7 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
     g.A = h1; g.B = m->ptr(m->c2_w); g.M = M; g.N = D; g.K = 3 * D;
     g.rows_per_seg = Tq; g.T_in = T2; g.stride = 2; g.pad = 1; g.cin = D; g.ld_in = D;
     g.bias = m->ptr<float>(m->c2_b); g.resid = m->ptr<float>(m->positions); g.resid_rows = Tq;
-    g.Cf = x; g.ldc = D; g.act = ACT_GELU; g.zero = zero;
+    set_out(g); g.ldc = D; g.act = ACT_GELU; g.zero = zero;
     RC(prof(m, s, "gemm_conv:conv2", gflops(g), gbytes<T>(g, AMODE_CONV), [&] { return launch_gemm<T>(g, AMODE_CONV, 1, s); }));
   }
   RC(sink.emit(0, x));
@@ -1177,26 +1193,26 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
   unsigned char* fq = (unsigned char*)(ws + w.ff);
   unsigned char* fq_s = fq + (size_t)M * F;
   auto mx_gemm = [&](const char* tag, const unsigned char* A, const unsigned char* As, size_t wq, size_t wsc, size_t bo,
-                     int N, int K, const float* resid, float* Cf, void* Ct, unsigned char* Cs, int act) {
+                     int N, int K, bool res, void* Ct, unsigned char* Cs, int act) {
     GemmArgs g{};
     g.A = A; g.a_scale = As; g.B = m->ptr(wq); g.b_scale = m->ptr<unsigned char>(wsc);
     g.M = M; g.N = N; g.K = K; g.rows_per_seg = M; g.lda = K;
-    g.bias = m->ptr<float>(bo); g.resid = resid; g.Cf = Cf; g.Ct = Ct; g.c_scale = Cs; g.ldc = N; g.act = act;
+    g.bias = m->ptr<float>(bo); g.Ct = Ct; g.c_scale = Cs; g.ldc = N; g.act = act;
+    if (res) set_resid(g);   // C = x + A B^T + b (the residual stream, in place)
     g.zero = zero;
     const double bytes = (double)M * K + (double)N * K + (M + (double)N) * K / 32.0 +
-                         (double)M * N * (Cf ? 4.0 : 0.0) + (double)M * N * (resid ? 4.0 : 0.0) +
-                         (Ct ? (double)M * N * (Cs ? 1.0 + 1.0 / 32 : 2.0) : 0.0);
+                         (res ? 2.0 * M * N * sizeof(R) : 0.0) +
+                         (!res && Ct ? (double)M * N * (Cs ? 1.0 + 1.0 / 32 : 2.0) : 0.0);
     return prof(m, s, tag, gflops(g), bytes, [&] { return launch_gemm8_mx(g, s); });
   };
   for (int l = 0; l < c.layers; ++l) {
     const LayerW& Lw = m->layers[l];
     if (mx) {
-      RC(launch_layernorm_mx(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, D, eps, xq, xq_s, s));
-      RC(mx_gemm("gemm_mx:qkv", xq, xq_s, Lw.qkv_q, Lw.qkv_s, Lw.qkv_b, 3 * D, D, nullptr, nullptr, qkv, nullptr,
-                 ACT_NONE));
+      RC(launch_layernorm_mx<R>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, D, eps, xq, xq_s, s));
+      RC(mx_gemm("gemm_mx:qkv", xq, xq_s, Lw.qkv_q, Lw.qkv_s, Lw.qkv_b, 3 * D, D, false, qkv, nullptr, ACT_NONE));
     } else {
-      RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, D, eps, ACT_NONE, nullptr,
-                                     xb, s)));
+      RC((launch_layernorm<R, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, D, eps, ACT_NONE, nullptr,
+                                 xb, s)));
       GemmArgs g{};
       g.A = xb; g.B = m->ptr(Lw.qkv_w); g.M = M; g.N = 3 * D; g.K = D; g.rows_per_seg = M; g.lda = D;
       g.bias = m->ptr<float>(Lw.qkv_b); g.Ct = qkv; g.ldc = 3 * D; g.zero = zero;
@@ -1209,32 +1225,31 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
             [&] { return launch_attention<T>(a, B, s); }));
     g = GemmArgs{};
     g.A = ctx; g.B = m->ptr(Lw.o_w); g.M = M; g.N = D; g.K = D; g.rows_per_seg = M; g.lda = D;
-    g.bias = m->ptr<float>(Lw.o_b); g.resid = x; g.Cf = x; g.ldc = D; g.zero = zero;
+    g.bias = m->ptr<float>(Lw.o_b); set_resid(g); g.ldc = D; g.zero = zero;
     RC(prof(m, s, "gemm:oproj", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     if (mx) {
-      RC(launch_layernorm_mx(x, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, D, eps, xq, xq_s, s));
-      RC(mx_gemm("gemm_mx:ffn1", xq, xq_s, Lw.f1_q, Lw.f1_s, Lw.f1_b, F, D, nullptr, nullptr, fq, fq_s,
-                 gelu_rounded_act<T>()));
-      RC(mx_gemm("gemm_mx:ffn2", fq, fq_s, Lw.f2_q, Lw.f2_s, Lw.f2_b, D, F, x, x, nullptr, nullptr, ACT_NONE));
+      RC(launch_layernorm_mx<R>(x, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, D, eps, xq, xq_s, s));
+      RC(mx_gemm("gemm_mx:ffn1", xq, xq_s, Lw.f1_q, Lw.f1_s, Lw.f1_b, F, D, false, fq, fq_s, gelu_rounded_act<T>()));
+      RC(mx_gemm("gemm_mx:ffn2", fq, fq_s, Lw.f2_q, Lw.f2_s, Lw.f2_b, D, F, true, nullptr, nullptr, ACT_NONE));
       if (l + 1 < c.layers) RC(sink.emit(l + 1, x));
       continue;
     }
-    RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, D, eps, ACT_NONE, nullptr,
-                                   xb, s)));
+    RC((launch_layernorm<R, T>(x, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, D, eps, ACT_NONE, nullptr,
+                               xb, s)));
     g = GemmArgs{};
     g.A = xb; g.B = m->ptr(Lw.f1_w); g.M = M; g.N = F; g.K = D; g.rows_per_seg = M; g.lda = D;
     g.bias = m->ptr<float>(Lw.f1_b); g.Ct = ff; g.ldc = F; g.act = gelu_rounded_act<T>(); g.zero = zero;
     RC(prof(m, s, "gemm:ffn1", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     g = GemmArgs{};
     g.A = ff; g.B = m->ptr(Lw.f2_w); g.M = M; g.N = D; g.K = F; g.rows_per_seg = M; g.lda = F;
-    g.bias = m->ptr<float>(Lw.f2_b); g.resid = x; g.Cf = x; g.ldc = D; g.zero = zero;
+    g.bias = m->ptr<float>(Lw.f2_b); set_resid(g); g.ldc = D; g.zero = zero;
     RC(prof(m, s, "gemm:ffn2", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     if (l + 1 < c.layers) RC(sink.emit(l + 1, x));
   }
   // hidden_states[-1] is the post-LN last_hidden_state (HF/utils/output_capturing.py:268-279)
   float* xf = (float*)(ws + w.xf);
-  RC((launch_layernorm<float, T>(x, m->ptr<float>(m->enc_ln_w), m->ptr<float>(m->enc_ln_b), M, D, eps, ACT_NONE, xf,
-                                 dsink ? xb : (T*)nullptr, s)));
+  RC((launch_layernorm<R, T>(x, m->ptr<float>(m->enc_ln_w), m->ptr<float>(m->enc_ln_b), M, D, eps, ACT_NONE, xf,
+                             dsink ? xb : (T*)nullptr, s)));
   RC(sink.emit(c.layers, xf));
   if (dsink) RC(whisper_decoder<T>(m, xb, B, *dsink, ws, w, s));
   return 0;
