@@ -1,7 +1,8 @@
 #pragma once
 #include "common.h"
 
-constexpr int LM_NB = 448;   // DFT basis rows: 201 cos + 201 sin, padded to a multiple of 64
+constexpr int LM_NFFT = 400;   // Whisper STFT: 400-point frames, hop 160, 201 bins
+constexpr int LM_MAXMEL = 128;   // n_mels: 80 (v1/v2) or 128 (v3)
 
 size_t logmel_workspace_bytes(int B, int n_mels);
 // x [B][L] fp32 -> out_hf [B][n_mels][3000] fp32 (optional) and out_cl [B][3000][n_mels] (optional);

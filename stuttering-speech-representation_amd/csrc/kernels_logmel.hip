@@ -1,14 +1,16 @@
 // K9: Whisper log-mel front end (HF/models/whisper/feature_extraction_whisper.py:135-168,
-// 300-307; HF/audio_utils.py:638-740) on gfx950.
+// 300-307; HF/audio_utils.py:638-740) on gfx950, one fused pass per 20-frame block:
 //
-//   1. lm_pad:   zero-pad/truncate to 480000 samples, reflect-pad 200 each side  -> xp [B][480400]
-//   2. DFT:      frames (row t = xp[160 t : 160 t + 400]) x windowed cos/sin basis [448][400]
-//                on the exact-f32 MFMA GEMM (kernels_gemm.hip, SEG mode, rows overlap)  -> S [B*3000][448]
-//   3. lm_mel:   |X|^2 -> Slaney mel (201 x n_mels, fp32 filters) -> log10(max(., 1e-10)), per-clip max
-//   4. lm_final: max(x, max_clip - 8), (x + 4) / 4  -> [B][n_mels][3000] (HF layout) and/or
+//   lm_stft_mel: the block's 3440 samples (zero-pad / truncate to 480000, reflect-pad 200 each side,
+//                computed on the fly from the raw clip) staged in LDS once; per frame (one wave)
+//                Hann window, the 400-point real DFT as a 200-point complex FFT of the even/odd
+//                samples (Stockham radix 8 x 5 x 5 in LDS, fp32, twiddles from fp64) plus the
+//                real-FFT split, |X|^2 (201 bins, LDS) -> Slaney mel over each filter's support ->
+//                log10(max(., 1e-10)) -> logv [B][3000][n_mels], per-clip max (atomic)
+//   lm_final:    max(x, max_clip - 8), (x + 4) / 4  -> [B][n_mels][3000] (HF layout) and/or
 //                channels-last [B][3000][n_mels] in the encoder's element type (conv1 operand)
-// The basis (Hann window folded in) and the filter bank are generated on device from the
-// closed forms in fp64 into the workspace, so the call needs no host state or allocation.
+// HBM traffic per clip: the clip once (1.92 MB) + logv written and read back (0.96 MB each) + the
+// output; the spectrum never leaves LDS.  The filter bank is generated on device in fp64.
 #include "common.h"
 #include "kernels_logmel.h"
 
@@ -16,34 +18,6 @@ namespace {
 
 constexpr int N_FFT = 400, HOP = 160, PAD = 200, NS = 480000, NP = NS + 2 * PAD, NFR = 3000;
 constexpr int NF = N_FFT / 2 + 1;   // 201 bins
-
-__global__ void lm_pad_kernel(const float* __restrict__ x, int L, int Lv, float* __restrict__ xp,
-                              const int* __restrict__ lens) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int b = blockIdx.y;
-  if (i >= NP) return;
-  if (lens) Lv = lens[b] < NS ? lens[b] : NS;   // ragged batch: the clip's own samples, zeros after
-  int j = (int)i - PAD;
-  if (j < 0) j = -j;
-  if (j >= NS) j = 2 * (NS - 1) - j;
-  xp[(long long)b * NP + i] = j < Lv ? x[(long long)b * L + j] : 0.f;
-}
-
-// basis[f][n] = hann(n) cos(2 pi f n / 400), basis[201 + f][n] = hann(n) sin(...), rest 0.
-__global__ void lm_basis_kernel(float* __restrict__ basis) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= LM_NB * N_FFT) return;
-  const int row = i / N_FFT, n = i - row * N_FFT;
-  // torch.hann_window(400) (periodic), float32
-  const float w = 0.5f - 0.5f * cosf(6.283185307179586f * (float)n / (float)N_FFT);
-  double v = 0.0;
-  if (row < NF) {
-    v = cospi(2.0 * ((row * n) % N_FFT) / N_FFT);
-  } else if (row < 2 * NF) {
-    v = sinpi(2.0 * (((row - NF) * n) % N_FFT) / N_FFT);
-  }
-  basis[i] = (float)((double)w * v);
-}
 
 __device__ double hz_to_mel(double f) {
   return f >= 1000.0 ? 15.0 + log(f / 1000.0) * (27.0 / log(6.4)) : 3.0 * f / 200.0;
@@ -76,8 +50,12 @@ __device__ __forceinline__ float unord_f32(unsigned u) {
   return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
 }
 
-// support [first, last] of each mel filter's nonzero bins (triangular filters: contiguous)
-__global__ void lm_support_kernel(const float* __restrict__ fb, int n_mels, int2* __restrict__ sup) {
+constexpr int MAXSUP = 32;   // bins per Slaney filter (80 mels on 201 bins: at most 27)
+
+// support [first, last] of each mel filter's nonzero bins (triangular filters: contiguous) and the
+// filter's weights over it packed [n_mels][MAXSUP] (staged in LDS by the STFT kernel)
+__global__ void lm_support_kernel(const float* __restrict__ fb, int n_mels, int2* __restrict__ sup,
+                                  float* __restrict__ fbp) {
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= n_mels) return;
   int lo = NF, hi = -1;
@@ -86,51 +64,205 @@ __global__ void lm_support_kernel(const float* __restrict__ fb, int n_mels, int2
       lo = f < lo ? f : lo;
       hi = f;
     }
+  if (hi - lo + 1 > MAXSUP) hi = lo + MAXSUP - 1;   // not reached for n_mels >= 64 (host checks n_mels)
   sup[m] = make_int2(lo, hi);
+  for (int i = 0; i < MAXSUP; ++i) fbp[m * MAXSUP + i] = lo + i <= hi ? fb[(lo + i) * n_mels + m] : 0.f;
 }
 
-constexpr int MEL_FR = 20;   // frames per block (3000 = 150 x 20)
+constexpr int MEL_FR = 20;   // frames per block (3000 = 150 x 20), 5 per wave
 static_assert(NFR % MEL_FR == 0, "mel grid must cover every frame");
+constexpr int NZ = N_FFT / 2;                       // 200-point complex FFT
+constexpr int SPAN = HOP * (MEL_FR - 1) + N_FFT;    // 3440 samples per block
 
-// mel = fb^T . |X|^2 over each filter's support only: the in-order fma chain over the support is
-// bit-identical to the dense 201-bin chain (the other terms are fma(0, P, acc) = acc)
-__global__ __launch_bounds__(256) void lm_mel_kernel(const float* __restrict__ S, const float* __restrict__ fb,
-                                                     const int2* __restrict__ sup, int n_mels,
-                                                     float* __restrict__ logv, unsigned* __restrict__ mx) {
-  __shared__ float P[MEL_FR][NF + 3];
-  const int b = blockIdx.y, t0 = blockIdx.x * MEL_FR;
-  for (int i = threadIdx.x; i < MEL_FR * NF; i += 256) {
-    const int fr = i / NF, f = i - fr * NF;
-    const float* row = S + ((long long)b * NFR + t0 + fr) * LM_NB;
-    const float re = row[f], im = row[NF + f];
-    P[fr][f] = re * re + im * im;
+// twiddles W_200^k = exp(-2 pi i k / 200) and the real-split W_400^k, k < 200, from fp64; then the
+// Hann window as (w[2n], w[2n+1]) pairs (torch.hann_window(400), periodic, evaluated in float32)
+__global__ void lm_twiddle_kernel(float2* __restrict__ tw) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < 2 * NZ) {
+    const double a = k < NZ ? -2.0 * (double)k / NZ : -2.0 * (double)(k - NZ) / N_FFT;   // in units of pi
+    tw[k] = make_float2((float)cospi(a), (float)sinpi(a));
+  } else if (k < 3 * NZ) {
+    const int n = k - 2 * NZ;
+    tw[k] = make_float2(0.5f - 0.5f * cosf(6.283185307179586f * (float)(2 * n) / (float)N_FFT),
+                        0.5f - 0.5f * cosf(6.283185307179586f * (float)(2 * n + 1) / (float)N_FFT));
   }
+}
+
+SSE_DEV float2 cmul(float2 a, float2 b) { return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
+
+// one radix-R Stockham stage over NZ points (span Ns so far): lane j < NZ/R does butterfly j
+template <int R>
+SSE_DEV void fft_stage(const float2* __restrict__ x, float2* __restrict__ y, int Ns, const float2* __restrict__ tw,
+                       int lane) {
+  constexpr int NB = NZ / R;
+  if (lane < NB) {
+    const int j = lane, k = j % Ns;
+    float2 v[R];
+    #pragma unroll
+    for (int r = 0; r < R; ++r) {
+      v[r] = x[j + r * NB];
+      if (r) v[r] = cmul(v[r], tw[(k * r * (NZ / (Ns * R))) % NZ]);   // W_{Ns R}^{k r}
+    }
+    float2 o[R];
+    if constexpr (R == 8) {   // 8-point DFT as radix 2 x 2 x 2 (constant twiddles)
+      const float h = 0.70710678118654752f;
+      float2 a[8];
+      #pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        a[r] = make_float2(v[r].x + v[r + 4].x, v[r].y + v[r + 4].y);
+        a[r + 4] = make_float2(v[r].x - v[r + 4].x, v[r].y - v[r + 4].y);
+      }
+      // twiddles W_8^r on the odd half: 1, (1 - i) h, -i, (-1 - i) h
+      a[5] = make_float2((a[5].x + a[5].y) * h, (a[5].y - a[5].x) * h);
+      a[6] = make_float2(a[6].y, -a[6].x);
+      a[7] = make_float2((a[7].y - a[7].x) * h, -(a[7].x + a[7].y) * h);
+      float2 c[8];
+      #pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const int b0 = 4 * g;
+        c[b0 + 0] = make_float2(a[b0].x + a[b0 + 2].x, a[b0].y + a[b0 + 2].y);
+        c[b0 + 2] = make_float2(a[b0].x - a[b0 + 2].x, a[b0].y - a[b0 + 2].y);
+        c[b0 + 1] = make_float2(a[b0 + 1].x + a[b0 + 3].x, a[b0 + 1].y + a[b0 + 3].y);
+        const float2 t = make_float2(a[b0 + 1].x - a[b0 + 3].x, a[b0 + 1].y - a[b0 + 3].y);
+        c[b0 + 3] = make_float2(t.y, -t.x);   // * W_4^1 = -i
+      }
+      // last radix-2 level; bit-reversed order -> natural
+      o[0] = make_float2(c[0].x + c[1].x, c[0].y + c[1].y);
+      o[4] = make_float2(c[0].x - c[1].x, c[0].y - c[1].y);
+      o[2] = make_float2(c[2].x + c[3].x, c[2].y + c[3].y);
+      o[6] = make_float2(c[2].x - c[3].x, c[2].y - c[3].y);
+      o[1] = make_float2(c[4].x + c[5].x, c[4].y + c[5].y);
+      o[5] = make_float2(c[4].x - c[5].x, c[4].y - c[5].y);
+      o[3] = make_float2(c[6].x + c[7].x, c[6].y + c[7].y);
+      o[7] = make_float2(c[6].x - c[7].x, c[6].y - c[7].y);
+    } else {
+      #pragma unroll
+      for (int q = 0; q < R; ++q) {   // R-point DFT, W_R^{q r} = W_200^{q r NZ / R}
+        float2 acc = v[0];
+        #pragma unroll
+        for (int r = 1; r < R; ++r) {
+          const float2 w = tw[((q * r) % R) * (NZ / R)];
+          acc.x = fmaf(v[r].x, w.x, fmaf(-v[r].y, w.y, acc.x));
+          acc.y = fmaf(v[r].x, w.y, fmaf(v[r].y, w.x, acc.y));
+        }
+        o[q] = acc;
+      }
+    }
+    const int d = (j / Ns) * Ns * R + k;
+    #pragma unroll
+    for (int q = 0; q < R; ++q) y[d + q * Ns] = o[q];
+  }
+}
+
+__global__ __launch_bounds__(256) void lm_stft_mel_kernel(const float* __restrict__ wave, int L, int Lv0,
+                                                          const int* __restrict__ lens, const float2* __restrict__ twg,
+                                                          const float* __restrict__ fbp, const int2* __restrict__ sup,
+                                                          int n_mels, float* __restrict__ logv,
+                                                          unsigned* __restrict__ mx) {
+  __shared__ float xs[SPAN];
+  __shared__ float2 tw[3 * NZ];   // W_200^k | W_400^k | Hann pairs
+  const float2* win = tw + 2 * NZ;
+  __shared__ float2 za[4][NZ], zb[4][NZ];
+  __shared__ float P[4][NF + 3];
+  __shared__ float fw[LM_MAXMEL * MAXSUP];   // packed filter weights
+  __shared__ int2 fs[LM_MAXMEL];
+  const int b = blockIdx.y, t0 = blockIdx.x * MEL_FR;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int Lv = lens ? (lens[b] < NS ? lens[b] : NS) : Lv0;   // the clip's samples, zeros after
+  const float* xw = wave + (long long)b * L;
+  for (int i = threadIdx.x; i < SPAN; i += 256) {   // padded index HOP t0 + i -> reflect -> zero-pad
+    int j = HOP * t0 + i - PAD;
+    if (j < 0) j = -j;
+    if (j >= NS) j = 2 * (NS - 1) - j;
+    xs[i] = j < Lv ? xw[j] : 0.f;
+  }
+  for (int i = threadIdx.x; i < 3 * NZ; i += 256) tw[i] = twg[i];
+  for (int i = threadIdx.x; i < n_mels * MAXSUP; i += 256) fw[i] = fbp[i];
+  for (int i = threadIdx.x; i < n_mels; i += 256) fs[i] = sup[i];
   __syncthreads();
   float lmax = -INFINITY;
-  for (int i = threadIdx.x; i < MEL_FR * n_mels; i += 256) {
-    const int fr = i / n_mels, m = i - fr * n_mels;
-    float acc = 0.f;
-    const int2 r = sup[m];
-    for (int f = r.x; f <= r.y; ++f) acc = fmaf(fb[f * n_mels + m], P[fr][f], acc);
-    const float v = log10f(fmaxf(acc, 1e-10f));
-    logv[((long long)b * NFR + t0 + fr) * n_mels + m] = v;
-    lmax = fmaxf(lmax, v);
+  // each wave owns its frame buffers: stages are ordered by a wave-local LDS fence, not a block barrier
+  auto wsync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  for (int f = 0; f < MEL_FR / 4; ++f) {
+    const int fr = wv * (MEL_FR / 4) + f;
+    const float* xf = xs + HOP * fr;
+    // z[n] = w[2n] x[2n] + i w[2n+1] x[2n+1]  (torch.hann_window(400), periodic, float32)
+    for (int n = lane; n < NZ; n += 64) {
+      const float2 w = win[n];
+      za[wv][n] = make_float2(w.x * xf[2 * n], w.y * xf[2 * n + 1]);
+    }
+    wsync();
+    fft_stage<8>(za[wv], zb[wv], 1, tw, lane);
+    wsync();
+    fft_stage<5>(zb[wv], za[wv], 8, tw, lane);
+    wsync();
+    fft_stage<5>(za[wv], zb[wv], 40, tw, lane);
+    wsync();
+    // real split: X[k] = (Z[k] + conj Z[N-k]) / 2 - i W_400^k (Z[k] - conj Z[N-k]) / 2, k = 0..200
+    for (int k = lane; k < NF; k += 64) {
+      float px;
+      if (k == 0 || k == NZ) {
+        const float2 z0 = zb[wv][0];
+        const float xr = k == 0 ? z0.x + z0.y : z0.x - z0.y;
+        px = xr * xr;
+      } else {
+        const float2 a = zb[wv][k], c = zb[wv][NZ - k];
+        const float2 e = make_float2(0.5f * (a.x + c.x), 0.5f * (a.y - c.y));   // (Z[k] + conj Z[N-k]) / 2
+        const float2 o = make_float2(0.5f * (a.x - c.x), 0.5f * (a.y + c.y));   // (Z[k] - conj Z[N-k]) / 2
+        const float2 wo = cmul(tw[NZ + k], o);                                  // W_400^k o
+        const float xr = e.x + wo.y, xi = e.y - wo.x;                           // e - i wo
+        px = xr * xr + xi * xi;
+      }
+      P[wv][k] = px;
+    }
+    wsync();
+    for (int m = lane; m < n_mels; m += 64) {
+      // in-order fma chain over the filter's support: bit-identical to the dense 201-bin chain (the
+      // other terms are fma(0, P, acc) = acc)
+      // fixed MAXSUP-long chain with zero weights past the support (all LDS reads issued together)
+      float acc = 0.f;
+      const int lo = fs[m].x;
+      #pragma unroll
+      for (int i = 0; i < MAXSUP; ++i) {
+        const int k = lo + i < NF ? lo + i : NF - 1;
+        acc = fmaf(fw[m * MAXSUP + i], P[wv][k], acc);
+      }
+      const float v = log10f(fmaxf(acc, 1e-10f));
+      logv[((long long)b * NFR + t0 + fr) * n_mels + m] = v;
+      lmax = fmaxf(lmax, v);
+    }
   }
   lmax = wave_max(lmax);
-  if ((threadIdx.x & 63) == 0) atomicMax(mx + b, ord_f32(lmax));
+  if (lane == 0) atomicMax(mx + b, ord_f32(lmax));
 }
 
+// 64 frames x n_mels per block: channels-last output straight through (coalesced), the HF layout
+// [B][n_mels][3000] through an LDS transpose so its 64-frame rows are coalesced too
+constexpr int FIN_T = 64;
 template <typename TO>
 __global__ __launch_bounds__(256) void lm_final_kernel(const float* __restrict__ logv, const unsigned* __restrict__ mx,
                                                        int n_mels, float* __restrict__ out_hf, TO* __restrict__ out_cl) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  const int b = blockIdx.y;
-  if (i >= (long long)NFR * n_mels) return;
-  const int t = (int)(i / n_mels), m = (int)(i - (long long)t * n_mels);
+  __shared__ float tile[LM_MAXMEL][FIN_T + 1];
+  const int b = blockIdx.y, t0 = blockIdx.x * FIN_T;
+  const int nt = NFR - t0 < FIN_T ? NFR - t0 : FIN_T;
   const float cl = unord_f32(mx[b]) - 8.0f;
-  const float v = (fmaxf(logv[(long long)b * NFR * n_mels + i], cl) + 4.0f) / 4.0f;
-  if (out_hf) out_hf[((long long)b * n_mels + m) * NFR + t] = v;
-  if (out_cl) out_cl[(long long)b * NFR * n_mels + i] = from_f32<TO>(v);
+  const float* src = logv + ((long long)b * NFR + t0) * n_mels;
+  for (int i = threadIdx.x; i < nt * n_mels; i += 256) {
+    const int t = i / n_mels, m = i - t * n_mels;
+    const float v = (fmaxf(src[i], cl) + 4.0f) / 4.0f;
+    if (out_cl) out_cl[((long long)b * NFR + t0) * n_mels + i] = from_f32<TO>(v);
+    tile[m][t] = v;
+  }
+  if (!out_hf) return;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n_mels * FIN_T; i += 256) {
+    const int m = i / FIN_T, t = i - m * FIN_T;
+    if (t < nt) out_hf[((long long)b * n_mels + m) * NFR + t0 + t] = tile[m][t];
+  }
 }
 
 template <typename TO>
@@ -168,41 +300,30 @@ int launch_normalize_apply(const float* x, int B, int L, const float* st, float*
 
 size_t logmel_workspace_bytes(int B, int n_mels) {
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  return al((size_t)LM_NB * N_FFT * 4) + al((size_t)NF * n_mels * 4) + al((size_t)B * NP * 4) +
-         al((size_t)B * NFR * LM_NB * 4) + al((size_t)B * NFR * n_mels * 4) + al((size_t)B * 4) + 256 +
-         al((size_t)n_mels * 8);
+  return al((size_t)3 * NZ * 8) + al((size_t)NF * n_mels * 4) + al((size_t)B * NFR * n_mels * 4) + al((size_t)B * 4) +
+         al((size_t)n_mels * 8) + al((size_t)n_mels * MAXSUP * 4);
 }
 
 template <typename TO>
 int launch_logmel(const float* x, int B, int L, int n_mels, float* out_hf, TO* out_cl, void* ws, size_t ws_bytes,
                   hipStream_t s, const int* lens) {
-  if (B <= 0 || L <= 0 || n_mels <= 0 || n_mels > 256) return -1;
+  if (B <= 0 || L <= 0 || n_mels < 64 || n_mels > LM_MAXMEL) return -1;   // Whisper: 80 or 128 mels
   if (ws_bytes < logmel_workspace_bytes(B, n_mels)) return -4;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   char* p = (char*)ws;
-  float* zero = (float*)p; p += 256;
-  float* basis = (float*)p; p += al((size_t)LM_NB * N_FFT * 4);
+  float2* tw = (float2*)p; p += al((size_t)3 * NZ * 8);
   float* fb = (float*)p; p += al((size_t)NF * n_mels * 4);
-  float* xp = (float*)p; p += al((size_t)B * NP * 4);
-  float* S = (float*)p; p += al((size_t)B * NFR * LM_NB * 4);
   float* logv = (float*)p; p += al((size_t)B * NFR * n_mels * 4);
   unsigned* mx = (unsigned*)p; p += al((size_t)B * 4);
-  int2* sup = (int2*)p;
-  if (hipMemsetAsync(zero, 0, 256, s) != hipSuccess) return -2;
+  int2* sup = (int2*)p; p += al((size_t)n_mels * 8);
+  float* fbp = (float*)p;
   if (hipMemsetAsync(mx, 0, (size_t)B * 4, s) != hipSuccess) return -2;
-  hipLaunchKernelGGL(lm_basis_kernel, dim3((LM_NB * N_FFT + 255) / 256), dim3(256), 0, s, basis);
+  hipLaunchKernelGGL(lm_twiddle_kernel, dim3((3 * NZ + 255) / 256), dim3(256), 0, s, tw);
   hipLaunchKernelGGL(lm_filters_kernel, dim3((NF * n_mels + 255) / 256), dim3(256), 0, s, fb, n_mels);
-  hipLaunchKernelGGL(lm_support_kernel, dim3((n_mels + 63) / 64), dim3(64), 0, s, fb, n_mels, sup);
-  hipLaunchKernelGGL(lm_pad_kernel, dim3((NP + 255) / 256, B), dim3(256), 0, s, x, L, L < NS ? L : NS, xp, lens);
-  if (hipGetLastError() != hipSuccess) return -2;
-  GemmArgs g{};
-  g.A = xp; g.B = basis; g.M = B * NFR; g.N = LM_NB; g.K = N_FFT;
-  g.rows_per_seg = NFR; g.seg_stride = NP; g.lda = HOP;
-  g.Cf = S; g.ldc = LM_NB; g.act = ACT_NONE; g.zero = zero;
-  int rc = launch_gemm_f32(g, AMODE_SEG, 1, s);
-  if (rc) return rc;
-  hipLaunchKernelGGL(lm_mel_kernel, dim3(NFR / MEL_FR, B), dim3(256), 0, s, S, fb, sup, n_mels, logv, mx);
-  hipLaunchKernelGGL((lm_final_kernel<TO>), dim3((NFR * n_mels + 255) / 256, B), dim3(256), 0, s, logv, mx, n_mels,
+  hipLaunchKernelGGL(lm_support_kernel, dim3((n_mels + 63) / 64), dim3(64), 0, s, fb, n_mels, sup, fbp);
+  hipLaunchKernelGGL(lm_stft_mel_kernel, dim3(NFR / MEL_FR, B), dim3(256), 0, s, x, L, L < NS ? L : NS, lens, tw, fbp,
+                     sup, n_mels, logv, mx);
+  hipLaunchKernelGGL((lm_final_kernel<TO>), dim3((NFR + FIN_T - 1) / FIN_T, B), dim3(256), 0, s, logv, mx, n_mels,
                      out_hf, out_cl);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

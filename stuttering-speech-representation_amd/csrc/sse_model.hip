@@ -1151,7 +1151,7 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
   if (mel_hf)
     RC(launch_mel_to_cl<T>(mel_hf, B, nm, mel, s));
   else
-    RC(prof(m, s, "logmel", 2.0 * B * 3000.0 * LM_NB * 400, (double)B * (480000.0 * 4 + 3000.0 * nm * sizeof(T)),
+    RC(prof(m, s, "logmel", B * 3000.0 * 5.0 * 200 * 7.64, (double)B * (480000.0 * 4 + 3000.0 * nm * (8.0 + sizeof(T))),
             [&] { return launch_logmel<T>(wave, B, L, nm, nullptr, mel, ws + w.lm, logmel_workspace_bytes(B, nm), s,
                                           lens); }));
   T* h1 = (T*)(ws + w.h1);
