@@ -1422,22 +1422,11 @@ __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
 // so padded keys read as zeros (a padded V row must be finite: its probability is exactly 0).
 // No register staging and a lean register budget (<= 96 VGPRs): two or three blocks share a CU,
 // so one block's loads overlap another's MFMA / softmax work.
-SSE_DEV bf16x8 v_frag_sw(const char* Vs, int k0, int d0, int g, int r16) {
-  // V^T fragment from swizzled row-major V (row = key, 128 B): lane reads 8 B of row k, columns
-  // d0 + 4 (r16 & 3) .. +3; the transpose read gathers the 16-bit elements across lanes.  V's 16-B
-  // chunks are XOR-swizzled by 2 ((row >> 1) & 3): the 32 lanes of one LDS pass read 8 rows x 32 B
-  // and every row pair lands on its own 8 banks of each half (the K swizzle, (row >> 1) & 7, maps
-  // chunk pairs {c, c+1} onto each other and conflicts here)
-  auto addr = [&](int row) {
-    const int byte = d0 * 2 + 8 * (r16 & 3);
-    return Vs + row * 128 + (((byte >> 4) ^ (((row >> 1) & 3) << 1)) << 4) + (byte & 15);
-  };
-  const int row = k0 + 4 * g + (r16 >> 2);
-  const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)addr(row));
-  const bf16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)addr(row + 16));
-  return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-}
-
+// V^T fragments come from swizzled row-major V (row = key, 128 B) by ds_read_b64_tr_b16: a lane reads
+// 8 B of row k, columns d0 + 4 (r16 & 3) .. +3, and the transpose read gathers the 16-bit elements
+// across lanes.  V's 16-B chunks are XOR-swizzled by 2 ((row >> 1) & 3): the 32 lanes of one LDS pass
+// read 8 rows x 32 B and every row pair lands on its own 8 banks of each half (the K swizzle,
+// (row >> 1) & 7, maps chunk pairs {c, c+1} onto each other and conflicts here).
 template <bool BIAS, int NKB, bool RAG>
 __global__ __launch_bounds__(32 * NKB, 3) void attention_full_kernel(AttnArgs a, int hpb) {
   constexpr int TP = NKB * 16;                                   // padded keys
@@ -1461,8 +1450,17 @@ __global__ __launch_bounds__(32 * NKB, 3) void attention_full_kernel(AttnArgs a,
   const __amdgpu_buffer_rsrc_t clip =
       __builtin_amdgcn_make_buffer_rsrc((void*)qkv, (short)0, T * H3 * 2, 0x00020000);
   // wave-instruction u (u = wave + NW * i) stages rows [8u, 8u + 8): lane -> row 8u + lane/8, LDS
-  // chunk lane%8 holding source chunk (lane%8) ^ swizzle(row) (K: (row >> 1) & 7, V: v_frag_sw's)
+  // chunk lane%8 holding source chunk (lane%8) ^ swizzle(row) (K: (row >> 1) & 7, V: 2 ((row >> 1) & 3))
   constexpr int NU = 2 * NKB / NW;   // wave-instructions per wave for each of K and V
+  // fragment read offsets are lane constants + compile-time immediates: the K swizzle of row
+  // kb*16 + r16 is (r16 >> 1) & 7 and the V swizzle of row 32 ks + 4 g + (r16 >> 2) (+16) is
+  // 2 (((4 g + (r16 >> 2)) >> 1) & 3), whatever kb / ks
+  const int swk = (r16 >> 1) & 7;
+  const int koff0 = r16 * 128 + ((g ^ swk) << 4), koff1 = r16 * 128 + (((g + 4) ^ swk) << 4);
+  const int rowv = 4 * g + (r16 >> 2), swv = ((rowv >> 1) & 3) << 1;
+  int voffs[4];
+  #pragma unroll
+  for (int db = 0; db < 4; ++db) voffs[db] = rowv * 128 + (((2 * db + ((r16 & 3) >> 1)) ^ swv) << 4) + 8 * (r16 & 1);
 
   for (int hh = 0; hh < hpb; ++hh) {
     const int h = h0 + hh;
@@ -1512,10 +1510,9 @@ __global__ __launch_bounds__(32 * NKB, 3) void attention_full_kernel(AttnArgs a,
     #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int kr = kb * 16 + r16;
       #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 kf = *(const bf16x8*)(Ks + kr * 128 + (((g + 4 * ks) ^ ((kr >> 1) & 7)) * 16));
+        const bf16x8 kf = *(const bf16x8*)(Ks + kb * 2048 + (ks ? koff1 : koff0));
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qq][ks], acc, 0, 0, 0);
       }
       s[kb] = acc;
@@ -1584,7 +1581,13 @@ __global__ __launch_bounds__(32 * NKB, 3) void attention_full_kernel(AttnArgs a,
       }
       #pragma unroll
       for (int db = 0; db < 4; ++db)
-        o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v_frag_sw(Vs, ks * 32, db * 16, g, r16), pf, o[db], 0, 0, 0);
+      {
+        const char* va = Vs + ks * 4096 + voffs[db];
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)va);
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(va + 2048));
+        const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[db], 0, 0, 0);
+      }
     }
     if (qv) {
       const float inv = 1.0f / l;
