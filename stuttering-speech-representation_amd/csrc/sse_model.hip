@@ -821,7 +821,17 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
   if (!c.stable_layer_norm)
     RC((launch_layernorm<float, T>(x, m->ptr<float>(m->enc_ln_w), m->ptr<float>(m->enc_ln_b), M, H, eps, ACT_NONE,
                                    x, xb, s)));
-  RC(sink.emit(0, x));
+  // bf16 pre-LN (stable-LN, WavLM-large): the residual stream is kept in bf16 (xt, free after the
+  // positional conv): the residual GEMMs read and write it in place, both LayerNorms read bf16, the
+  // pooled hidden states are taken from it (half the residual traffic of an fp32 stream)
+  const bool pre16 = sizeof(T) == 2 && c.stable_layer_norm;
+  bf16* x16 = pre16 ? (bf16*)xt : nullptr;
+  if (pre16) {
+    RC((launch_cast<bf16, float>(x, (long long)M * H, x16, s)));
+    RC(sink.emit(0, x16));
+  } else {
+    RC(sink.emit(0, x));
+  }
   // ---- encoder layers ----
   T* qkv = (T*)(ws + w.qkv);
   T* ctx = (T*)(ws + w.ctx);
@@ -843,7 +853,10 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
   for (int l = 0; l < c.layers; ++l) {
     const LayerW& Lw = m->layers[l];
     const LayerW* Lp = l > 0 ? &m->layers[l - 1] : nullptr;
-    if (c.stable_layer_norm)
+    if (pre16)
+      RC((launch_layernorm<bf16, T>(x16, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, ACT_NONE,
+                                    nullptr, xb, s)));
+    else if (c.stable_layer_norm)
       RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, ACT_NONE,
                                      nullptr, xb, s)));
     GemmArgs g{};
@@ -872,8 +885,14 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
       }
       g.Ct = xs; g.opart = p1;
     }
+    if (pre16) {
+      g.resid = nullptr; g.Cf = nullptr; g.resid_t = x16; g.Ct = x16;
+    }
     RC(prof(m, s, "gemm:oproj", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
-    if (!lnfold) {
+    if (pre16) {
+      RC((launch_layernorm<bf16, T>(x16, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, H, eps, ACT_NONE,
+                                    nullptr, xb, s)));
+    } else if (!lnfold) {
       if (!c.stable_layer_norm)
         RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, ACT_NONE, x,
                                        xb, s)));
@@ -897,7 +916,14 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
       g.rpart = p1; g.rpart_nt = nt; g.ln_eps = eps; g.rln_w = m->ptr<float>(Lw.ln1_w); g.rln_b = m->ptr<float>(Lw.ln1_b);
       g.Ct = xb; g.opart = p2;
     }
+    if (pre16) {
+      g.resid = nullptr; g.Cf = nullptr; g.resid_t = x16; g.Ct = x16;
+    }
     RC(prof(m, s, "gemm:ffn2", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    if (pre16) {
+      if (l + 1 < c.layers) RC(sink.emit(l + 1, x16));
+      continue;
+    }
     if (lnfold) {
       RC(sink.emit_ln<T>(l + 1, xb, nullptr, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), eps, p2, nt));
       continue;
@@ -908,7 +934,11 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     }
     if (l + 1 < c.layers || !c.stable_layer_norm) RC(sink.emit(l + 1, x));
   }
-  if (c.stable_layer_norm) {
+  if (pre16) {
+    RC((launch_layernorm<bf16, T>(x16, m->ptr<float>(m->enc_ln_w), m->ptr<float>(m->enc_ln_b), M, H, eps, ACT_NONE,
+                                  x, xb, s)));
+    RC(sink.emit(c.layers, x));
+  } else if (c.stable_layer_norm) {
     RC((launch_layernorm<float, T>(x, m->ptr<float>(m->enc_ln_w), m->ptr<float>(m->enc_ln_b), M, H, eps, ACT_NONE,
                                    x, xb, s)));
     RC(sink.emit(c.layers, x));
