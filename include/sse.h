@@ -103,8 +103,8 @@ int sse_output_frames(const sse_model* m, int L);
 size_t sse_workspace_bytes(const sse_model* m, int B, int L);
 
 /* Whisper front end: d_wave [B][L] fp32 (L <= 480000, zero-padded to 30 s like
- * WhisperFeatureExtractor) -> d_mel [B][n_mels][3000] fp32.  Needs
- * sse_logmel_workspace_bytes(B) of workspace. */
+ * WhisperFeatureExtractor) -> d_mel [B][n_mels][3000] fp32, n_mels in [64, 128] (80: v1/v2,
+ * 128: v3; SSE_ERR_INVALID otherwise).  Needs sse_logmel_workspace_bytes(B, n_mels) of workspace. */
 size_t sse_logmel_workspace_bytes(int B, int n_mels);
 int sse_logmel(const float* d_wave, int B, int L, int n_mels, float* d_mel,
                void* d_ws, size_t ws_bytes, void* stream);
