@@ -772,11 +772,113 @@ __global__ __launch_bounds__(256) void layernorm_mx_kernel(const TI* __restrict_
   }
 }
 
+// bf16 input: 8 elements (one 16-B load) per lane per 512-element chunk, so a row of 1280 is 3 load
+// instructions per lane instead of 5; an MX block of 32 is 4 lanes (DPP quad max); 8-byte fp8 stores.
+SSE_DEV float max4_dpp(float v) {
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true)));   // [1,0,3,2]
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true)));   // [2,3,0,1]
+  return v;
+}
+template <int NC>
+__global__ __launch_bounds__(256) void layernorm_mx8_kernel(const bf16* __restrict__ in, const float* __restrict__ w,
+                                                            const float* __restrict__ bta, int rows, int H, float eps,
+                                                            unsigned char* __restrict__ q,
+                                                            unsigned char* __restrict__ scale) {
+  __shared__ unsigned char sc[64 * LNMX_MAXB];
+  const int r0 = blockIdx.x * 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nb = H >> 5;
+  const float inv_h = 1.0f / (float)H;
+  bf16x8 cur[NC], nxt[NC];
+  auto load = [&](bf16x8 (&v)[NC], int row) {
+    const bf16* x = in + (long long)(row < rows ? row : rows - 1) * H;
+    #pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int c = 512 * i + 8 * lane;
+      v[i] = c < H ? *(const bf16x8*)(x + c) : bf16x8{};
+    }
+  };
+  load(cur, r0 + wave);
+  for (int rr = wave; rr < 64; rr += 4) {
+    const int row = r0 + rr;
+    if (row >= rows) break;
+    if (rr + 4 < 64) load(nxt, row + 4);
+    float s = 0.f;
+    #pragma unroll
+    for (int i = 0; i < NC; ++i)
+      #pragma unroll
+      for (int e = 0; e < 8; ++e) s += (float)cur[i][e];
+    const float mean = wave_sum_fast(s) * inv_h;
+    float qs = 0.f;
+    #pragma unroll
+    for (int i = 0; i < NC; ++i)
+      if (512 * i + 8 * lane < H)
+        #pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = (float)cur[i][e] - mean;
+          qs = fmaf(d, d, qs);
+        }
+    const float rstd = 1.0f / sqrtf(wave_sum_fast(qs) * inv_h + eps);
+    #pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int c = 512 * i + 8 * lane;
+      const bool ok = c < H;   // wave-uniform per 4-lane block (H % 128 == 0)
+      const int cc = ok ? c : 0;
+      const f32x4 w0 = *(const f32x4*)(w + cc), w1 = *(const f32x4*)(w + cc + 4);
+      const f32x4 b0 = *(const f32x4*)(bta + cc), b1 = *(const f32x4*)(bta + cc + 4);
+      float o[8];
+      #pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] = fmaf(((float)cur[i][e] - mean) * rstd, w0[e], b0[e]);   // = ln_apply4
+        o[4 + e] = fmaf(((float)cur[i][4 + e] - mean) * rstd, w1[e], b1[e]);
+      }
+      float m = 0.f;
+      #pragma unroll
+      for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(o[e]));
+      const float a = max4_dpp(m);
+      const int e8 = mx_scale_exp(a);
+      const float inv = mx_inv_scale(e8);
+      int x0 = __builtin_amdgcn_cvt_pk_fp8_f32(o[0] * inv, o[1] * inv, 0, false);
+      x0 = __builtin_amdgcn_cvt_pk_fp8_f32(o[2] * inv, o[3] * inv, x0, true);
+      int x1 = __builtin_amdgcn_cvt_pk_fp8_f32(o[4] * inv, o[5] * inv, 0, false);
+      x1 = __builtin_amdgcn_cvt_pk_fp8_f32(o[6] * inv, o[7] * inv, x1, true);
+      if (ok) {
+        *(int2*)(q + (long long)row * H + c) = make_int2(x0, x1);
+        if ((lane & 3) == 0) sc[rr * LNMX_MAXB + (c >> 5)] = (unsigned char)e8;
+      }
+    }
+    #pragma unroll
+    for (int i = 0; i < NC; ++i) cur[i] = nxt[i];
+  }
+  __syncthreads();
+  for (int u = threadIdx.x; u < 16 * nb; u += 256) {
+    const int r16 = u & 15, blk = u >> 4;
+    if (r0 + r16 >= rows) continue;
+    const unsigned v = (unsigned)sc[r16 * LNMX_MAXB + blk] | ((unsigned)sc[(r16 + 16) * LNMX_MAXB + blk] << 8) |
+                       ((unsigned)sc[(r16 + 32) * LNMX_MAXB + blk] << 16) |
+                       ((unsigned)sc[(r16 + 48) * LNMX_MAXB + blk] << 24);
+    *(unsigned*)(scale + mx_a_scale_off(r0 + r16, blk, H >> 7)) = v;
+  }
+}
+
 template <typename TI>
 int launch_layernorm_mx(const TI* in, const float* w, const float* b, int rows, int H, float eps, unsigned char* q,
                         unsigned char* scale, hipStream_t s) {
   if (H % 128 || H > 2048) return -3;
   const dim3 grid((rows + 63) / 64);
+  if constexpr (sizeof(TI) == 2) {
+    auto go8 = [&](auto ncc) {
+      constexpr int NC = decltype(ncc)::value;
+      hipLaunchKernelGGL((layernorm_mx8_kernel<NC>), grid, dim3(256), 0, s, in, w, b, rows, H, eps, q, scale);
+    };
+    switch ((H + 511) / 512) {
+      case 1: go8(std::integral_constant<int, 1>{}); break;
+      case 2: go8(std::integral_constant<int, 2>{}); break;
+      case 3: go8(std::integral_constant<int, 3>{}); break;
+      default: go8(std::integral_constant<int, 4>{}); break;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+  }
   auto go = [&](auto nic) {
     constexpr int NI = decltype(nic)::value;
     hipLaunchKernelGGL((layernorm_mx_kernel<TI, NI>), grid, dim3(256), 0, s, in, w, b, rows, H, eps, q, scale);
