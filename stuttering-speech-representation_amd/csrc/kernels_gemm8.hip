@@ -598,8 +598,9 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
             const f32x2 lo = gelu_erf2(f32x2{o[0], o[1]}), hi = gelu_erf2(f32x2{o[2], o[3]});
             o = f32x4{lo.x, lo.y, hi.x, hi.y};
           }
-          if (gelu_fast) {
-            const f32x2 lo = gelu_fast2(f32x2{o[0], o[1]}), hi = gelu_fast2(f32x2{o[2], o[3]});
+          if (gelu_fast) {   // fp8 out (Q8): the lower-degree form, its error far below e4m3 rounding
+            const f32x2 lo = Q8 ? gelu_fp8out2(f32x2{o[0], o[1]}) : gelu_fast2(f32x2{o[0], o[1]});
+            const f32x2 hi = Q8 ? gelu_fp8out2(f32x2{o[2], o[3]}) : gelu_fast2(f32x2{o[2], o[3]});
             o = f32x4{lo.x, lo.y, hi.x, hi.y};
           }
           if (has_res) {

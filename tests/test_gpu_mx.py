@@ -89,6 +89,27 @@ def test_gemm_mx_fp8_output_is_the_quantised_result(act):
     bias = torch.from_numpy(np.random.default_rng(3).standard_normal(N).astype(np.float32)).cuda()
     f = gemm_mx(*ops, bias=bias, act=act).cpu().numpy()
     q, sc = gemm_mx(*ops, bias=bias, act=act, out="fp8")
+    if act == "gelu_fast":
+        # the fp8-out epilogue uses the lower-degree GELU (common.h gelu_fp8out2, max abs error 8.2e-4,
+        # below the e4m3 half-step): restated here from the pre-activation, so the bytes agree except
+        # where the two evaluations (fused fma on the GPU, numpy here) straddle an e4m3 rounding boundary
+        # (observed: 0.7 % of the bytes, each one e4m3 step)
+        import sys, os
+        sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tools"))
+        from fit_gelu import gelu_fast as gelu_poly
+        coef = np.array([3.963519037e-01, -6.208017841e-02, 7.574830670e-03, -5.630472442e-04, 2.229058919e-05,
+                         -3.503167250e-07])
+        z = gemm_mx(*ops, bias=bias, act=None).cpu().numpy()
+        q0, _, e0 = mx.quantize(gelu_poly(z, coef, 3.5), 0)
+        qg = q.cpu().numpy().copy()
+        qg[qg == 0x80] = 0   # -0 (tails past the clamp: x Phi(-3.5) < 0) equals +0
+        q0 = q0.copy()
+        q0[q0 == 0x80] = 0
+        assert (qg == q0).mean() >= 0.98
+        assert (np.abs(qg.astype(np.int16) - q0.astype(np.int16)) <= 1).mean() >= 0.999   # sign-magnitude codes
+        assert (mx.exps_from_scales(sc.cpu().numpy(), M, N, 0) == e0).mean() >= 0.995
+        assert np.abs(gelu_poly(z, coef, 3.5) - f).max() <= 1e-3 * max(1.0, np.abs(z).max())
+        return
     q0, _, e0 = mx.quantize(f, 0)
     assert np.array_equal(q.cpu().numpy(), q0)
     assert np.array_equal(mx.exps_from_scales(sc.cpu().numpy(), M, N, 0), e0)
