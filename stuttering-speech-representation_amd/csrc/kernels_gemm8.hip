@@ -174,7 +174,19 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
     const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
     bid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
   }
-  const int m0 = (bid / n_tiles_n) * 256, n0 = (bid % n_tiles_n) * 256;
+  int mt = bid / n_tiles_n, nt_ = bid % n_tiles_n;
+  if constexpr (MX) {
+    // grouped raster (MX): 8 row tiles per group, row fastest, so an XCD's ~32 concurrent tiles span
+    // 8 A row-tiles x 4 B column-tiles (3.9 MB at K = 1280, L2-resident) instead of 2 x all columns
+    // (the whole weight matrix re-streamed into L2 every 2 row-tiles)
+    constexpr int GM = 8;
+    const int MT = (M + 255) / 256;
+    const int first = (bid / (GM * n_tiles_n)) * GM, gm = MT - first < GM ? MT - first : GM;
+    const int r = bid - first * n_tiles_n;
+    mt = first + r % gm;
+    nt_ = r / gm;
+  }
+  const int m0 = mt * 256, n0 = nt_ * 256;
   constexpr int ES = MX ? 1 : 2;   // operand element bytes; a K-tile is 128 B per row either way
   const int nk = K / (128 / ES);
 
