@@ -25,6 +25,8 @@
     }                                                                          \
   } while (0)
 
+typedef unsigned int u32x2_w4 __attribute__((ext_vector_type(2)));
+
 constexpr int W4_HALF = 256 * 128;     // one operand's K-tile: 256 rows x 128 B (64 bf16)
 constexpr int W4_BUF = 2 * W4_HALF;    // A | B
 constexpr int W4_SMEM = 2 * W4_BUF;    // two K-tiles in flight: 128 KiB
@@ -224,9 +226,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
 
 // Persistent form of the ASM kernel: a block walks tiles b, b + G, ...; after a tile's last
-// fragment reads it issues the next tile's K-tile 0 of LDS-DMA under its last 64 MFMAs, stores
-// C from registers, then issues K-tile 1 (vmcnt is one in-order counter for loads and stores on
-// gfx9, so the next tile's wait for K-tile 0 also waits for the stores; K-tile 1 stays in flight).
+// fragment reads it issues the next tile's K-tiles 0 and 1 of LDS-DMA, then runs its last 64 MFMAs
+// with each row block's C stores (buffer stores, exactly 64 per wave) right behind that block's
+// MFMAs; vmcnt retires in issue order, so the next tile's vmcnt(63) waits for both K-tiles but not
+// for the stores.  The first K-tile's MFMAs take srcC = 0 (no accumulator reset).
 // One block per CU (512 registers, 128 KiB of LDS): no co-resident block hides an exposed epilogue.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4p_kernel(
     const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ C, int M, int N, int K, int n_tiles) {
@@ -237,8 +240,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int q = lane >> 4, r16 = lane & 15;
   const int ntn = N / 256, MT = (M + 255) / 256;
   const int nk = K / 64;
-  constexpr int WAIT_ALL = 0x0070, WAIT_VM16 = 0x4F70;
+  constexpr int WAIT_ALL = 0x0070, WAIT_VM16 = 0x4F70, WAIT_VM63 = 0xCF7F;   // vmcnt 63 = hi 0b11, lo 0xF
   constexpr int NREC = 0x7FFFFFF0;
+  const __amdgpu_buffer_rsrc_t c_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)C, (short)0, (int)((long long)M * N * 2 < NREC ? (long long)M * N * 2 : NREC), 0x00020000);
   auto tile_origin = [&](int tid, int& m0, int& n0) {
     const int q8 = n_tiles / 8, r8 = n_tiles % 8, x = tid % 8;
     int bid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + tid / 8;
@@ -285,6 +290,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(rb[j]), "v"(ra[i]));
   };
 
+  // first K-tile of a tile: srcC = inline constant 0 instead of 256 accumulator writes
+  auto mma_row_z = [&](const bf16x8 (&ra)[8], const bf16x8 (&rb)[8], int i) {
+    #pragma unroll
+    for (int j = 0; j < 8; ++j)
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc[i][j]) : "v"(rb[j]), "v"(ra[i]));
+  };
+  auto half0 = [&](int t, bool zero) {   // MFMAs on a0/b0 (ks 0 of K-tile t), reads of a1/b1 (ks 1)
+    if (zero)
+      g8_sfor_w4<0, 8>([&](auto ic) {
+        mma_row_z(a0, b0, decltype(ic)::value);
+        load_frag(a1, b1, t, 1, decltype(ic)::value);
+      });
+    else
+      g8_sfor_w4<0, 8>([&](auto ic) {
+        mma_row(a0, b0, decltype(ic)::value);
+        load_frag(a1, b1, t, 1, decltype(ic)::value);
+      });
+  };
+  int m0c = 0, n0c = 0;
+  auto store_row = [&](int i) {   // exactly 8 buffer stores per row block; rows >= M are dropped
+    const int m = m0c + wm * 128 + i * 16 + r16;
+    const unsigned rowoff = (unsigned)(((long long)m * N + n0c + wn * 128 + 4 * q) * 2);
+    #pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4 v = acc[i][j];
+      const bf16x4 o = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_w4, o), c_rsrc, m < M ? rowoff + j * 32 : 0xFFFFFFF0u,
+                                            0, 0);
+    }
+  };
+
   int tid = blockIdx.x;
   if (tid >= n_tiles) return;
   int m0, n0;
@@ -293,19 +329,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   issue_all(0);
   issue_all(1);
   for (;;) {
-    #pragma unroll
-    for (int i = 0; i < 8; ++i)
-      #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    __builtin_amdgcn_s_waitcnt(WAIT_VM16);   // K-tile 0 (and the previous tile's stores) landed
+    // K-tiles 0 and 1 landed; after the first tile the previous tile's 64 stores per wave were issued
+    // after them (vmcnt retires in order): vmcnt(63) leaves those stores draining
+    if (tid == (int)blockIdx.x) __builtin_amdgcn_s_waitcnt(WAIT_VM16 & ~0x4000);   // vmcnt(0) first tile
+    else __builtin_amdgcn_s_waitcnt(WAIT_VM63);
     w4_barrier();
     g8_sfor_w4<0, 8>([&](auto ic) { load_frag(a0, b0, 0, 0, decltype(ic)::value); });
     for (int t = 0; t < nk - 1; ++t) {
-      g8_sfor_w4<0, 8>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        mma_row(a0, b0, i);
-        load_frag(a1, b1, t, 1, i);
-      });
+      half0(t, t == 0);
       __builtin_amdgcn_s_waitcnt(WAIT_ALL);
       w4_barrier();
       g8_sfor_w4<0, 8>([&](auto ic) {
@@ -315,37 +346,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         load_frag(a0, b0, t + 1, 0, i);
       });
     }
-    // last K-tile: no DMA into the buffers; the next tile's first two K-tiles go out before the stores
-    g8_sfor_w4<0, 8>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      mma_row(a0, b0, i);
-      load_frag(a1, b1, nk - 1, 1, i);
-    });
+    // last K-tile: no DMA into the buffers; the next tile's first two K-tiles go out before the
+    // stores, and each row block's stores follow its last 8 MFMAs (overlapping the next row's)
+    half0(nk - 1, nk == 1);
     __builtin_amdgcn_s_waitcnt(WAIT_ALL);   // also drains the redundant re-loads of tile nk-1
     w4_barrier();                           // every wave's reads of both buffers are done
-    const int m0c = m0, n0c = n0;
+    m0c = m0;
+    n0c = n0;
     const int next = tid + gridDim.x;
-    if (next < n_tiles) {   // K-tile 0 of the next tile lands under this tile's last MFMAs
+    if (next < n_tiles) {
       tile_origin(next, m0, n0);
       setup(m0, n0);
       issue_all(0);
+      issue_all(1);
     }
-    g8_sfor_w4<0, 8>([&](auto ic) { mma_row(a1, b1, decltype(ic)::value); });
-    asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
-    #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = m0c + wm * 128 + i * 16 + r16;
-      if (m < M) {
-        #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const f32x4 v = acc[i][j];
-          *(bf16x4*)(C + (long long)m * N + n0c + wn * 128 + j * 16 + 4 * q) =
-              bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-        }
+    // the reads of a row block's accumulators are pinned behind an asm that names them (a plain
+    // register read is otherwise free to move up to the MFMA asm that produced them, ahead of the
+    // hazard distance the compiler cannot see): row i-1 after row i's 8 MFMAs, row 7 after 24 nops
+    auto fence_row = [&](int i) {
+      asm volatile("" : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][3]), "+a"(acc[i][4]),
+                   "+a"(acc[i][5]), "+a"(acc[i][6]), "+a"(acc[i][7]));
+    };
+    g8_sfor_w4<0, 8>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      mma_row(a1, b1, i);
+      if constexpr (i > 0) {   // 8 independent MFMAs since row i-1's last one
+        fence_row(i - 1);
+        store_row(i - 1);
       }
-    }
+    });
+    asm volatile("s_nop 7\n s_nop 7\n s_nop 7" : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]),
+                 "+a"(acc[7][4]), "+a"(acc[7][5]), "+a"(acc[7][6]), "+a"(acc[7][7]));
+    store_row(7);
     if (next >= n_tiles) break;
-    issue_all(1);   // after the stores: the top-of-tile vmcnt(16) then leaves only this in flight
     tid = next;
   }
   __builtin_amdgcn_s_waitcnt(WAIT_ALL);
