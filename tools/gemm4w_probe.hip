@@ -208,7 +208,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     step(t, F_{}, F_{});
   }
   __builtin_amdgcn_s_waitcnt(WAIT_ALL);   // no LDS-DMA may land after the block releases its LDS
-  if constexpr (ASM) asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");   // MFMA results before reads
+  if constexpr (ASM) {   // MFMA write latency, then pin every accumulator read behind it (see gemm4p_kernel)
+    asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
+    #pragma unroll
+    for (int i = 0; i < 8; ++i)
+      asm volatile("" : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][3]), "+a"(acc[i][4]),
+                   "+a"(acc[i][5]), "+a"(acc[i][6]), "+a"(acc[i][7]));
+  }
   // C^T blocks: lane holds C[row r16][cols 4q .. 4q+3] of each 16x16 block
   #pragma unroll
   for (int i = 0; i < 8; ++i) {
