@@ -237,6 +237,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 // MFMAs; vmcnt retires in issue order, so the next tile's vmcnt(63) waits for both K-tiles but not
 // for the stores.  The first K-tile's MFMAs take srcC = 0 (no accumulator reset).
 // One block per CU (512 registers, 128 KiB of LDS): no co-resident block hides an exposed epilogue.
+template <int GM>   // tile raster: GM row tiles per group, row fastest (GM = 1: row-major)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4p_kernel(
     const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ C, int M, int N, int K, int n_tiles) {
   __shared__ __attribute__((aligned(16))) char smem[W4_SMEM];
@@ -253,7 +254,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   auto tile_origin = [&](int tid, int& m0, int& n0) {
     const int q8 = n_tiles / 8, r8 = n_tiles % 8, x = tid % 8;
     int bid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + tid / 8;
-    constexpr int GM = 8;
     const int first = (bid / (GM * ntn)) * GM, gm = MT - first < GM ? MT - first : GM;
     const int rr = bid - first * ntn;
     m0 = (first + rr % gm) * 256;
@@ -496,7 +496,11 @@ int main() {
       int cus = 256;
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
       const int gp = grid < cus ? grid : cus;
-      auto runp = [&] { hipLaunchKernelGGL(gemm4p_kernel, dim3(gp), dim3(256), 0, 0, a, b, c4, M, N, K, grid); };
+      for (int gmv = 0; gmv < 2; ++gmv) {
+      auto runp = [&] {
+        if (gmv) hipLaunchKernelGGL(gemm4p_kernel<1>, dim3(gp), dim3(256), 0, 0, a, b, c4, M, N, K, grid);
+        else hipLaunchKernelGGL(gemm4p_kernel<8>, dim3(gp), dim3(256), 0, 0, a, b, c4, M, N, K, grid);
+      };
       const float tp = time_ms(runp, 20);
       CK(hipDeviceSynchronize());
       std::vector<bf16> hc((size_t)M * N);
@@ -508,8 +512,10 @@ int main() {
           same += __builtin_bit_cast(unsigned short, hc[i]) == __builtin_bit_cast(unsigned short, h8[i]);
         eq = (double)same / hc.size();
       }
-      printf("  %-15s %.1f TF/s (%.1f us), bit-equal to 8-phase: %.4f\n", "4w persistent", tf / (tp * 1e-3), tp * 1e3, eq);
+      printf("  %-15s %.1f TF/s (%.1f us), bit-equal to 8-phase: %.4f\n", gmv ? "4w persistent rm" : "4w persistent",
+             tf / (tp * 1e-3), tp * 1e3, eq);
       fflush(stdout);
+      }
     }
     CK(hipFree(a)); CK(hipFree(b)); CK(hipFree(c4)); CK(hipFree(c8));
   }
