@@ -121,7 +121,10 @@ int sse_embed(sse_model* m, const float* d_in, int B, int L, const int32_t* laye
  * WavLM's GroupNorm statistics, attention keys, positional-conv padding and time-means cover the
  * clip's own frames; Whisper pads each clip with zeros to 30 s as the feature extractor does.
  * Bit-identical to the per-clip call when the batch's longest clip selects the same attention
- * kernel (WavLM: all clips <= 160 frames, or all > 160). */
+ * kernel (WavLM: all clips <= 160 frames, or all > 160).  The library clamps each length to [0, L]
+ * on the device (no kernel reads past its clip's row whatever the caller passes); a WavLM clip
+ * under 400 samples has no frames and its embedding slots are written as zeros (the Python
+ * wrapper rejects such clips before the call, as the reference's forward would raise). */
 int sse_embed_ragged(sse_model* m, const float* d_in, const int32_t* d_lengths, int B, int L,
                      const int32_t* layer_ids, int n_layers, float* d_out, void* d_ws, size_t ws_bytes,
                      void* stream);

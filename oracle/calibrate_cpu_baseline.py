@@ -10,7 +10,12 @@ The two are run in alternating rounds and each rate is the median over rounds.  
 restatement / reference must lie in [0.9, 1.1]; the result goes to
 profiles/r2_cpu_baseline_calibration.json (bench.py copies the ratio into its cpu_baseline).
 
-Usage: python oracle/calibrate_cpu_baseline.py [--clips 16] [--rounds 3] [--threads 8]
+Whisper (``--model whisper-large-v2``): the reference's ``extract_whisper_embeddings_fixed``
+(REF/whisper_embeddings_large.py:234-299: log-mel, encoder, 1-token decoder) on an HF Whisper-large-v2
+``WhisperModel`` vs ``oracle/whisper_aten.py``; result in profiles/r3_cpu_baseline_calibration_whisper.json.
+
+Usage: python oracle/calibrate_cpu_baseline.py [--model wavlm-base|whisper-large-v2] [--clips 16]
+       [--rounds 3] [--threads 8]
 """
 from __future__ import annotations
 
@@ -48,8 +53,14 @@ def main():
     ap.add_argument("--clips", type=int, default=16)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--threads", type=int, default=os.cpu_count())
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r2_cpu_baseline_calibration.json"))
+    ap.add_argument("--model", default="wavlm-base", choices=["wavlm-base", "whisper-large-v2"])
+    ap.add_argument("--out", default=None)
     a = ap.parse_args()
+    if a.out is None:
+        a.out = os.path.join(ROOT, "profiles", "r2_cpu_baseline_calibration.json" if a.model == "wavlm-base"
+                             else "r3_cpu_baseline_calibration_whisper.json")
+    if a.model != "wavlm-base":
+        return whisper(a)
 
     spec_mg = importlib.util.spec_from_file_location("make_golden", os.path.join(ROOT, "tests", "golden", "make_golden.py"))
     mg = importlib.util.module_from_spec(spec_mg)
@@ -101,6 +112,71 @@ def main():
            "max_rel_l2_restatement_vs_reference": max_rel, "torch": torch.__version__,
            "what": "REF/WavLM_embeddings.py:267-341 extract_wavlm_embeddings (HF WavLMModel, fp32, batch-1 loop) "
                    "vs oracle/wavlm_aten.py on the same clips / weights / threads, alternating rounds, medians"}
+    os.makedirs(os.path.dirname(a.out), exist_ok=True)
+    with open(a.out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res, indent=1))
+    if not 0.9 <= res["ratio"] <= 1.1:
+        raise SystemExit(f"calibration ratio {res['ratio']} outside [0.9, 1.1]")
+
+
+def whisper(a):
+    """Whisper-large-v2 (with its 32-layer decoder for the 1-token pass) vs oracle/whisper_aten.py."""
+    spec_mg = importlib.util.spec_from_file_location("make_golden", os.path.join(ROOT, "tests", "golden", "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec_mg)
+    spec_mg.loader.exec_module(mg)
+    import numpy as np
+    import torch
+    from transformers import WhisperConfig, WhisperFeatureExtractor, WhisperModel
+    from ssr_amd import config as C, synth
+    from oracle.whisper_aten import WhisperAten
+
+    torch.set_num_threads(a.threads)
+    spec = C.WHISPER_LARGE_V2_DEC
+    sd = synth.synth_whisper_state_dict(spec, seed=11, full_hf=True)
+    cfg = WhisperConfig(d_model=spec.d_model, encoder_layers=spec.layers, encoder_attention_heads=spec.heads,
+                        decoder_layers=spec.decoder_layers, decoder_attention_heads=spec.heads,
+                        encoder_ffn_dim=spec.ffn, decoder_ffn_dim=spec.dec_ffn_dim, num_mel_bins=spec.n_mels,
+                        vocab_size=spec.vocab_size, max_target_positions=spec.max_target_positions)
+    with torch.device("meta"):
+        model = WhisperModel(cfg)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True, assign=True)
+    model.eval()
+    proc = WhisperFeatureExtractor(feature_size=spec.n_mels)
+    aten = WhisperAten(spec, sd)
+    clips = synth.synth_clips(a.clips + 1, 48000, seed=2024)
+    enc_idx, dec_idx = spec.default_layer_indices(), spec.default_decoder_indices()
+    paths = mg._register("calibw", clips)
+    cwd = os.getcwd()
+    ref_rates, port_rates, max_rel = [], [], 0.0
+    with tempfile.TemporaryDirectory() as td:
+        os.chdir(td)
+        try:
+            mg._install_torchaudio_stub()
+            ref = mg._import_ref("ref_whisper_embeddings", "whisper_embeddings_large.py")
+            ref.extract_whisper_embeddings_fixed(paths[0], model, proc, "cpu", enc_idx, dec_idx)   # warm-up both
+            aten.extract(clips[0], enc_idx, dec_idx)
+            for _ in range(a.rounds):
+                t0 = time.perf_counter()
+                got_ref = [ref.extract_whisper_embeddings_fixed(p, model, proc, "cpu", enc_idx, dec_idx) for p in paths[1:]]
+                ref_rates.append(a.clips / (time.perf_counter() - t0))
+                t0 = time.perf_counter()
+                got = [aten.extract(c, enc_idx, dec_idx) for c in clips[1:]]
+                port_rates.append(a.clips / (time.perf_counter() - t0))
+                for d0, d1 in zip(got_ref, got):
+                    for k in d0:
+                        max_rel = max(max_rel, float(np.linalg.norm(d1[k] - d0[k]) / np.linalg.norm(d0[k])))
+        finally:
+            os.chdir(cwd)
+    r_ref, r_port = statistics.median(ref_rates), statistics.median(port_rates)
+    res = {"reference_clips_per_s": round(r_ref, 4), "restatement_clips_per_s": round(r_port, 4),
+           "ratio": round(r_port / r_ref, 4), "rounds_reference": [round(x, 4) for x in ref_rates],
+           "rounds_restatement": [round(x, 4) for x in port_rates], "threads": a.threads,
+           "host_cpus": os.cpu_count(), "cpu_model": cpu_model(), "clips": a.clips, "clip_s": 3.0,
+           "max_rel_l2_restatement_vs_reference": max_rel, "torch": torch.__version__,
+           "what": "REF/whisper_embeddings_large.py:234-299 extract_whisper_embeddings_fixed (HF WhisperModel "
+                   "large-v2 shape, encoder + 1-token decoder, fp32, batch-1 loop) vs oracle/whisper_aten.py on the "
+                   "same clips / weights / threads, alternating rounds, medians"}
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1)

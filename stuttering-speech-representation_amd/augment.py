@@ -147,18 +147,41 @@ def augment_audio(waveform, sample_rate=16000, augmentation_type="random", *, rn
         return x.numpy()
 
 
+def _recoverable(e: BaseException) -> bool:
+    """Errors one clip can cause and a per-clip retry can get past: out of memory, an invalid clip
+    (shorter than the receptive field: SSE_ERR_INVALID, or the wrapper's ValueError) or a shape the
+    kernels do not cover.  A HIP runtime failure (SSE_ERR_HIP: a fault or a sticky context error)
+    and anything unexpected are NOT: after those every clip would fail again, so they propagate
+    instead of silently dropping every augmented sample."""
+    from ._lib import SSEError, SSEOutOfMemoryError
+    if isinstance(e, (SSEOutOfMemoryError, torch.OutOfMemoryError, ValueError)):
+        return True
+    return isinstance(e, SSEError) and e.rc in (-1, -3, -4)
+
+
 def _per_clip_fallback(run, part):
-    """run(part) -> one result per clip.  A failing batch (a clip shorter than the receptive field,
-    OOM, ...) is retried one clip at a time; a clip that still fails gets None and is skipped, as
-    the reference's per-sample try/except does (REF/model_training_1.py:379-419)."""
+    """run(part) -> one result per clip.  A batch failing with a recoverable error (a clip shorter
+    than the receptive field, OOM, ...) is retried one clip at a time; a clip that still fails gets
+    None and is skipped, as the reference's per-sample try/except does
+    (REF/model_training_1.py:379-419).  Unrecoverable errors propagate."""
     try:
         return run(part)
     except Exception as e:
+        if not _recoverable(e):
+            raise
         if len(part) == 1:
             logger.warning(f"Error extracting embeddings from augmented audio: {e}")
             return [None]
         logger.warning(f"Batched embedding of {len(part)} augmented clips failed ({e}); retrying one at a time")
         return [r for j in part for r in _per_clip_fallback(run, [j])]
+
+
+def _length_sorted_batches(audios, batch):
+    """Ragged batches of up to `batch` clips, clips sorted by length so a batch's padding stays
+    small: every clip of any length shares a batch (sse_embed_ragged embeds each at its own length)
+    instead of one batch per exact length."""
+    order = sorted(range(len(audios)), key=lambda j: int(audios[j].shape[-1]))
+    return [order[c:c + batch] for c in range(0, len(order), batch)]
 
 
 def _embed_jobs(audios, model, feature_extractor, device, layer_names, model_type, batch):
@@ -172,23 +195,20 @@ def _embed_jobs(audios, model, feature_extractor, device, layer_names, model_typ
         if isinstance(model, WavLMModel):
             n_hs = model.sse.spec.layers + 1
             valid = [i for i in idx if i < n_hs]
-            by_len = {}
-            for j, a in enumerate(audios):
-                by_len.setdefault(int(a.shape[-1]), []).append(j)
             if not valid:                      # no requested layer exists: {} per clip (REF :259-264)
                 return [{} for _ in audios]
 
             def run(part):
-                x = torch.stack([audios[j] for j in part])
-                x = feature_extractor(x, sampling_rate=16000, return_tensors="pt").to(device).input_values
-                e = model.embed(x, valid).cpu().numpy()
+                # the feature extractor per clip (its normalisation statistics cover that clip only,
+                # like the reference's batch-1 call), then one ragged batch
+                xs = [feature_extractor(audios[j], sampling_rate=16000, return_tensors="pt").to(device)
+                      .input_values[0] for j in part]
+                e = model.sse.embed_clips(xs, valid).cpu().numpy()
                 return [{f"layer_{i}": e[r, q].copy() for q, i in enumerate(valid)} for r in range(len(part))]
 
-            for L, js in by_len.items():
-                for c in range(0, len(js), batch):
-                    part = js[c:c + batch]
-                    for j, r in zip(part, _per_clip_fallback(run, part)):
-                        out[j] = r
+            for part in _length_sorted_batches(audios, batch):
+                for j, r in zip(part, _per_clip_fallback(run, part)):
+                    out[j] = r
             return out
         for j, a in enumerate(audios):
             out[j] = extract_embeddings_from_audio_wavlm(a.cpu().numpy(), model, feature_extractor, device, idx)
@@ -200,14 +220,17 @@ def _embed_jobs(audios, model, feature_extractor, device, layer_names, model_typ
             dec = [int(n.split("_")[-1]) for n in layer_names if n.startswith("decoder_layer_")]
             enc = [i for i in enc if i < spec.layers + 1]
             dec = [i for i in dec if i < spec.decoder_layers + 1] if spec.decoder_layers else []
-            by_len = {}
-            for j, a in enumerate(audios):
-                by_len.setdefault(int(a.shape[-1]), []).append(j)
             if not enc and not dec:
                 return [{} for _ in audios]
 
             def run(part):
-                e, d = model.sse.whisper_embed(torch.stack([audios[j] for j in part]), enc, dec)
+                # Whisper pads every clip to 30 s (the feature extractor does): a zero-padded batch
+                # is the ragged batch
+                L = max(int(audios[j].shape[-1]) for j in part)
+                x = torch.zeros((len(part), L), dtype=torch.float32, device=model.sse.device)
+                for r, j in enumerate(part):
+                    x[r, :audios[j].shape[-1]] = audios[j]
+                e, d = model.sse.whisper_embed(x, enc, dec)
                 e, d = e.cpu().numpy(), d.cpu().numpy()
                 res = []
                 for r in range(len(part)):
@@ -216,11 +239,9 @@ def _embed_jobs(audios, model, feature_extractor, device, layer_names, model_typ
                     res.append(x)
                 return res
 
-            for L, js in by_len.items():
-                for c in range(0, len(js), batch):
-                    part = js[c:c + batch]
-                    for j, r in zip(part, _per_clip_fallback(run, part)):
-                        out[j] = r
+            for part in _length_sorted_batches(audios, batch):
+                for j, r in zip(part, _per_clip_fallback(run, part)):
+                    out[j] = r
             return out
         for j, a in enumerate(audios):
             out[j] = extract_embeddings_from_audio_whisper(a.cpu().numpy(), model, feature_extractor, device,

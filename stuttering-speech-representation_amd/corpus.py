@@ -1,22 +1,34 @@
 """Clip-sharded multi-GPU extraction (BASELINE configs[3]).
 
-The reference has no parallelism at all: one process, one device, batch 1
-(REF/WavLM_embeddings.py:575-586).  Here one process per GPU (torch.distributed, backend
-"nccl" = RCCL over xGMI) each embeds a contiguous shard of the corpus and ONE all-gather
-reassembles the [N, n_layers, H] embedding matrix in corpus order on every rank:
+The reference has no parallelism at all: one process, one device, batch 1, every file embedded at
+its own length (REF/WavLM_embeddings.py:575-586, :284-307).  Here one process per GPU
+(torch.distributed, backend "nccl" = RCCL over xGMI) each embeds a contiguous shard of the corpus
+and ONE all-gather reassembles the [N, n_layers, H] embedding matrix in corpus order on every rank:
 
   rank r owns clips [r*P, min((r+1)*P, N)), P = ceil(N / world)
-  each shard is processed in batches of `batch` clips into a [P, n_layers, H] buffer
-  (rows past the shard's end stay zero: equal counts for the all-gather), then
-  all_gather_into_tensor -> [world*P, ...] -> trimmed to N rows.
+  each shard is processed in batches of `batch` clips straight into a [P, n_layers, H] buffer
+  (``out=`` slices: nothing is allocated per batch; rows past the shard's end stay zero: equal
+  counts for the all-gather), then all_gather_into_tensor -> [world*P, ...] -> trimmed to N rows.
+
+Mixed-length corpora: ``clip_source`` may return a list of 1-D clips (or ``(wave, lengths)``);
+the batch is then a zero-padded ragged batch and every clip is embedded at its own length
+(``SSEModel.embed(lengths=)`` -> sse_embed_ragged), so a corpus of mixed lengths does not fragment
+into per-length batches.
+
+Host-staged clips (numpy / CPU tensors) are double-buffered: batch i+1 is packed into a pinned
+host buffer and copied on a side stream into the other of two device buffers while batch i
+computes; the compute stream waits only for its own batch's copy event, and a device / pinned
+buffer is rewritten only after the compute / copy that last used it has finished.  Clips already on
+the device are used in place.
 
 The exchange is the only collective (clips are independent); it moves N*n_layers*H*4 bytes
 in total (614 MB for 50k WavLM-base clips), milliseconds against seconds of compute.
 ``embed_fn`` is injectable so the sharding, padding and ordering logic is testable with the
-gloo backend on CPU; in production it is ``SSEModel.embed`` on the rank's GPU.
+gloo backend on CPU; in production it is ``sse_embed_fn`` (SSEModel.embed) on the rank's GPU.
 """
 from __future__ import annotations
 
+import inspect
 import math
 from typing import Callable
 
@@ -33,34 +45,141 @@ def shard_bounds(n_items: int, world: int, rank: int) -> tuple[int, int, int]:
     return start, min(start + per, n_items), per
 
 
-def extract_corpus(clip_source: Callable[[int, int], np.ndarray | torch.Tensor], n_items: int,
-                   embed_fn: Callable[[torch.Tensor], torch.Tensor], out_shape: tuple[int, int],
-                   device, batch: int = 256, group=None) -> torch.Tensor:
+def _as_batch(src):
+    """clip_source output -> (wave [b, L] tensor or ndarray, lengths list | None)."""
+    if isinstance(src, tuple):
+        wave, lens = src
+        return wave, (None if lens is None else [int(v) for v in lens])
+    if isinstance(src, list):
+        lens = [int(np.asarray(c).shape[-1]) if not isinstance(c, torch.Tensor) else int(c.shape[-1]) for c in src]
+        on_dev = all(isinstance(c, torch.Tensor) and c.device.type != "cpu" for c in src)
+        if on_dev:
+            wave = torch.zeros((len(src), max(lens)), dtype=torch.float32, device=src[0].device)
+            for i, c in enumerate(src):
+                wave[i, :lens[i]] = c.to(torch.float32)
+        else:
+            wave = np.zeros((len(src), max(lens)), np.float32)
+            for i, c in enumerate(src):
+                wave[i, :lens[i]] = c.cpu().numpy() if isinstance(c, torch.Tensor) else np.asarray(c, np.float32)
+        return wave, lens
+    return src, None
+
+
+def _accepts(fn, name: str) -> bool:
+    try:
+        sig = inspect.signature(fn)
+    except (TypeError, ValueError):
+        return False
+    return name in sig.parameters or any(p.kind == p.VAR_KEYWORD for p in sig.parameters.values())
+
+
+class _Stager:
+    """Double-buffered pinned-host -> device staging on a side stream (CUDA devices only)."""
+
+    def __init__(self, device):
+        self.dev = torch.device(device)
+        self.stream = torch.cuda.Stream(self.dev)
+        self.host = [None, None]       # pinned [b, L] fp32
+        self.dbuf = [None, None]       # device [b, L] fp32
+        self.copied = [None, None]     # event: the copy into dbuf[k] is done
+        self.freed = [None, None]      # event: the compute that read dbuf[k] is done
+
+    def put(self, k: int, wave) -> tuple[torch.Tensor, torch.cuda.Event]:
+        w = wave if isinstance(wave, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(wave, np.float32))
+        w = w.to(torch.float32)
+        shape = tuple(w.shape)
+        if self.copied[k] is not None:
+            self.copied[k].synchronize()         # the pinned buffer's last copy has been read
+        direct = w.is_pinned() and w.is_contiguous()   # caller-owned pinned memory: copied from in place
+        if not direct and (self.host[k] is None or self.host[k].numel() < w.numel()):
+            self.host[k] = torch.empty(w.numel(), dtype=torch.float32, pin_memory=True)
+        if direct:
+            h = w
+        else:
+            h = self.host[k][:w.numel()].view(shape)
+            h.copy_(w)
+        with torch.cuda.stream(self.stream):
+            if self.freed[k] is not None:
+                self.stream.wait_event(self.freed[k])   # compute on the old contents is finished
+            if self.dbuf[k] is None or self.dbuf[k].numel() < w.numel():
+                self.dbuf[k] = torch.empty(w.numel(), dtype=torch.float32, device=self.dev)
+            d = self.dbuf[k][:w.numel()].view(shape)
+            d.copy_(h, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        self.copied[k] = ev
+        return d, ev
+
+    def release(self, k: int) -> None:
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.dev))
+        self.freed[k] = ev
+
+
+def extract_corpus(clip_source: Callable[[int, int], object], n_items: int,
+                   embed_fn: Callable[..., torch.Tensor], out_shape: tuple[int, int],
+                   device, batch: int = 256, group=None, prefetch: bool = True) -> torch.Tensor:
     """Embed clips [0, n_items) across the process group; returns [n_items, *out_shape] fp32 on
     `device` on every rank (corpus order).
 
-    clip_source(start, stop) -> [stop-start, L] clips of this rank's range (host or device).
-    embed_fn(wave [b, L] on device) -> [b, *out_shape] fp32 on device.
+    clip_source(start, stop) -> the clips of that range: an array / tensor [stop-start, L]
+    (host or device), a list of 1-D clips of any lengths, or (wave [b, L], lengths).
+    embed_fn(wave [b, L] on device, lengths=None | list, out=None | [b, *out_shape]) ->
+    [b, *out_shape] fp32 on device (``lengths`` / ``out`` are passed only if it accepts them;
+    without ``lengths`` a ragged batch is an error).
     """
     import torch.distributed as dist
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     start, stop, per = shard_bounds(n_items, world, rank)
-    local = torch.zeros((per,) + tuple(out_shape), dtype=torch.float32, device=device)
-    for s in range(start, stop, batch):
-        e = min(s + batch, stop)
-        wave = clip_source(s, e)
-        if not isinstance(wave, torch.Tensor):
-            wave = torch.from_numpy(np.ascontiguousarray(wave))
-        local[s - start:e - start] = embed_fn(wave.to(device, torch.float32))
+    dev = torch.device(device)
+    local = torch.zeros((per,) + tuple(out_shape), dtype=torch.float32, device=dev)
+    takes_len, takes_out = _accepts(embed_fn, "lengths"), _accepts(embed_fn, "out")
+    stager = _Stager(dev) if (prefetch and dev.type == "cuda") else None
+    ranges = [(s, min(s + batch, stop)) for s in range(start, stop, batch)]
+
+    def fetch(i):
+        s, e = ranges[i]
+        wave, lens = _as_batch(clip_source(s, e))
+        if lens is not None and not takes_len:
+            raise ValueError("a ragged batch needs an embed_fn that takes lengths=")
+        if isinstance(wave, torch.Tensor) and wave.device == dev:
+            return wave.to(torch.float32), lens, None
+        if stager is not None:
+            d, ev = stager.put(i & 1, wave)
+            return d, lens, ev
+        w = wave if isinstance(wave, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(wave))
+        return w.to(dev, torch.float32), lens, None
+
+    nxt = fetch(0) if ranges else None
+    for i, (s, e) in enumerate(ranges):
+        wave, lens, ev = nxt
+        if ev is not None:
+            torch.cuda.current_stream(dev).wait_event(ev)
+        kw = {}
+        if lens is not None:
+            kw["lengths"] = lens
+        if takes_out:
+            kw["out"] = local[s - start:e - start]
+        res = embed_fn(wave, **kw)
+        if stager is not None and ev is not None:
+            stager.release(i & 1)
+        if i + 1 < len(ranges):
+            nxt = fetch(i + 1)             # staged (host pack + async copy) while batch i computes
+        if res is not None and res.data_ptr() != local[s - start:e - start].data_ptr():
+            local[s - start:e - start] = res
     if not dist.is_initialized():
         return local[:n_items]
-    full = torch.empty((world * per,) + tuple(out_shape), dtype=torch.float32, device=device)
+    full = torch.empty((world * per,) + tuple(out_shape), dtype=torch.float32, device=dev)
     dist.all_gather_into_tensor(full, local, group=group)
     return full[:n_items]
 
 
-def sse_embed_fn(model, layer_indices) -> Callable[[torch.Tensor], torch.Tensor]:
-    """embed_fn for extract_corpus backed by the HIP path (SSEModel.embed)."""
+def sse_embed_fn(model, layer_indices) -> Callable[..., torch.Tensor]:
+    """embed_fn for extract_corpus backed by the HIP path (SSEModel.embed): writes into ``out``,
+    ragged batches through ``lengths``."""
     idx = [int(i) for i in layer_indices]
-    return lambda wave: model.embed(wave, idx)
+
+    def fn(wave, lengths=None, out=None):
+        return model.embed(wave, idx, out=out, lengths=lengths)
+    return fn

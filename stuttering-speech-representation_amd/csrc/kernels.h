@@ -17,7 +17,8 @@ int launch_conv0_gn(const float* x, int B, int L, const float* norm, const float
 struct ClipFrames {
   int n_conv, kernel[8], stride[8];
 };
-int launch_clip_frames(const int* lens, int B, ClipFrames cf, int* t0, int* tf, hipStream_t s);
+// L: the batch's row length in samples (lengths are clamped to [0, L] on the device)
+int launch_clip_frames(const int* lens, int B, int L, ClipFrames cf, int* t0, int* tf, hipStream_t s);
 // zero rows t >= tlen[b] of x [B][T][H] (ragged batches: the padded positional conv must read zeros)
 template <typename TE>
 int launch_mask_rows(TE* x, int B, int T, int H, const int* tlen, hipStream_t s);

@@ -12,7 +12,9 @@
 __global__ __launch_bounds__(256) void wave_stats_kernel(const float* __restrict__ x, int LS,
                                                          float* __restrict__ out, const int* __restrict__ lens) {
   const float* xb = x + (long long)blockIdx.x * LS;
-  const int L = lens ? lens[blockIdx.x] : LS;
+  // ragged batches: the clip's own samples, clamped to the row (a length past the row never reads
+  // the next clip; an empty clip gives mean 0, rstd of eps alone)
+  const int L = lens ? min(max(lens[blockIdx.x], 0), LS) : LS;
   double s = 0.0, q = 0.0;
   for (int i = threadIdx.x; i < L; i += 256) {
     const double v = xb[i];
@@ -28,7 +30,7 @@ __global__ __launch_bounds__(256) void wave_stats_kernel(const float* __restrict
   if (threadIdx.x == 0) {
     const double S = sh[0][0] + sh[0][1] + sh[0][2] + sh[0][3];
     const double Q = sh[1][0] + sh[1][1] + sh[1][2] + sh[1][3];
-    const double mean = S / L, var = Q / L - mean * mean;
+    const double mean = L > 0 ? S / L : 0.0, var = L > 0 ? Q / L - mean * mean : 0.0;
     out[2 * blockIdx.x] = (float)mean;
     out[2 * blockIdx.x + 1] = (float)(1.0 / sqrt((var > 0 ? var : 0.0) + 1e-7));
   }
@@ -115,8 +117,9 @@ __global__ void gn_finalize_kernel(const double* __restrict__ mom, int B, int C,
     #pragma unroll
     for (int j = a; j < K0; ++j) q += (a == j ? 1.0 : 2.0) * w[a] * w[j] * G[k++];
   }
-  const double m0 = sw / T0;                           // mean of w.x_t
-  double var = q / T0 - m0 * m0;
+  const double inv = T0 > 0 ? 1.0 / T0 : 0.0;         // a frameless clip (ragged) stays finite
+  const double m0 = sw * inv;                          // mean of w.x_t
+  double var = q * inv - m0 * m0;
   var = var > 0 ? var : 0;
   const double mean = m0 + (b0 ? (double)b0[c] : 0.0);
   const float rstd = (float)(1.0 / sqrt(var + (double)eps));
@@ -995,7 +998,9 @@ __global__ __launch_bounds__(256) void pool_mean_kernel(const TI* __restrict__ x
   part[wv][lane * 4 + 3] = s3;
   __syncthreads();
   const int c = threadIdx.x, nc = blockIdx.x * 256 + c;
-  if (nc < H) out[b * out_stride + nc] = (float)((part[0][c] + part[1][c] + part[2][c] + part[3][c]) / T);
+  // a clip with no frames (ragged batch, shorter than the receptive field) pools to zeros, never
+  // 0/0; the host wrapper rejects such clips before the call (SSEModel.embed)
+  if (nc < H) out[b * out_stride + nc] = T > 0 ? (float)((part[0][c] + part[1][c] + part[2][c] + part[3][c]) / T) : 0.f;
 }
 
 template <typename TI>
@@ -1015,11 +1020,14 @@ template int launch_pool_mean<bf16>(const bf16*, int, int, int, float*, long lon
 // ---------------------------------------------------------------------------------------
 // Ragged batches: per-clip frame counts after conv0 and after the last conv layer (the same
 // integer recurrence as wavlm_frames on the host); 0 for a clip shorter than the receptive field.
-__global__ void clip_frames_kernel(const int* __restrict__ lens, int B, ClipFrames cf, int* __restrict__ t0,
+// The sample count is clamped to [0, L] (L = the batch's row length) on the device, so no length
+// the caller passes makes a later kernel read past its clip's rows: the recurrence is monotone, so
+// t0 <= T0 and tf <= Tf of the padded batch.
+__global__ void clip_frames_kernel(const int* __restrict__ lens, int B, int L, ClipFrames cf, int* __restrict__ t0,
                                    int* __restrict__ tf) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  int t = lens[b], f0 = 0;
+  int t = min(max(lens[b], 0), L), f0 = 0;
   for (int i = 0; i < cf.n_conv; ++i) {
     t = t < cf.kernel[i] ? 0 : (t - cf.kernel[i]) / cf.stride[i] + 1;
     if (i == 0) f0 = t;
@@ -1028,8 +1036,8 @@ __global__ void clip_frames_kernel(const int* __restrict__ lens, int B, ClipFram
   tf[b] = t;
 }
 
-int launch_clip_frames(const int* lens, int B, ClipFrames cf, int* t0, int* tf, hipStream_t s) {
-  hipLaunchKernelGGL(clip_frames_kernel, dim3((B + 255) / 256), dim3(256), 0, s, lens, B, cf, t0, tf);
+int launch_clip_frames(const int* lens, int B, int L, ClipFrames cf, int* t0, int* tf, hipStream_t s) {
+  hipLaunchKernelGGL(clip_frames_kernel, dim3((B + 255) / 256), dim3(256), 0, s, lens, B, L, cf, t0, tf);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -717,11 +717,11 @@ int gelu_rounded_act() {
 
 // Ragged batches (lens: samples of each clip, device): the per-clip conv0 frame counts t0 and
 // final frame counts tf go to the workspace; the sink's means run over tf.
-int ragged_frames(const sse_model* m, const int* lens, int B, int* t0, int* tf, hipStream_t s) {
+int ragged_frames(const sse_model* m, const int* lens, int B, int L, int* t0, int* tf, hipStream_t s) {
   ClipFrames cf{};
   cf.n_conv = m->cfg.n_conv;
   for (int i = 0; i < cf.n_conv; ++i) { cf.kernel[i] = m->cfg.conv_kernel[i]; cf.stride[i] = m->cfg.conv_stride[i]; }
-  return launch_clip_frames(lens, B, cf, t0, tf, s);
+  return launch_clip_frames(lens, B, L, cf, t0, tf, s);
 }
 
 template <typename T>
@@ -734,7 +734,7 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
   int* tflen = lens ? t0len + B : nullptr;
   Sink sink = sink_in;
   sink.tlen = tflen;
-  if (lens) RC(ragged_frames(m, lens, B, t0len, tflen, s));
+  if (lens) RC(ragged_frames(m, lens, B, L, t0len, tflen, s));
   int Ts[8];
   const int Tf = wavlm_frames(c, L, Ts);
   const int H = c.hidden, nh = c.heads, F = c.ffn;
@@ -999,7 +999,7 @@ int wavlm_forward_x3(sse_model* m, const float* wave, int B, int L, const Sink& 
   int* tflen = lens ? t0len + B : nullptr;
   Sink sink = sink_in;
   sink.tlen = tflen;
-  if (lens) RC(ragged_frames(m, lens, B, t0len, tflen, s));
+  if (lens) RC(ragged_frames(m, lens, B, L, t0len, tflen, s));
   int Ts[8];
   const int Tf = wavlm_frames(c, L, Ts);
   const int H = c.hidden, nh = c.heads, F = c.ffn;

@@ -164,6 +164,9 @@ class SSEModel:
         n = ids.numel()
         if out is None:
             out = torch.empty((B, n, self.spec.hidden), dtype=torch.float32, device=self.device)
+        elif (out.device != self.device or out.dtype != torch.float32 or tuple(out.shape) != (B, n, self.spec.hidden)
+              or not out.is_contiguous()):
+            raise ValueError(f"out must be a contiguous fp32 [{B}, {n}, {self.spec.hidden}] tensor on {self.device}")
         ws = self.workspace(B, L)
         if lengths is None:
             _lib.check(_lib.lib().sse_embed(self._h, wave.data_ptr(), B, L, ids.data_ptr(), n, out.data_ptr(),
@@ -174,7 +177,10 @@ class SSEModel:
             raise ValueError(f"lengths must be {B} values in [1, {L}]")
         if isinstance(self.spec, WavLMSpec) and min(self.spec.frames(v) for v in lens) <= 0:
             raise _lib.SSEError(-1, "a clip is shorter than the conv receptive field")
-        d_len = torch.tensor(lens, dtype=torch.int32).to(self.device, non_blocking=False)
+        # pinned + non_blocking: the copy is ordered on the current stream without a host sync, so a
+        # staged corpus loop keeps its copy / compute overlap (the caching host allocator keeps the
+        # pinned buffer alive until the copy has run)
+        d_len = torch.tensor(lens, dtype=torch.int32).pin_memory().to(self.device, non_blocking=True)
         _lib.check(_lib.lib().sse_embed_ragged(self._h, wave.data_ptr(), d_len.data_ptr(), B, L, ids.data_ptr(), n,
                                                out.data_ptr(), ws.data_ptr(), ws.numel(), self._stream()),
                    "sse_embed_ragged")

@@ -20,7 +20,27 @@ def _embed(wave):
     return wave.reshape(b, 2, 3, -1).mean(-1)
 
 
-def _worker(rank, world, port, n_items, batch, q):
+def _ragged_clip(i):
+    n = 20 + (i * 7919) % 41          # lengths 20..60
+    return np.sin(i * 0.37 + np.arange(n, dtype=np.float32) * 0.11).astype(np.float32)
+
+
+def _embed_one(x):
+    # one clip at its own length -> [2, 3] (depends on no padding)
+    return torch.stack([torch.stack([x.mean(), x.abs().max(), x[:7].sum()]),
+                        torch.stack([(x * x).mean(), x.min(), torch.tensor(float(x.numel()))])])
+
+
+def _embed_ragged(wave, lengths=None, out=None):
+    lens = lengths if lengths is not None else [wave.shape[1]] * wave.shape[0]
+    res = torch.stack([_embed_one(wave[b, :lens[b]]) for b in range(wave.shape[0])])
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res
+
+
+def _worker(rank, world, port, n_items, batch, q, ragged=False):
     import importlib
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -30,7 +50,11 @@ def _worker(rank, world, port, n_items, batch, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        out = extract_corpus(lambda s, e: _clips(s, e, 66), n_items, _embed, (2, 3), "cpu", batch=batch)
+        if ragged:   # mixed lengths: a list of 1-D clips per batch -> padded batch + lengths
+            out = extract_corpus(lambda s, e: [_ragged_clip(i) for i in range(s, e)], n_items, _embed_ragged, (2, 3),
+                                 "cpu", batch=batch)
+        else:
+            out = extract_corpus(lambda s, e: _clips(s, e, 66), n_items, _embed, (2, 3), "cpu", batch=batch)
         q.put((rank, out.numpy()))
     finally:
         dist.destroy_process_group()
@@ -68,3 +92,43 @@ def test_shard_bounds_cover_exactly_once():
             assert seen == list(range(n))
     with pytest.raises(ValueError):
         shard_bounds(10, 2, 2)
+
+
+@pytest.mark.parametrize("world,n_items,batch", [(2, 11, 4), (3, 8, 3)])
+def test_sharded_ragged_extraction_matches_per_clip(world, n_items, batch):
+    """Mixed-length corpus (REF/WavLM_embeddings.py:284-307 embeds each file at its own length):
+    every rank's ragged batches give exactly each clip's own embedding, in corpus order."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31500 + (os.getpid() % 1000) + world * 11 + n_items
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_items, batch, q, True)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = torch.stack([_embed_one(torch.from_numpy(_ragged_clip(i))) for i in range(n_items)]).numpy()
+    for r in range(world):
+        assert np.array_equal(res[r], ref), r
+
+
+def test_extract_corpus_out_and_lengths_protocol():
+    """Single process: embed_fn receives out= slices of the shard buffer (no per-batch allocation)
+    and lengths= only for ragged batches; an embed_fn without lengths= rejects a ragged batch."""
+    import importlib
+    importlib.import_module("stuttering-speech-representation_amd")
+    from ssr_amd.corpus import extract_corpus
+    seen = []
+
+    def fn(wave, lengths=None, out=None):
+        seen.append((lengths, out is not None))
+        return _embed_ragged(wave, lengths, out)
+
+    out = extract_corpus(lambda s, e: [_ragged_clip(i) for i in range(s, e)], 5, fn, (2, 3), "cpu", batch=2)
+    ref = torch.stack([_embed_one(torch.from_numpy(_ragged_clip(i))) for i in range(5)])
+    assert torch.equal(out, ref) and all(o for _, o in seen) and [len(l) for l, _ in seen] == [2, 2, 1]
+    extract_corpus(lambda s, e: _clips(s, e, 66), 3, fn, (2, 3), "cpu", batch=2)
+    assert seen[-1][0] is None
+    with pytest.raises(ValueError):
+        extract_corpus(lambda s, e: [_ragged_clip(i) for i in range(s, e)], 3, _embed, (2, 3), "cpu", batch=2)

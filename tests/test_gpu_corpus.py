@@ -61,3 +61,27 @@ def test_extract_corpus_hip_path_rccl(nccl_group, wavlm_sd, dtype):
         got = emb[sel].cpu().numpy()
         rel = np.linalg.norm(got - ref, axis=-1) / np.linalg.norm(ref, axis=-1)
         assert rel.max() <= 1e-4, rel.max()
+
+
+def test_extract_corpus_mixed_lengths_host_staged(nccl_group, wavlm_sd):
+    """a 600-clip corpus of MIXED lengths (0.5-3.2 s, every clip under the
+    160-frame attention split) from HOST memory through extract_corpus: ragged batches of 256 staged
+    by the double-buffered pinned H2D on the side stream, embedded into the shard buffer through
+    out=, the all-gather over RCCL -- bit-identical to embedding each clip alone."""
+    from ssr_amd import config as C, synth
+    from ssr_amd.corpus import extract_corpus, sse_embed_fn
+    from ssr_amd.model import SSEModel
+    spec = C.WAVLM_BASE
+    N = 600
+    idx = spec.default_layer_indices()
+    rng = np.random.default_rng(5)
+    lens = rng.integers(8000, 51000, size=N)
+    clips = [synth.synth_clips(1, int(n), seed=900 + i)[0] for i, n in enumerate(lens)]
+    m = SSEModel(spec, wavlm_sd, device="cuda:0", dtype="bf16")
+    emb = extract_corpus(lambda s, e: clips[s:e], N, sse_embed_fn(m, idx), (len(idx), spec.hidden),
+                         device="cuda:0", batch=256)
+    torch.cuda.synchronize()
+    assert emb.shape == (N, len(idx), spec.hidden) and torch.isfinite(emb).all()
+    for i in range(N):
+        one = m.embed(torch.from_numpy(clips[i]).cuda()[None], idx)
+        assert torch.equal(emb[i:i + 1], one), (i, int(lens[i]))

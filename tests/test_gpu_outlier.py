@@ -60,3 +60,23 @@ def test_whisper_outlier_weights(golden, dtype, tol, cos):
     ref = golden["whisper_emb"]
     print(dtype, "outlier Whisper rel-L2", _rel(got, ref).max(), "cos", _cos(got, ref).min())
     assert _rel(got, ref).max() <= tol and _cos(got, ref).min() >= cos
+
+
+def test_wavlm_outlier_bf16_residual_cost_measured(golden):
+    """the bf16 residual stream + folded LayerNorm (the production bf16 flow) and the
+    materialised flow (no_lnfold=1: LayerNorm kernels, fp32 residual) both measured against the
+    reference's outlier fixture every run, so the accuracy cost of the bf16 stream stays visible;
+    the production flow may not be worse than the fp32-residual one by more than the format's noise."""
+    from ssr_amd import _lib, config as C, synth
+    from ssr_amd.model import SSEModel
+    sd = synth.outlier_weights(synth.synth_wavlm_state_dict(C.WAVLM_BASE, seed=7))
+    m = SSEModel(C.WAVLM_BASE, sd, device="cuda:0", dtype="bf16")
+    clips = torch.from_numpy(synth.synth_clips(4, 48000, seed=1234)).cuda()
+    idx = [int(i) for i in golden["wavlm_layer_indices"]]
+    ref = golden["wavlm_emb"]
+    a = m.embed(clips, idx).cpu().numpy()
+    with _lib.option("no_lnfold", 1):
+        b = m.embed(clips, idx).cpu().numpy()
+    ea, eb = _rel(a, ref).max(), _rel(b, ref).max()
+    print("outlier bf16: bf16 residual + folded LN", ea, "| fp32 residual, materialised LN", eb)
+    assert ea <= 0.25 and eb <= 0.25 and ea <= 1.25 * eb + 0.02

@@ -88,3 +88,29 @@ def test_whisper_ragged_equals_per_clip(dtype):
     got = m.embed(wave, idx, lengths=lens)
     for i, c in enumerate(clips):
         assert torch.equal(got[i:i + 1], m.embed(torch.from_numpy(c).cuda()[None], idx)), i
+
+
+def test_wavlm_ragged_c_abi_clamps_out_of_range_lengths(wavlm_sd):
+    """the C-ABI clamps d_lengths on the device.  Called past the Python wrapper's checks
+    with a length beyond the row (treated as the row), one under the 400-sample receptive field and a
+    negative one (both pooled as zeros): no kernel reads outside its clip, every output is finite and
+    the in-range clips are untouched."""
+    import ctypes
+    from ssr_amd import _lib, config as C, synth
+    from ssr_amd.model import SSEModel
+    m = SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype="bf16")
+    L = 48000
+    clips = synth.synth_clips(4, L, seed=41)
+    wave = torch.from_numpy(clips).cuda()
+    lens = torch.tensor([L, 10 * L, 200, -5], dtype=torch.int32, device="cuda")
+    ids = torch.tensor([12, 6, 0], dtype=torch.int32)
+    out = torch.full((4, 3, 768), float("nan"), device="cuda")
+    ws = m.workspace(4, L)
+    rc = _lib.lib().sse_embed_ragged(m._h, wave.data_ptr(), lens.data_ptr(), 4, L, ids.data_ptr(), 3, out.data_ptr(),
+                                     ws.data_ptr(), ws.numel(), m._stream())
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    full = m.embed(wave[:2], [12, 6, 0])
+    assert torch.equal(out[0], full[0]) and torch.equal(out[1], full[1])
+    assert (out[2:] == 0).all()

@@ -139,7 +139,8 @@ def test_wavlm_large_matches_reference(dtype, tol):
 
 def test_bf16_lnfold_matches_materialised(wavlm_sd):
     """The bf16 post-LN path runs no LayerNorm kernel inside the layer loop: oproj / ffn2 write the
-    un-normalised sum (fp32 residual + bf16 GEMM operand) and per-256-column partial statistics;
+    un-normalised sum in bf16 (at once the next residual and the next GEMM's A operand; no fp32
+    stream) and per-256-column partial statistics of the rounded values;
     QKV / FFN1 apply the LayerNorm through folded weights (rstd (acc - mean acol) + b'), the next
     residual GEMM on its residual load, the pool on its loads.  Against the materialised flow
     (no_lnfold=1: LayerNorm kernels, bf16(LN(x)) operands): both are bf16 paths with different

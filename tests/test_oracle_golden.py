@@ -162,3 +162,22 @@ def test_oracles_vs_outlier_fixtures():
     got = WhisperOracle(spec, sdw).embed(wc[:1], [int(i) for i in g["whisper_layer_indices"]])
     ref = g["whisper_emb"][:1]
     assert (np.linalg.norm(got - ref, axis=-1) / np.linalg.norm(ref, axis=-1)).max() <= 1e-4
+
+
+def test_whisper_aten_restatement_matches_reference(golden_manifest):
+    """bench.py's Whisper cpu_baseline (oracle/whisper_aten.py: the reference's batch-1 loop on the
+    same ATen ops, encoder + 1-token decoder) reproduces the reference's own whisper_tiny fixture:
+    log-mel, encoder and decoder keys (observed bit-equal)."""
+    from oracle.whisper_aten import WhisperAten
+    from ssr_amd import config as C, synth
+    g = np.load(os.path.join(GOLDEN, "whisper_tiny.npz"))
+    man = golden_manifest["whisper_tiny"]
+    clips = [synth.synth_clips(1, int(16000 * d), seed=4321, first_clip=i)[0] for i, d in enumerate(man["durations_s"])]
+    o = WhisperAten(C.WHISPER_TINY_DEC, synth.synth_whisper_state_dict(C.WHISPER_TINY_DEC, seed=11))
+    ei = [int(i) for i in g["layer_indices"]]
+    di = [int(i) for i in g["decoder_indices"]]
+    for i, c in enumerate(clips):
+        assert np.abs(o.log_mel(c)[0].numpy() - g["mel"][i]).max() <= 1e-5
+        d = o.extract(c, ei, di)
+        assert _rel(np.stack([d[f"encoder_layer_{k}"] for k in ei]), g["emb"][i]).max() <= 1e-5
+        assert _rel(np.stack([d[f"decoder_layer_{k}"] for k in di]), g["dec_emb"][i]).max() <= 1e-5
