@@ -76,6 +76,9 @@ def parse():
     ap.add_argument("--corpus", type=int, default=0,
                     help="BASELINE configs[3] mode: embed a corpus of this many clips (e.g. 50000) sharded "
                          "across the ranks with corpus.extract_corpus (tail batch + one all-gather timed)")
+    ap.add_argument("--split", type=int, default=1,
+                    help="each step's batch split into this many sub-batches on their own HIP streams "
+                         "(SSEModel.embed_streams: one sub-batch's kernels fill CUs another leaves idle)")
     ap.add_argument("--corpus-resident", action="store_true",
                     help="--corpus with the clips already in HBM (default: staged from pinned host memory)")
     ap.add_argument("--ragged", action="store_true",
@@ -403,6 +406,8 @@ def main():
             torch.cuda.current_stream(dev).wait_event(ready[cur])
             model.embed(dbuf[cur], idx, out=out)
             done[cur].record()
+        elif a.split > 1:
+            model.embed_streams(clips, idx, out=out, n_streams=a.split)
         else:
             model.embed(clips, idx, out=out)
         if dist is not None:

@@ -201,6 +201,13 @@ int sse_profile_stop(sse_model* m);
 int sse_gemm(int dtype, const void* d_a, const void* d_b, const float* d_bias, const float* d_resid, float* d_cf,
              void* d_ct, int M, int N, int K, int act, const void* d_zero, void* stream);
 
+/* The folded-LayerNorm GEMM of the bf16 post-LN path (test hook): d_ct bf16 [M][N] =
+ * act(rstd_m * (A B^T)[m][n] + bias[n] - rstd_m mean_m acol[n]), (mean_m, rstd_m) combined from the
+ * per-256-column partials d_apart [M][3] (float2 (mean, M2)) with eps; K = 768 (three column tiles),
+ * act 0 none / 2 the bf16 path's GELU. */
+int sse_gemm_lnfold(const void* d_a, const void* d_b, const float* d_bias, const float* d_acol, const float* d_apart,
+                    void* d_ct, int M, int N, int K, int act, float eps, const void* d_zero, void* stream);
+
 /* MX-fp8 operands (SSE_DTYPE_FP8): e4m3 bytes [R][K] (K % 128 == 0) plus E8M0 scales, one per 32
  * consecutive K elements, in the tiled layout the GEMM stages (role 0: A operand / activations,
  * role 1: B operand / weights [N][K]); sse_mx_scale_bytes(R, K) bytes.  Quantisation: block

@@ -1625,6 +1625,16 @@ int sse_gemm(int dtype, const void* d_a, const void* d_b, const float* d_bias, c
                                  : launch_gemm_f32(g, AMODE_SEG, 1, (hipStream_t)stream);
 }
 
+int sse_gemm_lnfold(const void* d_a, const void* d_b, const float* d_bias, const float* d_acol, const float* d_apart,
+                    void* d_ct, int M, int N, int K, int act, float eps, const void* d_zero, void* stream) {
+  if (!d_a || !d_b || !d_acol || !d_apart || !d_ct || !d_zero || M <= 0 || N <= 0 || K != 768) return SSE_ERR_INVALID;
+  GemmArgs g{};
+  g.A = d_a; g.B = d_b; g.M = M; g.N = N; g.K = K; g.rows_per_seg = M; g.lda = K;
+  g.bias = d_bias; g.Ct = d_ct; g.ldc = N; g.act = act; g.zero = d_zero;
+  g.acol = d_acol; g.apart = (const float2*)d_apart; g.apart_nt = 3; g.ln_eps = eps;
+  return launch_gemm_bf16(g, AMODE_SEG, 1, (hipStream_t)stream);
+}
+
 size_t sse_mx_scale_bytes(int R, int K) {
   if (R <= 0 || K <= 0 || K % 128) return 0;
   return (size_t)mx_scale_bytes(R, K);

@@ -152,3 +152,46 @@ def test_gemm_persistent_agrees(M, N, K, epi):
     for o in outs[1:]:
         for x, y in zip(outs[0], o):
             assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("M,N,act", [(40704, 2560, 0), (40704, 3072, 2), (11448, 2560, 0)])
+def test_lnfold_gemm_position_invariant(M, N, act):
+    """The folded-LayerNorm GEMM (sse_gemm_lnfold, the bf16 post-LN path's QKV / FFN1): the persistent
+    kernel equals the non-persistent one bit for bit, and a row's result does not depend on its
+    position inside a 256-row tile (rows shifted by 128 and by whole tiles give the same bits).  Before
+    the library was built with -ffp-contract=off, instances of the LayerNorm-statistics expression
+    were contracted differently per tile position and 1-ulp bf16 flips appeared in ~4 % of clips."""
+    import ctypes
+    from ssr_amd import _lib
+    L = _lib.lib()
+    g = torch.Generator(device="cuda").manual_seed(3)
+    K = 768
+    a = (torch.randn(M, K, device="cuda", generator=g) * 2 + 0.3).bfloat16()
+    b = (torch.randn(N, K, device="cuda", generator=g) * 0.05).bfloat16()
+    bias = torch.randn(N, device="cuda", generator=g) * 0.1
+    acol = b.float().sum(1)
+    af = a.float().view(M, 3, 256)
+    mean = af.mean(2)
+    part = torch.stack([mean, ((af - mean[..., None]) ** 2).sum(2)], -1).contiguous()
+    z = torch.zeros(64, device="cuda")
+
+    def run(a_, part_, nonpersist=0):
+        ct = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+        with _lib.option("gemm_nonpersist", nonpersist):
+            rc = L.sse_gemm_lnfold(a_.data_ptr(), b.data_ptr(), bias.data_ptr(), acol.data_ptr(), part_.data_ptr(),
+                                   ct.data_ptr(), M, N, K, act, ctypes.c_float(1e-5), z.data_ptr(),
+                                   ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        assert rc == 0
+        return ct
+    p = run(a, part)
+    assert torch.equal(p, run(a, part, 1))
+    for sh in (128, 256 * 43 + 64):
+        q = torch.roll(run(torch.roll(a, sh, 0), torch.roll(part, sh, 0)), -sh, 0)
+        assert torch.equal(p, q), sh
+    # and against a torch fp32 restatement of the fold (bf16 output: within one bf16 ulp-scale)
+    rstd = 1.0 / torch.sqrt(part[..., 1].sum(1) / 768 + ((part[..., 0] - part[..., 0].mean(1, keepdim=True)) ** 2).sum(1)
+                            * 256 / 768 + 1e-5)
+    ref = rstd[:, None] * (a.float() @ b.float().T) + bias - (rstd * part[..., 0].mean(1))[:, None] * acol
+    if act == 2:
+        ref = torch.nn.functional.gelu(ref)
+    assert ((p.float() - ref).abs() <= 1e-2 * ref.abs() + 2e-2).all()

@@ -80,13 +80,15 @@ def test_fp32_do_normalize(wavlm_sd, wavlm_clips, golden_wavlm):
 
 def test_batch_invariance_full_batch(m16, m32):
     """Size-independent property at the bench shape (B=256): every clip's embedding in the
-    batch equals the embedding of that clip run alone, bit for bit (no cross-clip reduction)."""
+    batch equals the embedding of that clip run alone, bit for bit (no cross-clip reduction, and no
+    dependence on where a clip's rows fall inside the GEMM tiles: the library is built without
+    implicit FMA contraction, see the Makefile).  bf16: all 256 clips; fp32: every 8th."""
     from ssr_amd import synth
     clips = torch.from_numpy(synth.synth_clips(256, 48000, seed=99)).cuda()
     idx = [12, 11, 10, 6]
     for m in (m16, m32):
         full = m.embed(clips, idx)
-        for i in (0, 77, 255):
+        for i in (range(256) if m is m16 else range(0, 256, 8)):
             one = m.embed(clips[i:i + 1], idx)
             assert torch.equal(full[i:i + 1], one), (m.dtype, i)
         assert torch.isfinite(full).all()
