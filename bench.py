@@ -76,9 +76,6 @@ def parse():
     ap.add_argument("--corpus", type=int, default=0,
                     help="BASELINE configs[3] mode: embed a corpus of this many clips (e.g. 50000) sharded "
                          "across the ranks with corpus.extract_corpus (tail batch + one all-gather timed)")
-    ap.add_argument("--split", type=int, default=1,
-                    help="each step's batch split into this many sub-batches on their own HIP streams "
-                         "(SSEModel.embed_streams: one sub-batch's kernels fill CUs another leaves idle)")
     ap.add_argument("--corpus-resident", action="store_true",
                     help="--corpus with the clips already in HBM (default: staged from pinned host memory)")
     ap.add_argument("--ragged", action="store_true",
@@ -406,8 +403,6 @@ def main():
             torch.cuda.current_stream(dev).wait_event(ready[cur])
             model.embed(dbuf[cur], idx, out=out)
             done[cur].record()
-        elif a.split > 1:
-            model.embed_streams(clips, idx, out=out, n_streams=a.split)
         else:
             model.embed(clips, idx, out=out)
         if dist is not None:
@@ -427,6 +422,11 @@ def main():
     def timed(profile):
         """K steps between barriers + device syncs; with profile, HIP events around every launch."""
         if profile:
+            # per-launch timing runs single-stream: with the two-stream half-batch split (WavLM,
+            # split_forward in sse_model.hip) launches of the two halves overlap and each event pair
+            # would time a shared chip; the roofline is the kernels' own rate, alone on the chip
+            from ssr_amd import _lib
+            prev_split = _lib.lib().sse_set_option(b"no_split", 1)
             model.profile_start(max_launches=200 * max(a.steps, 1))
         if dist is not None:
             dist.barrier()
@@ -443,10 +443,11 @@ def main():
         if profile:
             recs = model.profile_read()
             model.profile_stop()
+            _lib.lib().sse_set_option(b"no_split", prev_split)
         return el, recs
 
     # value: an unperturbed timed region (per-launch event records add ~0.5 ms/step of launch
-    # gaps); roofline: a second timed region of the same K steps with the events
+    # gaps); roofline: a second timed region of the same K steps with the events (single-stream)
     elapsed, _ = timed(False)
     records, prof_elapsed = [], None
     if not a.no_profile:

@@ -81,28 +81,78 @@ def emulated_product(fn, x: torch.Tensor, w: torch.Tensor, fmt: str) -> torch.Te
     raise ValueError(fmt)
 
 
+_SDPA = F.scaled_dot_product_attention
+
+# pipeline stages a per-stage format assignment can name (the GEMM roles of the GPU path)
+STAGES = ("conv", "proj", "posconv", "qkv", "attn", "oproj", "ffn1", "ffn2")
+
+
+def stage_of(key: str) -> str | None:
+    """Weight key of the WavLM state dict -> pipeline stage."""
+    if key.startswith("feature_extractor.conv_layers.") and ".conv.weight" in key:
+        return None if key.startswith("feature_extractor.conv_layers.0.") else "conv"
+    if key == "feature_projection.projection.weight":
+        return "proj"
+    if key == "encoder.pos_conv_embed.conv.parametrizations.weight.original1":
+        return "posconv"
+    for frag, st in ((".q_proj.", "qkv"), (".k_proj.", "qkv"), (".v_proj.", "qkv"), ("gru_rel_pos_linear", "qkv"),
+                     (".out_proj.", "oproj"), ("intermediate_dense", "ffn1"), ("output_dense", "ffn2")):
+        if frag in key and key.endswith("weight"):
+            return st
+    return None
+
+
 class _Patch:
-    def __init__(self, fmt: str):
+    """fmt: one format for every GEMM (the historical mode), or a dict stage -> format (missing
+    stages stay exact fp32).  Stage of a call: looked up from the weight tensor's identity (``ids``);
+    the positional conv's weight is recomputed by weight norm every forward, so grouped convs are
+    the "posconv" stage; the attention core ("attn": Q.K^T and P.V operands) is emulated by patching
+    scaled_dot_product_attention."""
+
+    def __init__(self, fmt, ids: dict | None = None):
         self.fmt = fmt
+        self.ids = ids or {}
+
+    def _f(self, w, default_stage=None):
+        if isinstance(self.fmt, str):
+            return self.fmt
+        st = self.ids.get(id(w), default_stage)
+        return self.fmt.get(st, "fp32") if st else "fp32"
 
     def __enter__(self):
-        fmt = self.fmt
-
         def lin(x, w, b=None):
-            y = emulated_product(_LIN, x, w, fmt)
+            f = self._f(w)
+            y = _LIN(x, w) if f == "fp32" else emulated_product(_LIN, x, w, f)
             return y if b is None else y + b
 
         def conv(x, w, b=None, stride=1, padding=0, dilation=1, groups=1):
-            if groups != 1 or w.shape[1] == 1:      # positional conv / conv0: fp32 in every path
+            if w.shape[1] == 1:                      # conv0: fp32 in every path
                 return _CONV(x, w, b, stride, padding, dilation, groups)
-            y = emulated_product(lambda a, c: _CONV(a, c, None, stride, padding, dilation), x, w, fmt)
+            if groups != 1:                          # positional conv
+                f = "fp32" if isinstance(self.fmt, str) else self.fmt.get("posconv", "fp32")
+            else:
+                f = self._f(w)
+            if f == "fp32":
+                return _CONV(x, w, b, stride, padding, dilation, groups)
+            y = emulated_product(lambda a, c: _CONV(a, c, None, stride, padding, dilation, groups), x, w, f)
             return y if b is None else y + b[None, :, None]
 
-        F.linear, F.conv1d = lin, conv
+        def sdpa(q, k, v, attn_mask=None, dropout_p=0.0, is_causal=False, scale=None, **kw):
+            f = "fp32" if isinstance(self.fmt, str) else self.fmt.get("attn", "fp32")
+            if f == "fp32":
+                return _SDPA(q, k, v, attn_mask=attn_mask, dropout_p=dropout_p, is_causal=is_causal, scale=scale)
+            sc = (q.shape[-1] ** -0.5) if scale is None else scale
+            s_ = emulated_product(lambda a, c: a @ c.transpose(-2, -1), q, k, f) * sc
+            if attn_mask is not None:
+                s_ = s_ + attn_mask
+            p_ = torch.softmax(s_, dim=-1)
+            return emulated_product(lambda a, c: a @ c.transpose(-2, -1), p_, v.transpose(-2, -1).contiguous(), f)
+
+        F.linear, F.conv1d, F.scaled_dot_product_attention = lin, conv, sdpa
         return self
 
     def __exit__(self, *exc):
-        F.linear, F.conv1d = _LIN, _CONV
+        F.linear, F.conv1d, F.scaled_dot_product_attention = _LIN, _CONV, _SDPA
 
 
 def _rel_cos(got: np.ndarray, ref: np.ndarray):
@@ -111,9 +161,12 @@ def _rel_cos(got: np.ndarray, ref: np.ndarray):
     return rel, cos
 
 
-def emulate(spec, sd: dict, clips: np.ndarray, layer_indices, fmt: str) -> np.ndarray:
-    with torch.no_grad(), _Patch(fmt):
-        return WavLMAten(spec, sd).embed(clips, layer_indices)
+def emulate(spec, sd: dict, clips: np.ndarray, layer_indices, fmt) -> np.ndarray:
+    """fmt: a format name for every GEMM, or a dict stage -> format (others exact fp32)."""
+    o = WavLMAten(spec, sd)
+    ids = {id(v): stage_of(k) for k, v in o.w.items() if stage_of(k)}
+    with torch.no_grad(), _Patch(fmt, ids):
+        return o.embed(clips, layer_indices)
 
 
 def main() -> None:
@@ -122,6 +175,8 @@ def main() -> None:
     ap.add_argument("--formats", default="bf16,fp16,bf16x3,fp16x3")
     ap.add_argument("--threads", type=int, default=os.cpu_count())
     ap.add_argument("--out", default="")
+    ap.add_argument("--stages", action="store_true", help="per-stage sensitivity table (STAGES)")
+    ap.add_argument("--assign", action="append", default=[], help="stage=fmt,... assignment to evaluate")
     a = ap.parse_args()
     torch.set_num_threads(a.threads)
     from ssr_amd import config as C, synth
@@ -135,6 +190,23 @@ def main() -> None:
         clips = synth.synth_clips(16, 48000, seed=1234)[:4]
         idx, ref = [int(i) for i in g["layer_indices"]], g["emb_norm0"][:4]
     res = {}
+    if a.stages:
+        # per-stage sensitivity: each stage alone in the format (others exact fp32), then the
+        # assignment given by --assign (stage=fmt,...)
+        for fmt in a.formats.split(","):
+            for st in STAGES:
+                rel, cos = _rel_cos(emulate(C.WAVLM_BASE, sd, clips, idx, {st: fmt}), ref)
+                res[f"{st}:{fmt}"] = {"rel_l2_max": float(rel.max()), "cos_min": float(cos.min())}
+                print(st, fmt, json.dumps(res[f"{st}:{fmt}"]), flush=True)
+        for asg in a.assign:
+            d = dict(kv.split("=") for kv in asg.split(","))
+            rel, cos = _rel_cos(emulate(C.WAVLM_BASE, sd, clips, idx, d), ref)
+            res["assign:" + asg] = {"rel_l2_max": float(rel.max()), "cos_min": float(cos.min())}
+            print("assign", asg, json.dumps(res["assign:" + asg]), flush=True)
+        if a.out:
+            with open(a.out, "w") as f:
+                json.dump({"fixture": a.fixture, "per_stage": res}, f, indent=1)
+        return
     for fmt in a.formats.split(","):
         rel, cos = _rel_cos(emulate(C.WAVLM_BASE, sd, clips, idx, fmt), ref)
         res[fmt] = {"rel_l2_max": float(rel.max()), "cos_min": float(cos.min())}

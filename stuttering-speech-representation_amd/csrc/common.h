@@ -156,6 +156,7 @@ enum {
   OPT_POSCONV_GEMM,     // 1: grouped GEMM for the bf16 positional conv
   OPT_NO_LNFOLD,        // 1: materialise post-LN LayerNorm outputs (bf16 WavLM-base)
   OPT_GEMM_MX_STAGED,   // 1: LDS-staged epilogue for every MX-fp8 GEMM
+  OPT_NO_SPLIT,         // 1: WavLM batches run as one stream (no two-stream half-batch split)
   OPT_COUNT
 };
 int sse_opt(int id);

@@ -33,7 +33,7 @@
 // A/B switches (common.h OPT_*), set only through sse_set_option
 static int g_opt[OPT_COUNT] = {0};
 static const char* const g_opt_name[OPT_COUNT] = {"gemm_cfg", "gemm_nonpersist", "gelu_exact", "conv0_valu",
-                                                   "posconv_gemm", "no_lnfold", "gemm_mx_staged"};
+                                                   "posconv_gemm", "no_lnfold", "gemm_mx_staged", "no_split"};
 int sse_opt(int id) { return __atomic_load_n(&g_opt[id], __ATOMIC_RELAXED); }
 
 namespace {
@@ -245,6 +245,13 @@ struct sse_model {
     std::vector<std::string> tag;
     std::vector<double> flops, bytes;
   } prof;
+
+  // two-stream half-batch split of WavLM embedding calls (split_forward): the second half runs on
+  // aux, forked from / joined to the caller's stream by events (created on first use, on the model's
+  // device); the mutex serialises the host-side fork / join of concurrent callers
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  std::mutex split_mu;
 
   template <typename X = void> const X* ptr(size_t off) const { return (const X*)(dmem + off); }
   bool bf() const { return dtype == SSE_DTYPE_BF16 || dtype == SSE_DTYPE_FP8; }   // bf16 activations
@@ -1285,10 +1292,71 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
   return 0;
 }
 
+// WavLM embedding batches of at least SPLIT_MIN clips run as two half-batches on two streams (the
+// caller's and the model's aux stream): clips are independent, so each half is an ordinary forward
+// over its own rows, workspace and output slots, and the two halves' kernels share the CUs -- the last
+// partial round of one half's GEMM tiles (447 tiles of the N = 768 residual GEMMs on 256 CUs at B = 256)
+// and its latency-bound small kernels are filled with the other half's work.  Bit-identical to the
+// single-stream call (every clip's result is independent of the batch it is in).  Not for hidden-state
+// calls, Whisper (1500-frame clips already give full rounds) or when OPT_NO_SPLIT is set.
+constexpr int SPLIT_MIN = 128;
+bool split_applies(const sse_model* m, int B, const Sink* sink) {
+  return m->cfg.kind == SSE_KIND_WAVLM && B >= SPLIT_MIN && !sse_opt(OPT_NO_SPLIT) && (!sink || !sink->hs);
+}
+size_t wavlm_ws(const sse_model* m, int B, int L) {
+  Plan p;
+  if (m->x3()) x3_plan(m, B, L, p); else wavlm_plan(m, B, L, p);
+  return p.total;
+}
+
+int forward_one(sse_model* m, const float* d_in, int B, int L, const Sink& sink, void* d_ws, hipStream_t s,
+                bool from_mel, const Sink* dsink, const int* lens);
+
+int split_forward(sse_model* m, const float* d_in, int B, int L, const Sink& sink, char* ws, hipStream_t s,
+                  const int* lens) {
+  std::lock_guard<std::mutex> lk(m->split_mu);
+  if (!m->aux) {
+    if (hipStreamCreateWithFlags(&m->aux, hipStreamNonBlocking) != hipSuccess) { m->aux = nullptr; return SSE_ERR_HIP; }
+    if (hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&m->ev_join, hipEventDisableTiming) != hipSuccess)
+      return SSE_ERR_HIP;
+  }
+  const int B1 = (B + 1) / 2, B2 = B - B1;
+  const size_t w1 = (wavlm_ws(m, B1, L) + 255) & ~(size_t)255;
+  Sink s1 = sink, s2 = sink;
+  s1.B = B1;
+  s2.B = B2;
+  s2.pooled = sink.pooled + (size_t)B1 * sink.n_ids * sink.H;
+  s2.s = m->aux;
+  if (hipEventRecord(m->ev_fork, s) != hipSuccess || hipStreamWaitEvent(m->aux, m->ev_fork, 0) != hipSuccess)
+    return SSE_ERR_HIP;
+  int rc = forward_one(m, d_in, B1, L, s1, ws, s, false, nullptr, lens);
+  const int rc2 = forward_one(m, d_in + (size_t)B1 * L, B2, L, s2, ws + w1, m->aux, false, nullptr,
+                              lens ? lens + B1 : nullptr);
+  // the join is recorded whatever happened, so the caller's stream never runs ahead of aux work
+  if (hipEventRecord(m->ev_join, m->aux) != hipSuccess || hipStreamWaitEvent(s, m->ev_join, 0) != hipSuccess)
+    return SSE_ERR_HIP;
+  return rc ? rc : rc2;
+}
+
 int forward(sse_model* m, const float* d_in, int B, int L, const Sink& sink, void* d_ws, size_t ws_bytes,
             hipStream_t s, bool from_mel = false, const Sink* dsink = nullptr, const int* lens = nullptr) {
   if (!m || !d_in || B <= 0 || L <= 0) return SSE_ERR_INVALID;
   if (ws_bytes < sse_workspace_bytes(m, B, L)) return SSE_ERR_WORKSPACE;
+  if (!from_mel && !dsink && split_applies(m, B, &sink)) {
+    if (wavlm_frames(m->cfg, L, nullptr) <= 0) return SSE_ERR_INVALID;
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) return SSE_ERR_HIP;
+    if (dev != m->device && hipSetDevice(m->device) != hipSuccess) return SSE_ERR_HIP;
+    const int rc = split_forward(m, d_in, B, L, sink, (char*)d_ws, s, lens);
+    if (dev != m->device) (void)hipSetDevice(dev);
+    return rc;
+  }
+  return forward_one(m, d_in, B, L, sink, d_ws, s, from_mel, dsink, lens);
+}
+
+int forward_one(sse_model* m, const float* d_in, int B, int L, const Sink& sink, void* d_ws, hipStream_t s,
+                bool from_mel, const Sink* dsink, const int* lens) {
   if (m->cfg.kind == SSE_KIND_WAVLM && wavlm_frames(m->cfg, L, nullptr) <= 0) return SSE_ERR_INVALID;
   int dev = -1;
   if (hipGetDevice(&dev) != hipSuccess) return SSE_ERR_HIP;
@@ -1418,6 +1486,9 @@ int sse_model_create(const sse_cfg* cfg, const float* host_weights, size_t nbyte
 void sse_model_destroy(sse_model* m) {
   if (!m) return;
   for (auto e : m->prof.ev) (void)hipEventDestroy(e);
+  if (m->ev_fork) (void)hipEventDestroy(m->ev_fork);
+  if (m->ev_join) (void)hipEventDestroy(m->ev_join);
+  if (m->aux) (void)hipStreamDestroy(m->aux);
   if (m->dmem) {
     int prev = -1;
     (void)hipGetDevice(&prev);
@@ -1438,7 +1509,13 @@ size_t sse_workspace_bytes(const sse_model* m, int B, int L) {
   Plan p;
   if (m->cfg.kind == SSE_KIND_WAVLM) {
     if (wavlm_frames(m->cfg, L, nullptr) <= 0) return 0;
-    if (m->x3()) x3_plan(m, B, L, p); else wavlm_plan(m, B, L, p);
+    const size_t one = wavlm_ws(m, B, L);
+    if (split_applies(m, B, nullptr)) {   // two half-batch workspaces (split_forward); also covers one stream
+      const int B1 = (B + 1) / 2;
+      const size_t two = ((wavlm_ws(m, B1, L) + 255) & ~(size_t)255) + wavlm_ws(m, B - B1, L);
+      return two > one ? two : one;
+    }
+    return one;
   } else {
     whisper_plan(m, B, p);
   }
@@ -1548,7 +1625,9 @@ int sse_profile_read(sse_model* m, int cap, char* tags, float* ms, double* flops
   if (!m || cap < 0) return SSE_ERR_INVALID;
   auto& P = m->prof;
   const int n = (int)P.tag.size();
-  if (n > 0 && hipEventSynchronize(P.ev[2 * n - 1]) != hipSuccess) return SSE_ERR_HIP;
+  // launches may sit on two streams (split_forward): wait for every recorded end event
+  for (int i = 0; i < n; ++i)
+    if (hipEventSynchronize(P.ev[2 * i + 1]) != hipSuccess) return SSE_ERR_HIP;
   for (int i = 0; i < n && i < cap; ++i) {
     float t = 0.f;
     if (hipEventElapsedTime(&t, P.ev[2 * i], P.ev[2 * i + 1]) != hipSuccess) return SSE_ERR_HIP;

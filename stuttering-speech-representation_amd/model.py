@@ -188,44 +188,6 @@ class SSEModel:
                    "sse_embed_ragged")
         return out
 
-    def embed_streams(self, wave: torch.Tensor, layer_indices, out: torch.Tensor | None = None,
-                      n_streams: int = 2) -> torch.Tensor:
-        """``embed`` with the batch split into ``n_streams`` contiguous sub-batches, each on its own
-        HIP stream with its own workspace, so one sub-batch's kernels fill the CUs another leaves idle
-        (the last round of a GEMM's tiles, the latency-bound small kernels).  Clips are independent:
-        the result equals ``embed`` of the whole batch.  The sub-streams start after the current
-        stream's prior work and the current stream waits for all of them."""
-        wave = self._check_wave(wave)
-        B, L = wave.shape
-        n = max(1, min(int(n_streams), B))
-        ids = [int(i) for i in layer_indices]
-        if out is None:
-            out = torch.empty((B, len(ids), self.spec.hidden), dtype=torch.float32, device=self.device)
-        if n == 1:
-            return self.embed(wave, ids, out=out)
-        if not hasattr(self, "_sub"):
-            self._sub = {}
-        cur = torch.cuda.current_stream(self.device)
-        start = torch.cuda.Event()
-        start.record(cur)
-        bounds = [(B * i) // n for i in range(n + 1)]
-        for i in range(n):
-            b0, b1 = bounds[i], bounds[i + 1]
-            st, ws = self._sub.get(i, (None, None))
-            need = _lib.lib().sse_workspace_bytes(self._h, int(b1 - b0), int(L))
-            if st is None:
-                st = torch.cuda.Stream(self.device)
-            if ws is None or ws.numel() < need:
-                ws = torch.empty(need, dtype=torch.uint8, device=self.device)
-            self._sub[i] = (st, ws)
-            st.wait_event(start)
-            with torch.cuda.stream(st):
-                self.embed(wave[b0:b1], ids, out=out[b0:b1], workspace=ws)
-            done = torch.cuda.Event()
-            done.record(st)
-            cur.wait_event(done)
-        return out
-
     def embed_clips(self, clips, layer_indices) -> torch.Tensor:
         """A list of 1-D clips of any lengths -> [N, len(layer_indices), H]: one ragged batch
         (zero-padded rows + lengths), every clip embedded at its own length."""

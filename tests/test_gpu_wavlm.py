@@ -276,3 +276,25 @@ def test_fp16x3_normalize_and_batch_invariance(wavlm_sd, golden_wavlm):
     full = m.embed(w, idx)
     for i in (0, 39):
         assert torch.equal(full[i:i + 1], m.embed(w[i:i + 1], idx))
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16x3"])
+def test_two_stream_split_equals_one_stream(wavlm_sd, dtype):
+    """Batches of >= 128 WavLM clips run as two half-batches on two streams (split_forward): bit-identical
+    to the single-stream call (no_split=1), for an odd batch and a ragged one, and the result is on the
+    caller's stream when the call returns (the join)."""
+    from ssr_amd import _lib, synth
+    from ssr_amd import config as C
+    from ssr_amd.model import SSEModel
+    m = SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype=dtype)
+    w = torch.from_numpy(synth.synth_clips(131, 48000, seed=17)).cuda()
+    idx = [12, 11, 10, 6, 0]
+    a = m.embed(w, idx)
+    with _lib.option("no_split", 1):
+        b = m.embed(w, idx)
+    assert torch.equal(a, b)
+    lens = [48000 - 97 * i for i in range(131)]
+    a = m.embed(w, idx, lengths=lens)
+    with _lib.option("no_split", 1):
+        b = m.embed(w, idx, lengths=lens)
+    assert torch.equal(a, b)
