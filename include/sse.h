@@ -42,8 +42,13 @@ enum sse_kind { SSE_KIND_WAVLM = 0, SSE_KIND_WHISPER = 1 };
  * operand is an fp16 subnormal), products hi*hi + lo*hi + hi*lo accumulated in fp32 (~22 significant
  * bits per operand) -- fp32-class embeddings (<= 1e-4 rel-L2, also with outlier-channel weights) at
  * ~1/3 of the bf16 GEMM rate, with conv0, the positional conv and the attention core in exact fp32.
- * Activations must stay inside the fp16 range (|x| < 65504); an overflow shows as non-finite output. */
-enum sse_dtype { SSE_DTYPE_F32 = 0, SSE_DTYPE_BF16 = 1, SSE_DTYPE_FP8 = 2, SSE_DTYPE_FP16X3 = 3 };
+ * Activations must stay inside the fp16 range (|x| < 65504): a non-finite output is reported by
+ * sse_check_range as SSE_ERR_RANGE. */
+/* SSE_DTYPE_FP16 (WavLM): the bf16 path's kernels and data flow with fp16 instead of bf16 activations,
+ * weights and MFMA operands -- the same matrix-core rate, 8 more mantissa bits per operand (emulated
+ * ideal-operand error on outlier-channel weights 0.017 rel-L2 vs 0.226 for bf16, oracle/emulate.py).
+ * Range as FP16X3 (|x| < 65504, checked by sse_check_range). */
+enum sse_dtype { SSE_DTYPE_F32 = 0, SSE_DTYPE_BF16 = 1, SSE_DTYPE_FP8 = 2, SSE_DTYPE_FP16X3 = 3, SSE_DTYPE_FP16 = 4 };
 enum sse_err {
   SSE_OK = 0,
   SSE_ERR_INVALID = -1,      /* bad argument / null pointer / bad layer index         */
@@ -51,7 +56,8 @@ enum sse_err {
   SSE_ERR_UNSUPPORTED = -3,  /* shape outside what the kernels implement              */
   SSE_ERR_WORKSPACE = -4,    /* ws_bytes < sse_workspace_bytes(...)                    */
   SSE_ERR_WEIGHTS = -5,      /* host weight blob size does not match the config        */
-  SSE_ERR_OOM = -6           /* device allocation failed (torch.OutOfMemoryError twin) */
+  SSE_ERR_OOM = -6,          /* device allocation failed (torch.OutOfMemoryError twin) */
+  SSE_ERR_RANGE = -7         /* an fp16-range path produced a non-finite output (sse_check_range) */
 };
 
 /* Model shape.  Field meaning follows the HF configs (WavLMConfig / WhisperConfig). */
@@ -90,7 +96,7 @@ typedef struct sse_model sse_model;
 size_t sse_weight_floats(const sse_cfg* cfg);
 
 /* Upload + repack weights (weight-norm folded, conv kernels reshaped to [out][k*in],
- * QKV concatenated, bf16 cast if dtype == SSE_DTYPE_BF16, relative-position bias table
+ * QKV concatenated, bf16 / fp16 cast for SSE_DTYPE_BF16 / SSE_DTYPE_FP16, relative-position bias table
  * precomputed).  Synchronous.  `host_weights` is fp32, `nbytes` = 4 * sse_weight_floats. */
 int sse_model_create(const sse_cfg* cfg, const float* host_weights, size_t nbytes,
                      int device, int dtype, sse_model** out);
@@ -128,6 +134,14 @@ int sse_embed(sse_model* m, const float* d_in, int B, int L, const int32_t* laye
 int sse_embed_ragged(sse_model* m, const float* d_in, const int32_t* d_lengths, int B, int L,
                      const int32_t* layer_ids, int n_layers, float* d_out, void* d_ws, size_t ws_bytes,
                      void* stream);
+
+/* Range check of the fp16-range dtypes (SSE_DTYPE_FP16, SSE_DTYPE_FP16X3): every sse_embed /
+ * sse_embed_ragged / sse_hidden_states call on such a model also scans the fp32 values it wrote and
+ * raises a device flag when one is non-finite (an fp16 activation overflowed: |x| >= 65504 somewhere
+ * in the forward).  sse_check_range synchronises `stream`, reads and clears the flag and returns
+ * SSE_ERR_RANGE if it was raised since the last check (0 otherwise; always 0 for other dtypes).  The
+ * flag is per handle: with concurrent streams, check after joining them. */
+int sse_check_range(sse_model* m, void* stream);
 
 /* Same forward, materialising every hidden state: d_hs [layers+1][B][T][hidden] fp32. */
 int sse_hidden_states(sse_model* m, const float* d_in, int B, int L, float* d_hs,

@@ -20,6 +20,9 @@ SSE_DTYPE_F32 = 0
 SSE_DTYPE_BF16 = 1
 SSE_DTYPE_FP8 = 2   # bf16 activations + MX-fp8 encoder-layer GEMMs (Whisper)
 SSE_DTYPE_FP16X3 = 3   # fp32 activations, split-fp16 (hi/lo) GEMMs: fp32-class results (WavLM-base)
+SSE_DTYPE_FP16 = 4   # the bf16 path with fp16 activations / weights / MFMA operands (WavLM-base)
+SSE_ERR_OOM = -6
+SSE_ERR_RANGE = -7   # an fp16-range call wrote a non-finite value (sse_check_range)
 
 EXPORTED = ("sse_weight_floats", "sse_model_create", "sse_model_destroy", "sse_output_frames",
             "sse_workspace_bytes", "sse_logmel_workspace_bytes", "sse_logmel", "sse_embed",
@@ -29,7 +32,7 @@ EXPORTED = ("sse_weight_floats", "sse_model_create", "sse_model_destroy", "sse_o
             "sse_whisper_decoder_hidden_states", "sse_mono", "sse_resample_length", "sse_resample_workspace_bytes",
             "sse_resample", "sse_augment", "sse_mx_scale_bytes", "sse_mx_scale_offset", "sse_mx_quantize",
             "sse_mx_quantize_host", "sse_gemm_mx", "sse_pitch_shift_workspace_bytes", "sse_pitch_shift",
-            "sse_set_option", "sse_get_option", "sse_embed_ragged", "sse_gemm_lnfold")
+            "sse_set_option", "sse_get_option", "sse_embed_ragged", "sse_gemm_lnfold", "sse_check_range")
 
 
 class SSEError(RuntimeError):
@@ -40,6 +43,11 @@ class SSEError(RuntimeError):
 
 class SSEOutOfMemoryError(SSEError, MemoryError):
     pass
+
+
+class SSERangeError(SSEError, OverflowError):
+    """An fp16-range dtype (fp16, fp16x3) produced a non-finite output: an activation left the fp16
+    range somewhere in the forward (sse_check_range)."""
 
 
 class sse_cfg(ctypes.Structure):
@@ -121,6 +129,8 @@ def lib() -> ctypes.CDLL:
     L.sse_embed.restype = i32
     L.sse_embed_ragged.argtypes = [vp, vp, vp, i32, i32, vp, i32, vp, vp, sz, vp]
     L.sse_embed_ragged.restype = i32
+    L.sse_check_range.argtypes = [vp, vp]
+    L.sse_check_range.restype = i32
     L.sse_hidden_states.argtypes = [vp, vp, i32, i32, vp, vp, sz, vp]
     L.sse_hidden_states.restype = i32
     L.sse_whisper_hidden_states_from_mel.argtypes = [vp, vp, i32, vp, vp, sz, vp]
@@ -193,8 +203,10 @@ def strerror(rc: int) -> str:
 def check(rc: int, what: str) -> None:
     if rc == 0:
         return
-    if rc == -6:
+    if rc == SSE_ERR_OOM:
         raise SSEOutOfMemoryError(rc, what)
+    if rc == SSE_ERR_RANGE:
+        raise SSERangeError(rc, what)
     raise SSEError(rc, what)
 
 

@@ -122,8 +122,48 @@ SSE_DEV f32x2 gelu_fp8out2(f32x2 x) {
 template <typename T> SSE_DEV T from_f32(float v);
 template <> SSE_DEV float from_f32<float>(float v) { return v; }
 template <> SSE_DEV bf16 from_f32<bf16>(float v) { return (bf16)v; }
+template <> SSE_DEV f16 from_f32<f16>(float v) { return (f16)v; }
 SSE_DEV float to_f32(float v) { return v; }
 SSE_DEV float to_f32(bf16 v) { return (float)v; }
+SSE_DEV float to_f32(f16 v) { return (float)v; }
+
+// 16-bit activation formats: bf16 (SSE_DTYPE_BF16 / FP8) and fp16 (SSE_DTYPE_FP16).  Four values of
+// either packed into 8 bytes and back; H16 = true selects fp16.
+template <bool H16> SSE_DEV uint2 pack_h4(const f32x4& v) {
+  if constexpr (H16) {
+    const f16x4 x = {(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+    return __builtin_bit_cast(uint2, x);
+  } else {
+    const bf16x4 x = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+    return __builtin_bit_cast(uint2, x);
+  }
+}
+template <bool H16> SSE_DEV f32x4 unpack_h4(uint2 u) {
+  if constexpr (H16) {
+    const f16x4 x = __builtin_bit_cast(f16x4, u);
+    return f32x4{(float)x[0], (float)x[1], (float)x[2], (float)x[3]};
+  } else {
+    const bf16x4 x = __builtin_bit_cast(bf16x4, u);
+    return f32x4{(float)x[0], (float)x[1], (float)x[2], (float)x[3]};
+  }
+}
+template <bool H16> SSE_DEV float round_h(float v) { return H16 ? (float)(f16)v : (float)(bf16)v; }
+// one 16-bit value in a bf16x8 / bf16x4 lane (the 16-bit vectors are bit containers for both formats)
+template <bool H16> SSE_DEV bf16 hbits(float v) { return H16 ? __builtin_bit_cast(bf16, (f16)v) : (bf16)v; }
+template <bool H16> SSE_DEV float hval(bf16 b) { return H16 ? (float)__builtin_bit_cast(f16, b) : (float)b; }
+// 16x16x32 MFMA on bf16 or fp16 operands held in bf16x8 containers
+template <bool H16> SSE_DEV f32x4 mfma_h(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  if constexpr (H16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// 8 fp32 -> 16 B of bf16 / fp16
+template <bool H16> SSE_DEV uint4 pack_h8(const f32x4& a, const f32x4& b) {
+  const uint2 x = pack_h4<H16>(a), y = pack_h4<H16>(b);
+  return make_uint4(x.x, x.y, y.x, y.y);
+}
+template <typename T> constexpr bool is_f16_v = __is_same(T, f16);
 
 SSE_DEV float wave_sum(float v) {
 #pragma unroll
@@ -223,6 +263,9 @@ struct GemmArgs {
   int f16;
   float alpha;
   int ct3;
+  // plain fp16 GEMM (SSE_DTYPE_FP16): A, B, Ct and resid_t are fp16 instead of bf16, the f16 MFMA, no
+  // scale; otherwise exactly the bf16 path (launch_gemm<f16> sets it)
+  int h16;
 };
 
 // (mean, rstd) of a row of 256 * NT values from its per-tile partials (mean_t, M2_t), Chan's pairwise
@@ -337,4 +380,12 @@ template <> inline int launch_gemm<bf16>(const GemmArgs& a, int amode, int group
 }
 template <> inline int launch_gemm<float>(const GemmArgs& a, int amode, int groups, hipStream_t s) {
   return launch_gemm_f32(a, amode, groups, s);
+}
+// fp16 operands: the 8-phase kernels only (N % 256 == 0, K % 64 == 0, SEG addressing); -3 otherwise
+template <> inline int launch_gemm<f16>(const GemmArgs& a, int amode, int groups, hipStream_t s) {
+  if (amode != AMODE_SEG || groups != 1 || a.f16 || a.ct3) return -3;
+  GemmArgs g = a;
+  g.h16 = 1;
+  g.alpha = 1.f;
+  return launch_gemm8_bf16(g, s);
 }

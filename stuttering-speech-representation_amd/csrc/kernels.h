@@ -48,7 +48,7 @@ int launch_mx_quantize(const float* x, int R, int K, int role, unsigned char* q,
 
 // kernels_posconv.hip: WavLM positional conv (bf16 path); -3 = shape not covered (use the GEMM)
 int launch_posconv_bf16(const bf16* xt, const bf16* W, const float* bias, float* x, int B, int T, int H, int G, int K,
-                        int pad, hipStream_t s);
+                        int pad, hipStream_t s, bool h16 = false);   // h16: xt / W are fp16
 
 // st: per-row (mean, rstd), or part: per-256-column partials [rows][nt] (ln_part_stats): each element
 // is LayerNorm'd with (w, b) before the mean.  tlen (ragged batches): the mean runs over each clip's
@@ -76,6 +76,7 @@ int launch_attention(const AttnArgs& a, int B, hipStream_t s);
 template <typename TE>
 int launch_xattn1(const TE* q, const TE* kv, int B, int T, int D, int nh, TE* out, hipStream_t s);
 int launch_bcast_rows(const float* v, int D, int B, float* out, hipStream_t s);
+int launch_finite_flag(const float* x, long long n, int* flag, hipStream_t s);   // sse_check_range
 template <typename TO, typename TI = float>
 int launch_cast(const TI* x, long long n, TO* y, hipStream_t s);
 

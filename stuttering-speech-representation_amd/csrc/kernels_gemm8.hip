@@ -1249,10 +1249,8 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
           const uint4 v = rvb[i][ni];
           const auto x = __builtin_amdgcn_permlane16_swap(v.x, v.z, false, false);
           const auto y = __builtin_amdgcn_permlane16_swap(v.y, v.w, false, false);
-          const bf16x4 x0 = __builtin_bit_cast(bf16x4, make_uint2(x[0], y[0]));
-          const bf16x4 x1 = __builtin_bit_cast(bf16x4, make_uint2(x[1], y[1]));
-          rv[i][ni][0] = f32x4{(float)x0[0], (float)x0[1], (float)x0[2], (float)x0[3]};
-          rv[i][ni][1] = f32x4{(float)x1[0], (float)x1[1], (float)x1[2], (float)x1[3]};
+          rv[i][ni][0] = unpack_h4<F16>(make_uint2(x[0], y[0]));   // bf16, or fp16 (h16 path)
+          rv[i][ni][1] = unpack_h4<F16>(make_uint2(x[1], y[1]));
         }
     }
   };
@@ -1291,9 +1289,9 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
           const f32x4 bvv = *(const f32x4*)(smem + c * 4);
           const f32x4 bv = has_bias ? bvv : f32x4{0.f, 0.f, 0.f, 0.f};
           f32x4 o = ((F16 ? acc[mi][ni][i][j] * g.alpha : acc[mi][ni][i][j]) + bv) + r;
-          if constexpr (RB) {   // bf16 output: the statistics describe the rounded values
+          if constexpr (RB) {   // 16-bit output: the statistics describe the rounded values
             #pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = (float)(bf16)o[e];
+            for (int e = 0; e < 4; ++e) o[e] = round_h<F16>(o[e]);
           }
           acc[mi][ni][i][j] = o;
           sum += (o[0] + o[1]) + (o[2] + o[3]);
@@ -1332,10 +1330,7 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
             *(f32x4*)(g.Cf + row + n0 + ni * 128 + wn * 32 + j * 16 + q * 4) = acc[mi][ni][i][j];
         }
         if (RB || g.Ct) {
-          const f32x4 o0 = acc[mi][ni][i][0], o1 = acc[mi][ni][i][1];
-          const bf16x4 x0 = {(bf16)o0[0], (bf16)o0[1], (bf16)o0[2], (bf16)o0[3]};
-          const bf16x4 x1 = {(bf16)o1[0], (bf16)o1[1], (bf16)o1[2], (bf16)o1[3]};
-          const uint2 X = __builtin_bit_cast(uint2, x0), Y = __builtin_bit_cast(uint2, x1);
+          const uint2 X = pack_h4<F16>(acc[mi][ni][i][0]), Y = pack_h4<F16>(acc[mi][ni][i][1]);
           const auto s0 = __builtin_amdgcn_permlane16_swap(X.x, Y.x, false, false);
           const auto s1 = __builtin_amdgcn_permlane16_swap(X.y, Y.y, false, false);
           if (ok) {
@@ -1389,7 +1384,23 @@ int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
     }
     if (a.ct3 ? (a.act != ACT_GELU || a.Cf) : (a.act != ACT_NONE || !a.Cf || a.Ct)) return -3;
   }
-  if (sse_opt(OPT_GEMM_NONPERSIST) && !a.resid_t && !a.f16) {
+  if (a.h16) {
+    // plain fp16 (SSE_DTYPE_FP16): the bf16 path's kernels with fp16 operands (F16 = true, alpha = 1,
+    // no split planes); the folded post-LN flow (fp16 residual stream) or non-residual persistent GEMMs
+    if (a.f16 || a.ct3 || a.resid || a.rstats || a.resid_rows || a.alpha != 1.f) return -3;
+    if (a.resid_t) {
+      if (!a.Ct || a.Cf) return -3;
+      if (a.rpart) {
+        if (a.opart) hipLaunchKernelGGL((gemm8r_kernel<true, true, true, true>), grid, dim3(512), 0, s, a);
+        else hipLaunchKernelGGL((gemm8r_kernel<true, false, true, true>), grid, dim3(512), 0, s, a);
+      } else {
+        if (a.opart) hipLaunchKernelGGL((gemm8r_kernel<false, true, true, true>), grid, dim3(512), 0, s, a);
+        else hipLaunchKernelGGL((gemm8r_kernel<false, false, true, true>), grid, dim3(512), 0, s, a);
+      }
+      return hipGetLastError() == hipSuccess ? 0 : -2;
+    }
+  }
+  if (sse_opt(OPT_GEMM_NONPERSIST) && !a.resid_t && !a.f16 && !a.h16) {
     hipLaunchKernelGGL((gemm8_kernel<0, false, false>), grid, dim3(512), 0, s, a);
   } else if (a.resid_t) {
     // bf16 residual stream (folded post-LN path): bf16 out only
@@ -1434,7 +1445,14 @@ int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
     };
     using F_ = std::false_type;
     using T_ = std::true_type;
-    if (a.f16) {   // split-fp16: ct3 + erf-GELU (conv layers, ffn1) or fp32 out (proj, qkv)
+    if (a.h16) {   // plain fp16: GELU_FAST (conv layers, ffn1; ACT_GELU under OPT_GELU_EXACT) or none
+      if (a.act == ACT_GELU_FAST)
+        go(std::integral_constant<int, ACT_GELU_FAST>{}, F_{}, T_{});
+      else if (a.act == ACT_GELU)
+        go(std::integral_constant<int, ACT_GELU>{}, F_{}, T_{});
+      else
+        go(std::integral_constant<int, ACT_NONE>{}, F_{}, T_{});
+    } else if (a.f16) {   // split-fp16: ct3 + erf-GELU (conv layers, ffn1) or fp32 out (proj, qkv)
       if (a.ct3)
         go(std::integral_constant<int, ACT_GELU>{}, T_{}, T_{});
       else

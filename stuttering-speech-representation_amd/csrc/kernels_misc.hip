@@ -224,9 +224,8 @@ __global__ __launch_bounds__(256) void conv0_apply_kernel(const float* __restric
           }
           const long long row = (long long)(t + 4 * f) * C;
           if constexpr (sizeof(TO) == 2) {
-            const bf16x8 o8 = {(bf16)o[0].x, (bf16)o[0].y, (bf16)o[1].x, (bf16)o[1].y,
-                               (bf16)o[2].x, (bf16)o[2].y, (bf16)o[3].x, (bf16)o[3].y};
-            *(bf16x8*)(ob + row) = o8;
+            *(uint4*)(ob + row) = pack_h8<is_f16_v<TO>>(f32x4{o[0].x, o[0].y, o[1].x, o[1].y},
+                                                         f32x4{o[2].x, o[2].y, o[3].x, o[3].y});
           } else {
             *(f32x4*)((float*)ob + row) = f32x4{o[0].x, o[0].y, o[1].x, o[1].y};
             *(f32x4*)((float*)ob + row + 4) = f32x4{o[2].x, o[2].y, o[3].x, o[3].y};
@@ -251,9 +250,8 @@ __global__ __launch_bounds__(256) void conv0_apply_kernel(const float* __restric
         }
       }
       if constexpr (sizeof(TO) == 2) {
-        const bf16x8 o8 = {(bf16)y[0].x, (bf16)y[0].y, (bf16)y[1].x, (bf16)y[1].y,
-                           (bf16)y[2].x, (bf16)y[2].y, (bf16)y[3].x, (bf16)y[3].y};
-        *(bf16x8*)(ob + (long long)t * C) = o8;
+        *(uint4*)(ob + (long long)t * C) = pack_h8<is_f16_v<TO>>(f32x4{y[0].x, y[0].y, y[1].x, y[1].y},
+                                                                   f32x4{y[2].x, y[2].y, y[3].x, y[3].y});
       } else {
         *(f32x4*)((float*)ob + (long long)t * C) = f32x4{y[0].x, y[0].y, y[1].x, y[1].y};
         *(f32x4*)((float*)ob + (long long)t * C + 4) = f32x4{y[2].x, y[2].y, y[3].x, y[3].y};
@@ -305,11 +303,12 @@ __global__ void conv0_wfrag_kernel(const float* __restrict__ w0, int C, bf16x8* 
 // Wave w computes channel blocks cb = w, w+4, ..., both 16-frame blocks of the chunk.
 constexpr int C0M_PAD = 16;              // bf16 per tile row of padding: row stride = 8 banks mod 64
 
+template <typename TO>   // bf16 or fp16 output (the products are split-bf16 either way)
 __global__ __launch_bounds__(256) void conv0_mfma_kernel(const float* __restrict__ x, int L,
                                                          const float* __restrict__ norm,
                                                          const bf16x8* __restrict__ wf, const float* __restrict__ b0,
                                                          int T0, const float2* __restrict__ ss,
-                                                         bf16* __restrict__ out) {
+                                                         TO* __restrict__ out) {
   constexpr int S0 = 5, C = 512, NCB = C / 16 / 4;
   __shared__ float xs[(C0M_T - 1) * S0 + K0 + 2];
   __shared__ __attribute__((aligned(16))) bf16 tile[C0M_T][C + C0M_PAD];
@@ -369,11 +368,11 @@ __global__ __launch_bounds__(256) void conv0_mfma_kernel(const float* __restrict
         const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[i], xf[fb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
         const f32x2 o0 = gelu_fast2(__builtin_elementwise_fma(f32x2{acc[0], acc[1]}, sc0[i], sh0[i]));
         const f32x2 o1 = gelu_fast2(__builtin_elementwise_fma(f32x2{acc[2], acc[3]}, sc1[i], sh1[i]));
-        *(bf16x4*)&tile[fb * 16 + r16][c] = bf16x4{(bf16)o0.x, (bf16)o0.y, (bf16)o1.x, (bf16)o1.y};
+        *(uint2*)&tile[fb * 16 + r16][c] = pack_h4<is_f16_v<TO>>(f32x4{o0.x, o0.y, o1.x, o1.y});
       }
     }
     __syncthreads();
-    bf16* ob = out + ((long long)b * T0 + t0) * C;
+    TO* ob = out + ((long long)b * T0 + t0) * C;
     for (int r = wv; r < nt; r += 4) *(uint4*)(ob + (long long)r * C + lane * 8) = *(const uint4*)&tile[r][lane * 8];
   }
 }
@@ -406,8 +405,8 @@ int launch_conv0_gn(const float* x, int B, int L, const float* norm, const float
     const int nchunk = (T0 + C0M_T - 1) / C0M_T;
     int G = (3 * cus[dev] + B - 1) / B;
     G = G < 1 ? 1 : (G > nchunk ? nchunk : G);
-    hipLaunchKernelGGL(conv0_mfma_kernel, dim3(G, B), dim3(256), 0, s, x, L, norm, (const bf16x8*)wf, b0, T0,
-                       (const float2*)ss, (bf16*)out);
+    hipLaunchKernelGGL(conv0_mfma_kernel<TO>, dim3(G, B), dim3(256), 0, s, x, L, norm, (const bf16x8*)wf, b0, T0,
+                       (const float2*)ss, out);
   } else if (sizeof(TO) == 2 && !gelu_exact_env())   // bf16 output: gelu_fast2 (common.h)
     hipLaunchKernelGGL((conv0_apply_kernel<TO, false, true>), grid, block, 0, s, x, L, norm, w0, b0, C, T0, ss, out);
   else
@@ -455,6 +454,13 @@ template int launch_conv0_gn<float>(const float*, int, int, const float*, const 
 template int launch_conv0_gn<bf16>(const float*, int, int, const float*, const float*, const float*, int, int,
                                    int, int, const float*, const float*, float, double*, float2*, bf16*,
                                    hipStream_t, const int*);
+template int launch_conv0_gn<f16>(const float*, int, int, const float*, const float*, const float*, int, int,
+                                  int, int, const float*, const float*, float, double*, float2*, f16*,
+                                  hipStream_t, const int*);
+template int launch_conv0_ln<f16>(const float*, int, int, const float*, const float*, const float*, int, int, int,
+                                  int, const float*, const float*, float, f16*, hipStream_t);
+template int launch_conv0_raw<f16>(const float*, int, int, const float*, const float*, const float*, int, int, int,
+                                   int, f16*, hipStream_t);
 
 // ---------------------------------------------------------------------------------------
 // LayerNorm over rows of H (H % 4 == 0, H <= 2048).  One wave per row, 4 rows per block;
@@ -463,6 +469,10 @@ template <typename TI> SSE_DEV f32x4 load4(const TI* p);
 template <> SSE_DEV f32x4 load4<float>(const float* p) { return *(const f32x4*)p; }
 template <> SSE_DEV f32x4 load4<bf16>(const bf16* p) {
   const bf16x4 v = *(const bf16x4*)p;
+  return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+template <> SSE_DEV f32x4 load4<f16>(const f16* p) {
+  const f16x4 v = *(const f16x4*)p;
   return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
 }
 // a split-fp16 value from its hi plane (p) and lo' plane (p + H): hi + lo' * 2^-11
@@ -550,8 +560,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TI* __restrict__ i
         mx_quant4(o, (unsigned char*)out_t + off, (unsigned char*)stats, row, c, H, lane);
       } else if (out_t) {
         if constexpr (sizeof(TO) == 2) {
-          bf16x4 ob = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
-          *(bf16x4*)(out_t + off) = ob;
+          *(uint2*)(out_t + off) = pack_h4<is_f16_v<TO>>(o);
         } else {
           *(f32x4*)(out_t + off) = o;
         }
@@ -564,7 +573,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TI* __restrict__ i
 // and the feature projection's LN): one 16-B load per lane per row, R rows per wave with every load
 // issued first (the one-row-per-wave kernel keeps only 1 KiB in flight per wave: ~2.4 TB/s on these
 // rows), DPP/permlane reductions for the R rows interleaved.  GELU: the bf16 path's gelu_fast2.
-template <int R>
+template <int R, bool H16 = false>   // H16: fp16 rows (SSE_DTYPE_FP16) in bf16x8 containers
 __global__ __launch_bounds__(256) void layernorm_bf16_rows_kernel(const bf16* __restrict__ in, const float* __restrict__ w,
                                                                   const float* __restrict__ bta, int rows, int H,
                                                                   float eps, int act, bf16* __restrict__ out) {
@@ -591,7 +600,7 @@ __global__ __launch_bounds__(256) void layernorm_bf16_rows_kernel(const bf16* __
     float sm = 0.f;
     #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      x[i][e] = (float)v[i][e];
+      x[i][e] = hval<H16>(v[i][e]);
       sm += x[i][e];
     }
     mean[i] = sm;
@@ -628,8 +637,7 @@ __global__ __launch_bounds__(256) void layernorm_bf16_rows_kernel(const bf16* __
       }
     }
     if (on && row < rows) {
-      const bf16x8 o8 = {(bf16)y[0], (bf16)y[1], (bf16)y[2], (bf16)y[3], (bf16)y[4], (bf16)y[5], (bf16)y[6], (bf16)y[7]};
-      *(bf16x8*)(out + row * H + lane * 8) = o8;
+      *(uint4*)(out + row * H + lane * 8) = pack_h8<H16>(f32x4{y[0], y[1], y[2], y[3]}, f32x4{y[4], y[5], y[6], y[7]});
     }
   }
 }
@@ -639,11 +647,12 @@ int launch_layernorm(const TI* in, const float* w, const float* b, int rows, int
                      float* out_f, TO* out_t, hipStream_t s, float2* stats) {
   if (H % 4 || H > 2048) return -3;
   if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2) {
+    static_assert(is_f16_v<TI> == is_f16_v<TO>, "16-bit LayerNorm: one format in and out");
     if (H % 8 == 0 && H <= 512 && !out_f && !stats && out_t) {
       constexpr int R = 4;
-      const int a2 = act == ACT_GELU && !gelu_exact_env() ? (int)ACT_GELU_FAST : act;   // bf16 output
-      hipLaunchKernelGGL((layernorm_bf16_rows_kernel<R>), dim3((rows + 4 * R - 1) / (4 * R)), dim3(256), 0, s,
-                         (const bf16*)in, w, b, rows, H, eps, a2, (bf16*)out_t);
+      const int a2 = act == ACT_GELU && !gelu_exact_env() ? (int)ACT_GELU_FAST : act;   // 16-bit output
+      hipLaunchKernelGGL((layernorm_bf16_rows_kernel<R, is_f16_v<TO>>), dim3((rows + 4 * R - 1) / (4 * R)), dim3(256), 0,
+                         s, (const bf16*)in, w, b, rows, H, eps, a2, (bf16*)out_t);
       return hipGetLastError() == hipSuccess ? 0 : -2;
     }
   }
@@ -694,6 +703,12 @@ template int launch_layernorm<bf16, bf16>(const bf16*, const float*, const float
                                           bf16*, hipStream_t, float2*);
 template int launch_layernorm<bf16, float>(const bf16*, const float*, const float*, int, int, float, int, float*,
                                            float*, hipStream_t, float2*);
+template int launch_layernorm<float, f16>(const float*, const float*, const float*, int, int, float, int,
+                                          float*, f16*, hipStream_t, float2*);
+template int launch_layernorm<f16, f16>(const f16*, const float*, const float*, int, int, float, int, float*,
+                                        f16*, hipStream_t, float2*);
+template int launch_layernorm<f16, float>(const f16*, const float*, const float*, int, int, float, int, float*,
+                                          float*, hipStream_t, float2*);
 
 // LayerNorm -> MX-fp8 GEMM operand (pre-LN Whisper, SSE_DTYPE_FP8).  Block = 64 consecutive rows
 // (4 waves x 16 rows, one row per wave at a time, the layernorm_kernel arithmetic), so the block
@@ -1016,6 +1031,8 @@ template int launch_pool_mean<float>(const float*, int, int, int, float*, long l
                                      const float*, const float*, const float2*, int, float, const int*);
 template int launch_pool_mean<bf16>(const bf16*, int, int, int, float*, long long, hipStream_t, const float2*,
                                     const float*, const float*, const float2*, int, float, const int*);
+template int launch_pool_mean<f16>(const f16*, int, int, int, float*, long long, hipStream_t, const float2*,
+                                   const float*, const float*, const float2*, int, float, const int*);
 
 // ---------------------------------------------------------------------------------------
 // Ragged batches: per-clip frame counts after conv0 and after the last conv layer (the same
@@ -1041,6 +1058,29 @@ int launch_clip_frames(const int* lens, int B, int L, ClipFrames cf, int* t0, in
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+// Range flag of the fp16-range dtypes (sse_check_range): *flag = 1 if any of x[0, n) is non-finite.
+// Grid-stride over 16-B groups; every thread that sees a non-finite value stores 1 (a plain vector
+// store: all writers write the same value).
+__global__ __launch_bounds__(256) void finite_flag_kernel(const float* __restrict__ x, long long n, int* flag) {
+  const long long n4 = n >> 2;
+  bool bad = false;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    const f32x4 v = *(const f32x4*)(x + 4 * i);
+    bad |= !(__builtin_isfinite(v[0]) && __builtin_isfinite(v[1]) && __builtin_isfinite(v[2]) &&
+             __builtin_isfinite(v[3]));
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) bad |= !__builtin_isfinite(x[4 * n4 + threadIdx.x]);
+  if (bad) *flag = 1;
+}
+
+int launch_finite_flag(const float* x, long long n, int* flag, hipStream_t s) {
+  if (n <= 0) return 0;
+  long long nb = ((n >> 2) + 255) / 256;
+  nb = nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
+  hipLaunchKernelGGL(finite_flag_kernel, dim3((unsigned)nb), dim3(256), 0, s, x, n, flag);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 template <typename TE>
 __global__ __launch_bounds__(256) void mask_rows_kernel(TE* __restrict__ x, int T, int H, const int* __restrict__ tlen) {
   const int b = blockIdx.y;
@@ -1057,6 +1097,7 @@ int launch_mask_rows(TE* x, int B, int T, int H, const int* tlen, hipStream_t s)
 }
 template int launch_mask_rows<float>(float*, int, int, int, const int*, hipStream_t);
 template int launch_mask_rows<bf16>(bf16*, int, int, int, const int*, hipStream_t);
+template int launch_mask_rows<f16>(f16*, int, int, int, const int*, hipStream_t);
 
 // ---------------------------------------------------------------------------------------
 // K5/K6/K11: attention, flash style.  Block = (64 queries, head, clip), 4 waves x 16 queries.
@@ -1106,9 +1147,10 @@ SSE_DEV float wavlm_gate(const TE* rp, float c) {
   return ga * (gb * c - 1.0f) + 2.0f;
 }
 
+template <bool H16 = false>   // H16: the 8 projections are fp16 (SSE_DTYPE_FP16) in a bf16x8 container
 SSE_DEV float wavlm_gate_v(const bf16x8& r, float c) {
-  const float ra = (float)r[0] + (float)r[1] + (float)r[2] + (float)r[3];
-  const float rb = (float)r[4] + (float)r[5] + (float)r[6] + (float)r[7];
+  const float ra = hval<H16>(r[0]) + hval<H16>(r[1]) + hval<H16>(r[2]) + hval<H16>(r[3]);
+  const float rb = hval<H16>(r[4]) + hval<H16>(r[5]) + hval<H16>(r[6]) + hval<H16>(r[7]);
   const float ga = 1.f / (1.f + expf(-ra)), gb = 1.f / (1.f + expf(-rb));
   return ga * (gb * c - 1.0f) + 2.0f;
 }
@@ -1341,7 +1383,7 @@ SSE_DEV bf16x8 v_frag_tr(const char* Vs, int k0, int d0, int g, int r16) {
   return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
-template <bool BIAS>
+template <bool BIAS, bool H16 = false>   // H16: fp16 q/k/v/gate and output (SSE_DTYPE_FP16)
 __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* gate = (float*)(smem + 2 * F2_BUF);       // [F2_Q]
@@ -1358,7 +1400,9 @@ __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
 
   if (BIAS) {
     if (tid < F2_Q)
-      gate[tid] = q0 + tid < T ? wavlm_gate(qkv + (long long)(q0 + tid) * LQ + 3 * H + 8 * h, a.gconst[h]) : 0.f;
+      gate[tid] = q0 + tid < T ? wavlm_gate_v<H16>(*(const bf16x8*)(qkv + (long long)(q0 + tid) * LQ + 3 * H + 8 * h),
+                                                   a.gconst[h])
+                               : 0.f;
     const float* rh = a.relb + (long long)h * (2 * a.maxd + 1) + a.maxd;
     for (int u = tid; u < 2 * Tk - 1; u += 256) {
       int d = u - (Tk - 1);
@@ -1434,8 +1478,8 @@ __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
       const bf16x8 k1 = *(const bf16x8*)(Ks + kr * 128 + (((g + 4) ^ ((kr >> 1) & 7)) * 16));
       #pragma unroll
       for (int qq = 0; qq < 2; ++qq) {
-        f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf[qq][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        sc[qq][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf[qq][1], acc, 0, 0, 0);
+        f32x4 acc = mfma_h<H16>(k0, qf[qq][0], f32x4{0.f, 0.f, 0.f, 0.f});
+        sc[qq][kb] = mfma_h<H16>(k1, qf[qq][1], acc);
       }
     }
     // online softmax in the log2 domain: v = s * scale * log2(e) (+ gate * log2(e) * bias), p = 2^(v - m)
@@ -1489,8 +1533,8 @@ __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
         const f32x2 d = v2[e] + mm;
         const f32x2 pv = {__builtin_amdgcn_exp2f(d.x), __builtin_amdgcn_exp2f(d.y)};
         l_run[qq] += pv;
-        pf[qq][e >> 2][(e & 3) * 2] = (bf16)pv.x;
-        pf[qq][e >> 2][(e & 3) * 2 + 1] = (bf16)pv.y;
+        pf[qq][e >> 2][(e & 3) * 2] = hbits<H16>(pv.x);
+        pf[qq][e >> 2][(e & 3) * 2 + 1] = hbits<H16>(pv.y);
       }
     }
     #pragma unroll
@@ -1499,7 +1543,7 @@ __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
       for (int db = 0; db < 4; ++db) {
         const bf16x8 vf = v_frag_tr(Vs, ks * 32, db * 16, g, r16);
         #pragma unroll
-        for (int qq = 0; qq < 2; ++qq) o[qq][db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qq][ks], o[qq][db], 0, 0, 0);
+        for (int qq = 0; qq < 2; ++qq) o[qq][db] = mfma_h<H16>(vf, pf[qq][ks], o[qq][db]);
       }
     if (kt + 1 < nkt) store_tile(cur ^ 1);         // buffer cur^1 was last read before the previous barrier
     __syncthreads();
@@ -1517,9 +1561,7 @@ __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
       bf16* orow = (bf16*)a.out + ((long long)b * TS + qi[qq]) * H + h * AT_HD;
       #pragma unroll
       for (int db = 0; db < 4; ++db) {
-        bf16x4 ov = {(bf16)(o[qq][db][0] * inv), (bf16)(o[qq][db][1] * inv), (bf16)(o[qq][db][2] * inv),
-                     (bf16)(o[qq][db][3] * inv)};
-        *(bf16x4*)(orow + db * 16 + 4 * g) = ov;
+        *(uint2*)(orow + db * 16 + 4 * g) = pack_h4<H16>(o[qq][db] * inv);
       }
     }
   }
@@ -1537,7 +1579,7 @@ __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
 // across lanes.  V's 16-B chunks are XOR-swizzled by 2 ((row >> 1) & 3): the 32 lanes of one LDS pass
 // read 8 rows x 32 B and every row pair lands on its own 8 banks of each half (the K swizzle,
 // (row >> 1) & 7, maps chunk pairs {c, c+1} onto each other and conflicts here).
-template <bool BIAS, int NKB, bool RAG>
+template <bool BIAS, int NKB, bool RAG, bool H16 = false>   // H16: fp16 operands / output (SSE_DTYPE_FP16)
 __global__ __launch_bounds__(32 * NKB, 3) void attention_full_kernel(AttnArgs a, int hpb) {
   constexpr int TP = NKB * 16;                                   // padded keys
   constexpr int QPW = 2;                                         // query blocks per wave (NKB is even)
@@ -1605,7 +1647,7 @@ __global__ __launch_bounds__(32 * NKB, 3) void attention_full_kernel(AttnArgs a,
         rbv = a.relb[(long long)h * (2 * a.maxd + 1) + a.maxd + d];
       }
       const float gc = a.gconst[h];
-      if (tid < TP) gate[tid] = tid < T ? wavlm_gate_v(greg, gc) : 0.f;
+      if (tid < TP) gate[tid] = tid < T ? wavlm_gate_v<H16>(greg, gc) : 0.f;
       if (tid < 2 * TP - 1) rb[tid] = rbv;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1623,7 +1665,7 @@ __global__ __launch_bounds__(32 * NKB, 3) void attention_full_kernel(AttnArgs a,
       #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const bf16x8 kf = *(const bf16x8*)(Ks + kb * 2048 + (ks ? koff1 : koff0));
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qq][ks], acc, 0, 0, 0);
+        acc = mfma_h<H16>(kf, qf[qq][ks], acc);
       }
       s[kb] = acc;
     }
@@ -1686,8 +1728,8 @@ __global__ __launch_bounds__(32 * NKB, 3) void attention_full_kernel(AttnArgs a,
       bf16x8 pf;
       #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        pf[r] = (bf16)s[2 * ks][r];
-        pf[4 + r] = (bf16)s[2 * ks + 1][r];
+        pf[r] = hbits<H16>(s[2 * ks][r]);
+        pf[4 + r] = hbits<H16>(s[2 * ks + 1][r]);
       }
       #pragma unroll
       for (int db = 0; db < 4; ++db)
@@ -1696,24 +1738,20 @@ __global__ __launch_bounds__(32 * NKB, 3) void attention_full_kernel(AttnArgs a,
         const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)va);
         const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(va + 2048));
         const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[db], 0, 0, 0);
+        o[db] = mfma_h<H16>(vf, pf, o[db]);
       }
     }
     if (qv) {
       const float inv = 1.0f / l;
       bf16* orow = (bf16*)a.out + ((long long)b * TS + qi) * H + h * AT_HD;
       #pragma unroll
-      for (int db = 0; db < 4; ++db) {
-        bf16x4 ov = {(bf16)(o[db][0] * inv), (bf16)(o[db][1] * inv), (bf16)(o[db][2] * inv),
-                     (bf16)(o[db][3] * inv)};
-        *(bf16x4*)(orow + db * 16 + 4 * g) = ov;
-      }
+      for (int db = 0; db < 4; ++db) *(uint2*)(orow + db * 16 + 4 * g) = pack_h4<H16>(o[db] * inv);
     }
     }
   }
 }
 
-template <bool BIAS, int NKB, bool RAG>
+template <bool BIAS, int NKB, bool RAG, bool H16>
 int launch_attention_full(const AttnArgs& a, int B, hipStream_t s) {
   constexpr int TP = NKB * 16;
   const size_t lds = (size_t)2 * TP * 128 + (size_t)TP * 4 + (size_t)2 * TP * 4;
@@ -1724,7 +1762,7 @@ int launch_attention_full(const AttnArgs& a, int B, hipStream_t s) {
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -2;
   if (!cus[dev]) {
     if (hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu[dev], attention_full_kernel<BIAS, NKB, RAG>, NT, lds) !=
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu[dev], attention_full_kernel<BIAS, NKB, RAG, H16>, NT, lds) !=
             hipSuccess)
       return -2;
     if (per_cu[dev] < 1) per_cu[dev] = 1;
@@ -1739,19 +1777,19 @@ int launch_attention_full(const AttnArgs& a, int B, hipStream_t s) {
     const double cost = (double)rounds * c + 1e-3 * c;
     if (cost < best) best = cost, hpb = c;
   }
-  hipLaunchKernelGGL((attention_full_kernel<BIAS, NKB, RAG>), dim3(a.nh / hpb, B), dim3(NT), lds, s, a, hpb);
+  hipLaunchKernelGGL((attention_full_kernel<BIAS, NKB, RAG, H16>), dim3(a.nh / hpb, B), dim3(NT), lds, s, a, hpb);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-template <bool BIAS, bool RAG>
+template <bool BIAS, bool RAG, bool H16>
 int dispatch_full(const AttnArgs& a, int B, hipStream_t s) {
   const int nkb = ((a.T + 31) / 32) * 2;
   switch (nkb) {
-    case 2: return launch_attention_full<BIAS, 2, RAG>(a, B, s);
-    case 4: return launch_attention_full<BIAS, 4, RAG>(a, B, s);
-    case 6: return launch_attention_full<BIAS, 6, RAG>(a, B, s);
-    case 8: return launch_attention_full<BIAS, 8, RAG>(a, B, s);
-    case 10: return launch_attention_full<BIAS, 10, RAG>(a, B, s);
+    case 2: return launch_attention_full<BIAS, 2, RAG, H16>(a, B, s);
+    case 4: return launch_attention_full<BIAS, 4, RAG, H16>(a, B, s);
+    case 6: return launch_attention_full<BIAS, 6, RAG, H16>(a, B, s);
+    case 8: return launch_attention_full<BIAS, 8, RAG, H16>(a, B, s);
+    case 10: return launch_attention_full<BIAS, 10, RAG, H16>(a, B, s);
     default: return -3;
   }
 }
@@ -1767,29 +1805,33 @@ int launch_attention(const AttnArgs& a, int B, hipStream_t s) {
   if (a.relb) lds += (size_t)(2 * nkt * AT_K) * 4;
   if (lds > 160 * 1024) return -3;
   if constexpr (BF) {   // fp32 (parity) path keeps the flash kernel: its full-row form spills
+    constexpr bool H = is_f16_v<T>;   // fp16 (SSE_DTYPE_FP16) or bf16 operands
     if (a.T <= 160) {   // <= 10 key blocks: the whole row in registers
-      if (a.relb) return a.tlen ? dispatch_full<true, true>(a, B, s) : dispatch_full<true, false>(a, B, s);
-      return a.tlen ? dispatch_full<false, true>(a, B, s) : dispatch_full<false, false>(a, B, s);
+      if (a.relb) return a.tlen ? dispatch_full<true, true, H>(a, B, s) : dispatch_full<true, false, H>(a, B, s);
+      return a.tlen ? dispatch_full<false, true, H>(a, B, s) : dispatch_full<false, false, H>(a, B, s);
     }
     const int Tk = ((a.T + F2_K - 1) / F2_K) * F2_K;
     const size_t lds2 = 2 * F2_BUF + F2_Q * 4 + (a.relb ? (size_t)2 * Tk * 4 : 0);
     if (lds2 > 160 * 1024) return -3;
     dim3 g2((a.T + F2_Q - 1) / F2_Q, a.nh, B);
     if (a.relb)
-      hipLaunchKernelGGL(attention_flash2_kernel<true>, g2, dim3(256), lds2, s, a);
+      hipLaunchKernelGGL((attention_flash2_kernel<true, H>), g2, dim3(256), lds2, s, a);
     else
-      hipLaunchKernelGGL(attention_flash2_kernel<false>, g2, dim3(256), lds2, s, a);
+      hipLaunchKernelGGL((attention_flash2_kernel<false, H>), g2, dim3(256), lds2, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
   }
-  dim3 grid((a.T + AT_Q - 1) / AT_Q, a.nh, B);
-  if (a.relb)
-    hipLaunchKernelGGL((attention_kernel<T, true>), grid, dim3(256), lds, s, a);
-  else
-    hipLaunchKernelGGL((attention_kernel<T, false>), grid, dim3(256), lds, s, a);
+  if constexpr (!is_f16_v<T>) {   // fp32 (and the bf16 grid's unused tail)
+    dim3 grid((a.T + AT_Q - 1) / AT_Q, a.nh, B);
+    if (a.relb)
+      hipLaunchKernelGGL((attention_kernel<T, true>), grid, dim3(256), lds, s, a);
+    else
+      hipLaunchKernelGGL((attention_kernel<T, false>), grid, dim3(256), lds, s, a);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 template int launch_attention<float>(const AttnArgs&, int, hipStream_t);
 template int launch_attention<bf16>(const AttnArgs&, int, hipStream_t);
+template int launch_attention<f16>(const AttnArgs&, int, hipStream_t);
 
 // ---------------------------------------------------------------------------------------
 // Whisper decoder cross-attention for ONE query token per clip (REF/whisper_embeddings_large.py
@@ -1875,3 +1917,5 @@ int launch_cast(const TI* x, long long n, TO* y, hipStream_t s) {
 template int launch_cast<float, float>(const float*, long long, float*, hipStream_t);
 template int launch_cast<bf16, float>(const float*, long long, bf16*, hipStream_t);
 template int launch_cast<float, bf16>(const bf16*, long long, float*, hipStream_t);
+template int launch_cast<f16, float>(const float*, long long, f16*, hipStream_t);
+template int launch_cast<float, f16>(const f16*, long long, float*, hipStream_t);

@@ -1,11 +1,11 @@
-// K4: WavLM positional conv embedding (HF/models/wavlm/modeling_wavlm.py:37-90), bf16 path:
+// K4: WavLM positional conv embedding (HF/models/wavlm/modeling_wavlm.py:37-90), bf16 / fp16 paths:
 //   x[b][t][g*cg + n] += gelu( bias + sum_{j<K} sum_{c<cg} W[g*cg + n][j*cg + c] * xt[b][t + j - pad][g*cg + c] )
 // (weight-norm folded, SamePad's dropped last frame = only t < T is produced).  As a GEMM per group
 // it is M = B*T rows, N = cg = 48, K = 128 taps x 48 = 6144: N is too narrow for the 256x256
 // kernels and the generic 128x48 tile re-reads the same 255-frame input window from L2 for
 // every 64-deep K step (540 TF/s).  Here a block owns one group of TWO clips:
 //   * the clips' zero-padded input windows (TP + K - 1 frames x cg channels, bf16) are staged in
-//     LDS once; A fragments are read from the window at frame t + j (the conv's sliding window is
+//     LDS once (clips over 256 frames: per 256-frame chunk, grid z); A fragments are read from the window at frame t + j (the conv's sliding window is
 //     just an address offset, no im2col),
 //   * the group's weights stream through a double-buffered LDS stage of 128 K (48 x 256 B rows,
 //     16-B chunks XOR-swizzled by row: conflict-free B fragment reads), register-staged (loads of
@@ -23,7 +23,7 @@ constexpr int PC_CG = 48;            // channels per group (WavLM: 768 / 16)
 constexpr int PC_KST = 128;          // K per weight stage
 constexpr int PC_STAGE = PC_CG * PC_KST * 2;   // 12 KiB
 
-template <int TP>
+template <int TP, bool H16 = false>   // H16: fp16 input window / weights (SSE_DTYPE_FP16) in bf16 containers
 __global__ __launch_bounds__(64 * (2 * TP / 64)) void posconv_kernel(const bf16* __restrict__ xt, const bf16* __restrict__ W,
                                                                     const float* __restrict__ bias, float* __restrict__ x,
                                                                     int B, int T, int H, int K, int pad) {
@@ -34,6 +34,7 @@ __global__ __launch_bounds__(64 * (2 * TP / 64)) void posconv_kernel(const bf16*
   char* win = smem;                               // [2][WF][cg] bf16
   char* wst = smem + ((2 * WF * PC_CG * 2 + 15) & ~15);   // [2][cg][PC_KST] bf16, swizzled
   const int grp = blockIdx.y, b0 = blockIdx.x * 2;
+  const int f0 = blockIdx.z * TP;                 // first output frame of this block (clips > 256 frames: chunks)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = lane >> 4, r16 = lane & 15;
@@ -66,7 +67,7 @@ __global__ __launch_bounds__(64 * (2 * TP / 64)) void posconv_kernel(const bf16*
     const int n16 = 2 * WF * (PC_CG / 8);
     for (int i = tid; i < n16; i += NT) {
       const int c = i / (WF * 6), r = i - c * WF * 6, f = r / 6, ch = r - f * 6;
-      const int tt = f - pad, b = b0 + c;
+      const int tt = f0 + f - pad, b = b0 + c;
       bf16x8 v = bf16x8{};
       if (b < B && tt >= 0 && tt < T) v = *(const bf16x8*)(xt + ((long long)b * T + tt) * H + grp * PC_CG + ch * 8);
       *(bf16x8*)(win + ((c * WF + f) * PC_CG + ch * 8) * 2) = v;
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(64 * (2 * TP / 64)) void posconv_kernel(const bf16*
       #pragma unroll
       for (int i = 0; i < 4; ++i)
         #pragma unroll
-        for (int j = 0; j < 3; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 3; ++j) acc[i][j] = mfma_h<H16>(bf[j], af[i], acc[i][j]);
       ch += 32;
       if (ch >= PC_CG) { ch -= PC_CG; ++tap; }
     }
@@ -116,7 +117,7 @@ __global__ __launch_bounds__(64 * (2 * TP / 64)) void posconv_kernel(const bf16*
   // ---- epilogue: lane holds C[t][n .. n+3], n = j*16 + 4q; x += gelu(acc + bias) ----
   #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int rb = wave * 4 + i, c = (rb * 16) / TP, t = rb * 16 - c * TP + r16, b = b0 + c;
+    const int rb = wave * 4 + i, c = (rb * 16) / TP, t = f0 + rb * 16 - c * TP + r16, b = b0 + c;
     if (b >= B || t >= T) continue;
     float* xr = x + ((long long)b * T + t) * H + grp * PC_CG;
     #pragma unroll
@@ -134,12 +135,17 @@ __global__ __launch_bounds__(64 * (2 * TP / 64)) void posconv_kernel(const bf16*
 
 template <int TP>
 int launch_tp(const bf16* xt, const bf16* W, const float* bias, float* x, int B, int T, int H, int G, int K, int pad,
-              hipStream_t s) {
+              hipStream_t s, bool h16) {
   const int WF = TP + K - 1;
   const size_t lds = ((size_t)(2 * WF * PC_CG * 2 + 15) & ~(size_t)15) + 2 * (size_t)PC_STAGE;
   if (lds > 160 * 1024) return -3;
   constexpr int NT = 64 * (2 * TP / 64);
-  hipLaunchKernelGGL((posconv_kernel<TP>), dim3((B + 1) / 2, G), dim3(NT), lds, s, xt, W, bias, x, B, T, H, K, pad);
+  if (h16)
+    hipLaunchKernelGGL((posconv_kernel<TP, true>), dim3((B + 1) / 2, G, (T + TP - 1) / TP), dim3(NT), lds, s, xt, W, bias,
+                       x, B, T, H, K, pad);
+  else
+    hipLaunchKernelGGL((posconv_kernel<TP>), dim3((B + 1) / 2, G, (T + TP - 1) / TP), dim3(NT), lds, s, xt, W, bias, x,
+                       B, T, H, K, pad);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -147,18 +153,20 @@ int launch_tp(const bf16* xt, const bf16* W, const float* bias, float* x, int B,
 
 // -3: shape outside this kernel (the caller falls back to the grouped GEMM)
 int launch_posconv_bf16(const bf16* xt, const bf16* W, const float* bias, float* x, int B, int T, int H, int G, int K,
-                        int pad, hipStream_t s) {
+                        int pad, hipStream_t s, bool h16) {
   if (H != G * PC_CG || (K * PC_CG) % PC_KST || T <= 0 || pad < 0 || pad >= K) return -3;
-  const int tp = ((T + 31) / 32) * 32;
-  switch (tp) {   // 2*TP rows per block, 4 row blocks per wave
-    case 32: return launch_tp<32>(xt, W, bias, x, B, T, H, G, K, pad, s);
-    case 64: return launch_tp<64>(xt, W, bias, x, B, T, H, G, K, pad, s);
-    case 96: return launch_tp<96>(xt, W, bias, x, B, T, H, G, K, pad, s);
-    case 128: return launch_tp<128>(xt, W, bias, x, B, T, H, G, K, pad, s);
-    case 160: return launch_tp<160>(xt, W, bias, x, B, T, H, G, K, pad, s);
-    case 192: return launch_tp<192>(xt, W, bias, x, B, T, H, G, K, pad, s);
-    case 224: return launch_tp<224>(xt, W, bias, x, B, T, H, G, K, pad, s);
-    case 256: return launch_tp<256>(xt, W, bias, x, B, T, H, G, K, pad, s);
+  // 2*TP rows per block, 4 row blocks per wave; clips longer than 256 frames in 256-frame chunks
+  // (blockIdx.z), each chunk's input window staged with its own pad-frame borders
+  const int tp = T > 256 ? 256 : ((T + 31) / 32) * 32;
+  switch (tp) {
+    case 32: return launch_tp<32>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
+    case 64: return launch_tp<64>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
+    case 96: return launch_tp<96>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
+    case 128: return launch_tp<128>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
+    case 160: return launch_tp<160>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
+    case 192: return launch_tp<192>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
+    case 224: return launch_tp<224>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
+    case 256: return launch_tp<256>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
     default: return -3;
   }
 }

@@ -162,10 +162,15 @@ struct Arena {
     alpha[off] = std::ldexp(1.f, -e);
     return off;
   }
-  size_t put_elem(const std::vector<float>& v, bool bf) {
-    if (!bf) return put(v.data(), v.size() * 4);
+  // kind 0: fp32, 1: bf16, 2: fp16 (SSE_DTYPE_FP16)
+  size_t put_elem(const std::vector<float>& v, int kind) {
+    if (!kind) return put(v.data(), v.size() * 4);
     std::vector<uint16_t> h(v.size());
-    for (size_t i = 0; i < v.size(); ++i) h[i] = f2bf_bits(v[i]);
+    if (kind == 2) {
+      for (size_t i = 0; i < v.size(); ++i) h[i] = __builtin_bit_cast(uint16_t, (f16)v[i]);
+    } else {
+      for (size_t i = 0; i < v.size(); ++i) h[i] = f2bf_bits(v[i]);
+    }
     return put(h.data(), h.size() * 2);
   }
   // MX-fp8 weight [N][K] (B layout): e4m3 bytes at the returned offset, scales at *scale_off
@@ -178,19 +183,22 @@ struct Arena {
   }
 };
 
-// LayerNorm folded into the GEMM that consumes its output: B' = W diag(lw) (bf16), acol[n] = sum_k
-// bf16(B'[n][k]) (the operand values the MFMAs multiply), bias'[n] = bias[n] + sum_k W[n][k] lb[k]
+// LayerNorm folded into the GEMM that consumes its output: B' = W diag(lw) (bf16, or fp16 when h16),
+// acol[n] = sum_k B'[n][k] of the rounded values (the operand values the MFMAs multiply),
+// bias'[n] = bias[n] + sum_k W[n][k] lb[k]
 void put_folded(Arena& ar, const float* W, const float* bias, int N, int K, const float* lw, const float* lb,
-                size_t* w_off, size_t* c_off, size_t* b_off) {
+                size_t* w_off, size_t* c_off, size_t* b_off, bool h16) {
   std::vector<uint16_t> wf((size_t)N * K);
   std::vector<float> cs(N), bf(N);
   for (int n = 0; n < N; ++n) {
     double c = 0.0, d = bias ? (double)bias[n] : 0.0;
     for (int k = 0; k < K; ++k) {
       const float w = W[(size_t)n * K + k];
-      const uint16_t h = f2bf_bits(w * lw[k]);
+      const float wl = w * lw[k];
+      const f16 hh = (f16)wl;
+      const uint16_t h = h16 ? __builtin_bit_cast(uint16_t, hh) : f2bf_bits(wl);
       wf[(size_t)n * K + k] = h;
-      c += (double)bf_bits2f(h);
+      c += h16 ? (double)(float)hh : (double)bf_bits2f(h);
       d += (double)w * (double)lb[k];
     }
     cs[n] = (float)c;
@@ -229,6 +237,7 @@ struct sse_model {
   size_t conv_w[8], conv_b[8], conv_ln_w[8], conv_ln_b[8];
   bool has_conv_b = false;
   size_t fp_ln_w, fp_ln_b, fp_w, fp_b, pos_w, pos_b, enc_ln_w, enc_ln_b, relb, zero;
+  size_t status = 0;   // device int: raised when an fp16-range call wrote a non-finite value (sse_check_range)
   // Whisper
   size_t c1_w, c1_b, c2_w, c2_b, positions;
   size_t dec_x0, dec_ln_w, dec_ln_b;   // decoder: embed_tokens[0] + embed_positions[0]; final LN
@@ -255,6 +264,9 @@ struct sse_model {
 
   template <typename X = void> const X* ptr(size_t off) const { return (const X*)(dmem + off); }
   bool bf() const { return dtype == SSE_DTYPE_BF16 || dtype == SSE_DTYPE_FP8; }   // bf16 activations
+  bool h16() const { return dtype == SSE_DTYPE_FP16; }   // fp16 activations and GEMM operands (WavLM)
+  bool half() const { return bf() || h16(); }          // 16-bit activations
+  int ekind() const { return h16() ? 2 : (bf() ? 1 : 0); }   // Arena::put_elem kind of GEMM weights
   bool x3() const { return dtype == SSE_DTYPE_FP16X3; }   // split-fp16 GEMMs, fp32 activations
   std::map<size_t, float> x3_alpha;   // split-fp16 weight offset -> epilogue scale (Arena::put_x3)
   float alpha(size_t off) const {
@@ -284,7 +296,7 @@ bool cfg_valid(const sse_cfg* c) {
 // Walk the canonical order; with a null blob only counts.
 int build_wavlm(sse_model* m, Blob& bl, Arena& ar) {
   const sse_cfg& c = m->cfg;
-  const bool BF = m->bf();
+  const int BF = m->ekind();   // weight element kind (fp32 / bf16 / fp16)
   const int H = c.hidden, F = c.ffn, nh = c.heads;
   int cin = 1;
   for (int i = 0; i < c.n_conv; ++i) {
@@ -352,7 +364,7 @@ int build_wavlm(sse_model* m, Blob& bl, Arena& ar) {
     }
     m->relb = ar.put_f32(tab.data(), tab.size());
   }
-  const bool fold = BF && !c.stable_layer_norm && H == 768;   // the GEMM epilogues combine 3 column-tile partials
+  const bool fold = m->half() && !c.stable_layer_norm && H == 768;   // the GEMM epilogues combine 3 column-tile partials
   const float *prev_l2w = nullptr, *prev_l2b = nullptr;
   for (int l = 0; l < c.layers; ++l) {
     const float *qw = bl.take((size_t)H * H), *qb = bl.take(H), *kw = bl.take((size_t)H * H), *kb = bl.take(H);
@@ -401,8 +413,9 @@ int build_wavlm(sse_model* m, Blob& bl, Arena& ar) {
     L.ln2_w = ar.put_f32(l2w, H);
     L.ln2_b = ar.put_f32(l2b, H);
     if (fold) {
-      if (l > 0) put_folded(ar, qkv.data(), qkvb.data(), ldq, H, prev_l2w, prev_l2b, &L.qkv_wf, &L.qkv_c, &L.qkv_bf);
-      put_folded(ar, f1w, f1b, F, H, l1w, l1b, &L.f1_wf, &L.f1_c, &L.f1_bf);
+      if (l > 0)
+        put_folded(ar, qkv.data(), qkvb.data(), ldq, H, prev_l2w, prev_l2b, &L.qkv_wf, &L.qkv_c, &L.qkv_bf, m->h16());
+      put_folded(ar, f1w, f1b, F, H, l1w, l1b, &L.f1_wf, &L.f1_c, &L.f1_bf, m->h16());
     }
     prev_l2w = l2w;
     prev_l2b = l2b;
@@ -597,7 +610,7 @@ struct WavlmWs {
 
 WavlmWs wavlm_plan(const sse_model* m, int B, int L, Plan& p) {
   const sse_cfg& c = m->cfg;
-  const size_t es = m->bf() ? 2 : 4;
+  const size_t es = m->half() ? 2 : 4;
   int Ts[8];
   const int T = wavlm_frames(c, L, Ts);
   const size_t M = (size_t)B * T;
@@ -820,7 +833,7 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     RC(prof(m, s, "gemm_conv:posconv", gflops(g, G), gbytes<T>(g, AMODE_CONV, G), [&] {
       if (!use_gemm) {
         const int rc = launch_posconv_bf16((const bf16*)xt, m->ptr<bf16>(m->pos_w), m->ptr<float>(m->pos_b), x, B, Tf, H,
-                                           G, K, K / 2, s);
+                                           G, K, K / 2, s, is_f16_v<T>);
         if (rc != -3) return rc;
       }
       return launch_gemm<T>(g, AMODE_CONV, G, s); }));
@@ -832,9 +845,9 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
   // positional conv): the residual GEMMs read and write it in place, both LayerNorms read bf16, the
   // pooled hidden states are taken from it (half the residual traffic of an fp32 stream)
   const bool pre16 = sizeof(T) == 2 && c.stable_layer_norm;
-  bf16* x16 = pre16 ? (bf16*)xt : nullptr;
+  T* x16 = pre16 ? xt : nullptr;
   if (pre16) {
-    RC((launch_cast<bf16, float>(x, (long long)M * H, x16, s)));
+    RC((launch_cast<T, float>(x, (long long)M * H, x16, s)));
     RC(sink.emit(0, x16));
   } else {
     RC(sink.emit(0, x));
@@ -861,8 +874,8 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     const LayerW& Lw = m->layers[l];
     const LayerW* Lp = l > 0 ? &m->layers[l - 1] : nullptr;
     if (pre16)
-      RC((launch_layernorm<bf16, T>(x16, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, ACT_NONE,
-                                    nullptr, xb, s)));
+      RC((launch_layernorm<T, T>(x16, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, ACT_NONE,
+                                 nullptr, xb, s)));
     else if (c.stable_layer_norm)
       RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, ACT_NONE,
                                      nullptr, xb, s)));
@@ -893,12 +906,12 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
       g.Ct = xs; g.opart = p1;
     }
     if (pre16) {
-      g.resid = nullptr; g.Cf = nullptr; g.resid_t = x16; g.Ct = x16;
+      g.resid = nullptr; g.Cf = nullptr; g.resid_t = (const bf16*)x16; g.Ct = x16;
     }
     RC(prof(m, s, "gemm:oproj", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     if (pre16) {
-      RC((launch_layernorm<bf16, T>(x16, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, H, eps, ACT_NONE,
-                                    nullptr, xb, s)));
+      RC((launch_layernorm<T, T>(x16, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, H, eps, ACT_NONE,
+                                 nullptr, xb, s)));
     } else if (!lnfold) {
       if (!c.stable_layer_norm)
         RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, ACT_NONE, x,
@@ -924,7 +937,7 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
       g.Ct = xb; g.opart = p2;
     }
     if (pre16) {
-      g.resid = nullptr; g.Cf = nullptr; g.resid_t = x16; g.Ct = x16;
+      g.resid = nullptr; g.Cf = nullptr; g.resid_t = (const bf16*)x16; g.Ct = x16;
     }
     RC(prof(m, s, "gemm:ffn2", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     if (pre16) {
@@ -942,8 +955,8 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     if (l + 1 < c.layers || !c.stable_layer_norm) RC(sink.emit(l + 1, x));
   }
   if (pre16) {
-    RC((launch_layernorm<bf16, T>(x16, m->ptr<float>(m->enc_ln_w), m->ptr<float>(m->enc_ln_b), M, H, eps, ACT_NONE,
-                                  x, xb, s)));
+    RC((launch_layernorm<T, T>(x16, m->ptr<float>(m->enc_ln_w), m->ptr<float>(m->enc_ln_b), M, H, eps, ACT_NONE,
+                               x, xb, s)));
     RC(sink.emit(c.layers, x));
   } else if (c.stable_layer_norm) {
     RC((launch_layernorm<float, T>(x, m->ptr<float>(m->enc_ln_w), m->ptr<float>(m->enc_ln_b), M, H, eps, ACT_NONE,
@@ -1339,8 +1352,23 @@ int split_forward(sse_model* m, const float* d_in, int B, int L, const Sink& sin
   return rc ? rc : rc2;
 }
 
+int forward_any(sse_model* m, const float* d_in, int B, int L, const Sink& sink, void* d_ws, size_t ws_bytes,
+                hipStream_t s, bool from_mel, const Sink* dsink, const int* lens);
+
+// fp16-range dtypes: every value the call wrote is scanned and the handle's range flag raised on a
+// non-finite one (sse_check_range reports it)
 int forward(sse_model* m, const float* d_in, int B, int L, const Sink& sink, void* d_ws, size_t ws_bytes,
             hipStream_t s, bool from_mel = false, const Sink* dsink = nullptr, const int* lens = nullptr) {
+  const int rc = forward_any(m, d_in, B, L, sink, d_ws, ws_bytes, s, from_mel, dsink, lens);
+  if (rc || !(m->h16() || m->x3())) return rc;
+  int* flag = (int*)(m->dmem + m->status);
+  if (sink.pooled) RC(launch_finite_flag(sink.pooled, (long long)B * sink.n_ids * sink.H, flag, s));
+  if (sink.hs) RC(launch_finite_flag(sink.hs, (long long)(m->cfg.layers + 1) * B * sink.T * sink.H, flag, s));
+  return 0;
+}
+
+int forward_any(sse_model* m, const float* d_in, int B, int L, const Sink& sink, void* d_ws, size_t ws_bytes,
+                hipStream_t s, bool from_mel, const Sink* dsink, const int* lens) {
   if (!m || !d_in || B <= 0 || L <= 0) return SSE_ERR_INVALID;
   if (ws_bytes < sse_workspace_bytes(m, B, L)) return SSE_ERR_WORKSPACE;
   if (!from_mel && !dsink && split_applies(m, B, &sink)) {
@@ -1365,8 +1393,9 @@ int forward_one(sse_model* m, const float* d_in, int B, int L, const Sink& sink,
   if (m->cfg.kind == SSE_KIND_WAVLM && m->x3())
     rc = wavlm_forward_x3(m, d_in, B, L, sink, (char*)d_ws, s, lens);
   else if (m->cfg.kind == SSE_KIND_WAVLM)
-    rc = m->bf() ? wavlm_forward<bf16>(m, d_in, B, L, sink, (char*)d_ws, s, lens)
-                 : wavlm_forward<float>(m, d_in, B, L, sink, (char*)d_ws, s, lens);
+    rc = m->bf()    ? wavlm_forward<bf16>(m, d_in, B, L, sink, (char*)d_ws, s, lens)
+         : m->h16() ? wavlm_forward<f16>(m, d_in, B, L, sink, (char*)d_ws, s, lens)
+                    : wavlm_forward<float>(m, d_in, B, L, sink, (char*)d_ws, s, lens);
   else
     rc = m->bf() ? whisper_forward<bf16>(m, d_in, B, L, sink, (char*)d_ws, s, from_mel ? d_in : nullptr, dsink, lens)
                  : whisper_forward<float>(m, d_in, B, L, sink, (char*)d_ws, s, from_mel ? d_in : nullptr, dsink, lens);
@@ -1406,6 +1435,7 @@ const char* sse_strerror(int err) {
     case SSE_ERR_WORKSPACE: return "workspace too small";
     case SSE_ERR_WEIGHTS: return "weight blob size does not match the config";
     case SSE_ERR_OOM: return "HIP out of memory";
+    case SSE_ERR_RANGE: return "non-finite output: an fp16 activation overflowed (|x| >= 65504)";
     default: return "unknown error";
   }
 }
@@ -1442,8 +1472,14 @@ size_t sse_weight_floats(const sse_cfg* cfg) {
 int sse_model_create(const sse_cfg* cfg, const float* host_weights, size_t nbytes, int device, int dtype,
                      sse_model** out) {
   if (!out || !host_weights || !cfg_valid(cfg) ||
-      (dtype != SSE_DTYPE_F32 && dtype != SSE_DTYPE_BF16 && dtype != SSE_DTYPE_FP8 && dtype != SSE_DTYPE_FP16X3))
+      (dtype != SSE_DTYPE_F32 && dtype != SSE_DTYPE_BF16 && dtype != SSE_DTYPE_FP8 && dtype != SSE_DTYPE_FP16X3 &&
+       dtype != SSE_DTYPE_FP16))
     return SSE_ERR_INVALID;
+  // fp16: WavLM whose every GEMM fits the 8-phase kernels and whose positional conv has 48-channel
+  // groups (the dedicated kernel; WavLM-base) -- the grouped-GEMM fallback has no fp16 form
+  if (dtype == SSE_DTYPE_FP16 &&
+      (cfg->kind != SSE_KIND_WAVLM || cfg->hidden % 256 || cfg->ffn % 256 || cfg->hidden / cfg->pos_groups != 48))
+    return SSE_ERR_UNSUPPORTED;
   // split-fp16: WavLM "group" frontend + post-LN encoder (WavLM-base); every GEMM N % 256 == 0
   if (dtype == SSE_DTYPE_FP16X3 &&
       (cfg->kind != SSE_KIND_WAVLM || cfg->feat_norm_layer || cfg->stable_layer_norm || cfg->hidden % 256 ||
@@ -1465,6 +1501,7 @@ int sse_model_create(const sse_cfg* cfg, const float* host_weights, size_t nbyte
   const int rc = cfg->kind == SSE_KIND_WAVLM ? build_wavlm(m, bl, ar) : build_whisper(m, bl, ar);
   if (rc != SSE_OK || bl.off != need) { delete m; return SSE_ERR_WEIGHTS; }
   m->zero = ar.put(nullptr, 256);
+  m->status = ar.put(nullptr, 256);
   m->x3_alpha = ar.alpha;
   int prev = -1;
   if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) { delete m; return SSE_ERR_HIP; }
@@ -1528,6 +1565,21 @@ int sse_logmel(const float* d_wave, int B, int L, int n_mels, float* d_mel, void
                void* stream) {
   if (!d_wave || !d_mel || !d_ws) return SSE_ERR_INVALID;
   return launch_logmel<float>(d_wave, B, L, n_mels, d_mel, (float*)nullptr, d_ws, ws_bytes, (hipStream_t)stream);
+}
+
+int sse_check_range(sse_model* m, void* stream) {
+  if (!m) return SSE_ERR_INVALID;
+  if (!(m->h16() || m->x3())) return SSE_OK;
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(m->device) != hipSuccess) return SSE_ERR_HIP;
+  int v = 0;
+  int* flag = (int*)(m->dmem + m->status);
+  bool ok = hipStreamSynchronize((hipStream_t)stream) == hipSuccess &&
+            hipMemcpy(&v, flag, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess;
+  if (ok && v) ok = hipMemset(flag, 0, sizeof(int)) == hipSuccess;
+  (void)hipSetDevice(prev);
+  if (!ok) return SSE_ERR_HIP;
+  return v ? SSE_ERR_RANGE : SSE_OK;
 }
 
 int sse_embed(sse_model* m, const float* d_in, int B, int L, const int32_t* layer_ids, int n_layers, float* d_out,

@@ -20,7 +20,10 @@ from .config import WavLMSpec, WhisperSpec, param_specs
 
 DTYPES = {"fp32": _lib.SSE_DTYPE_F32, "float32": _lib.SSE_DTYPE_F32, "f32": _lib.SSE_DTYPE_F32,
           "bf16": _lib.SSE_DTYPE_BF16, "bfloat16": _lib.SSE_DTYPE_BF16,
-          "fp8": _lib.SSE_DTYPE_FP8, "mxfp8": _lib.SSE_DTYPE_FP8, "fp16x3": _lib.SSE_DTYPE_FP16X3}
+          "fp8": _lib.SSE_DTYPE_FP8, "mxfp8": _lib.SSE_DTYPE_FP8, "fp16x3": _lib.SSE_DTYPE_FP16X3,
+          "fp16": _lib.SSE_DTYPE_FP16, "float16": _lib.SSE_DTYPE_FP16}
+# dtypes whose activations live in the fp16 range: their calls are range-checked (sse_check_range)
+FP16_RANGE = ("fp16", "float16", "fp16x3")
 
 
 def _as_numpy(v) -> np.ndarray:
@@ -64,9 +67,15 @@ class SSEModel:
     """One model on one GPU.  ``dtype``: "bf16" (throughput path), "fp32" (parity path), "fp16x3"
     (WavLM-base: fp32 activations, split-fp16 GEMMs -- fp32-class parity at ~3x the fp32 path's
     throughput) or "fp8" (Whisper only: bf16 activations, MX-fp8 QKV / fc1 / fc2 GEMMs, BASELINE
-    configs[4])."""
+    configs[4]), "fp16" (WavLM-base: the bf16 path with fp16 activations and operands -- the same
+    matrix-core rate, 8 more mantissa bits).
 
-    def __init__(self, spec, state_dict: dict, device="cuda:0", dtype: str = "bf16", do_normalize: bool = False):
+    fp16 / fp16x3 keep activations in the fp16 range: with ``check_range`` (default) every embed /
+    hidden_states call synchronises and raises ``SSERangeError`` if it produced a non-finite value
+    (an overflow); throughput loops pass ``check_range=False`` and call ``check_range_now()`` once."""
+
+    def __init__(self, spec, state_dict: dict, device="cuda:0", dtype: str = "bf16", do_normalize: bool = False,
+                 check_range: bool = True):
         if not isinstance(spec, (WavLMSpec, WhisperSpec)):
             raise TypeError(spec)
         self.spec = spec
@@ -89,6 +98,7 @@ class SSEModel:
                                       DTYPES[dtype], ctypes.byref(h)), "sse_model_create")
         self._h = h
         self._ws = None
+        self.check_range = bool(check_range) and dtype in FP16_RANGE
 
     # -- plumbing -------------------------------------------------------------------------
     def close(self):
@@ -120,6 +130,15 @@ class SSEModel:
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def check_range_now(self) -> None:
+        """Synchronise the current stream; raise SSERangeError if a call since the last check wrote a
+        non-finite value (fp16 / fp16x3 models; a no-op for the others)."""
+        _lib.check(_lib.lib().sse_check_range(self._h, self._stream()), "sse_check_range")
+
+    def _after(self):
+        if self.check_range:
+            self.check_range_now()
 
     def _check_wave(self, wave: torch.Tensor) -> torch.Tensor:
         if not isinstance(wave, torch.Tensor) or wave.device != self.device:
@@ -173,6 +192,7 @@ class SSEModel:
         if lengths is None:
             _lib.check(_lib.lib().sse_embed(self._h, wave.data_ptr(), B, L, ids.data_ptr(), n, out.data_ptr(),
                                             ws.data_ptr(), ws.numel(), self._stream()), "sse_embed")
+            self._after()
             return out
         lens = [int(v) for v in (lengths.tolist() if isinstance(lengths, torch.Tensor) else lengths)]
         if len(lens) != B or min(lens) < 1 or max(lens) > L:
@@ -186,6 +206,7 @@ class SSEModel:
         _lib.check(_lib.lib().sse_embed_ragged(self._h, wave.data_ptr(), d_len.data_ptr(), B, L, ids.data_ptr(), n,
                                                out.data_ptr(), ws.data_ptr(), ws.numel(), self._stream()),
                    "sse_embed_ragged")
+        self._after()
         return out
 
     def embed_clips(self, clips, layer_indices) -> torch.Tensor:
@@ -208,6 +229,7 @@ class SSEModel:
         ws = self.workspace(B, L)
         _lib.check(_lib.lib().sse_hidden_states(self._h, wave.data_ptr(), B, L, hs.data_ptr(), ws.data_ptr(),
                                                 ws.numel(), self._stream()), "sse_hidden_states")
+        self._after()
         return tuple(hs.unbind(0))
 
     def hidden_states_from_mel(self, mel: torch.Tensor) -> tuple:

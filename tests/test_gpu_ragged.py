@@ -28,7 +28,7 @@ def _batch(lens, seed, garbage=True):
     return torch.from_numpy(wave).cuda(), clips
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp16x3"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp16x3", "fp16"])
 @pytest.mark.parametrize("lens", [[48000, 400, 12345, 47999, 30000, 16000], [80000, 60000, 52000, 70001]])
 def test_wavlm_ragged_equals_per_clip(wavlm_sd, dtype, lens):
     from ssr_amd import config as C

@@ -171,12 +171,13 @@ def test_bf16_lnfold_matches_materialised(wavlm_sd):
     assert _rel(a[:2], pooled_hs).max() <= 1e-5
 
 
-@pytest.mark.parametrize("n_clips,samples", [(7, 48000), (2, 16000), (3, 80000)])
+@pytest.mark.parametrize("n_clips,samples", [(7, 48000), (2, 16000), (3, 80000), (3, 160000), (1, 170000)])
 def test_bf16_posconv_kernel_matches_grouped_gemm(wavlm_sd, n_clips, samples):
     """The dedicated positional-conv kernel (input window staged once per block, kernels_posconv.hip)
     against the grouped-GEMM path it replaces (posconv_gemm=1), on hidden_states[0] (the
     layer right after it) and the pooled layers: same math, fp32 accumulation in another order.
-    Odd clip counts (the second clip of the last block is empty) and T = 49 / 149 / 249 frames."""
+    Odd clip counts (the second clip of the last block is empty) and T = 49 / 149 / 249 frames, and
+    clips over 256 frames (T = 499 / 530: 256-frame chunks, each with its own window borders)."""
     from ssr_amd import config as C, synth
     from ssr_amd.model import SSEModel
     m = SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype="bf16")
@@ -278,7 +279,7 @@ def test_fp16x3_normalize_and_batch_invariance(wavlm_sd, golden_wavlm):
         assert torch.equal(full[i:i + 1], m.embed(w[i:i + 1], idx))
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "fp16x3"])
+@pytest.mark.parametrize("dtype", ["bf16", "fp16x3", "fp16"])
 def test_two_stream_split_equals_one_stream(wavlm_sd, dtype):
     """Batches of >= 128 WavLM clips run as two half-batches on two streams (split_forward): bit-identical
     to the single-stream call (no_split=1), for an odd batch and a ragged one, and the result is on the
