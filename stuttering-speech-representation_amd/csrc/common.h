@@ -197,6 +197,7 @@ enum {
   OPT_NO_LNFOLD,        // 1: materialise post-LN LayerNorm outputs (bf16 WavLM-base)
   OPT_GEMM_MX_STAGED,   // 1: LDS-staged epilogue for every MX-fp8 GEMM
   OPT_NO_SPLIT,         // 1: WavLM batches run as one stream (no two-stream half-batch split)
+  OPT_LOGMEL_V1,        // 1: the round-2 log-mel kernel (one frame per wave) instead of 4 frames per wave
   OPT_COUNT
 };
 int sse_opt(int id);

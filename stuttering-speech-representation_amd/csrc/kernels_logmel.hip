@@ -53,20 +53,24 @@ __device__ __forceinline__ float unord_f32(unsigned u) {
 constexpr int MAXSUP = 32;   // bins per Slaney filter (80 mels on 201 bins: at most 27)
 
 // support [first, last] of each mel filter's nonzero bins (triangular filters: contiguous) and the
-// filter's weights over it packed [n_mels][MAXSUP] (staged in LDS by the STFT kernel)
-__global__ void lm_support_kernel(const float* __restrict__ fb, int n_mels, int2* __restrict__ sup,
-                                  float* __restrict__ fbp) {
-  const int m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= n_mels) return;
-  int lo = NF, hi = -1;
-  for (int f = 0; f < NF; ++f)
-    if (fb[f * n_mels + m] != 0.f) {
-      lo = f < lo ? f : lo;
-      hi = f;
-    }
+// filter's weights over it packed [n_mels][MAXSUP] (staged in LDS by the STFT kernel).  Block = one
+// filter, a thread per bin (one load each, min / max of the nonzero bins in LDS).
+__global__ __launch_bounds__(256) void lm_support_kernel(const float* __restrict__ fb, int n_mels,
+                                                         int2* __restrict__ sup, float* __restrict__ fbp) {
+  __shared__ int lh[2];
+  const int m = blockIdx.x, f = threadIdx.x;
+  if (f == 0) { lh[0] = NF; lh[1] = -1; }
+  __syncthreads();
+  if (f < NF && fb[f * n_mels + m] != 0.f) {
+    atomicMin(&lh[0], f);
+    atomicMax(&lh[1], f);
+  }
+  __syncthreads();
+  const int lo = lh[0];
+  int hi = lh[1];
   if (hi - lo + 1 > MAXSUP) hi = lo + MAXSUP - 1;   // not reached for n_mels >= 64 (host checks n_mels)
-  sup[m] = make_int2(lo, hi);
-  for (int i = 0; i < MAXSUP; ++i) fbp[m * MAXSUP + i] = lo + i <= hi ? fb[(lo + i) * n_mels + m] : 0.f;
+  if (f == 0) sup[m] = make_int2(lo, hi);
+  if (f < MAXSUP) fbp[m * MAXSUP + f] = lo + f <= hi ? fb[(lo + f) * n_mels + m] : 0.f;
 }
 
 constexpr int MEL_FR = 20;   // frames per block (3000 = 150 x 20), 5 per wave
@@ -76,8 +80,9 @@ constexpr int SPAN = HOP * (MEL_FR - 1) + N_FFT;    // 3440 samples per block
 
 // twiddles W_200^k = exp(-2 pi i k / 200) and the real-split W_400^k, k < 200, from fp64; then the
 // Hann window as (w[2n], w[2n+1]) pairs (torch.hann_window(400), periodic, evaluated in float32)
-__global__ void lm_twiddle_kernel(float2* __restrict__ tw) {
+__global__ void lm_twiddle_kernel(float2* __restrict__ tw, unsigned* __restrict__ mx, int B) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  for (int b = k; b < B; b += gridDim.x * blockDim.x) mx[b] = 0u;   // per-clip maxima (ord_f32(-inf) > 0)
   if (k < 2 * NZ) {
     const double a = k < NZ ? -2.0 * (double)k / NZ : -2.0 * (double)(k - NZ) / N_FFT;   // in units of pi
     tw[k] = make_float2((float)cospi(a), (float)sinpi(a));
@@ -240,6 +245,273 @@ __global__ __launch_bounds__(256) void lm_stft_mel_kernel(const float* __restric
   if (lane == 0) atomicMax(mx + b, ord_f32(lmax));
 }
 
+// ---- round 3: four frames per wave, every lane busy -------------------------------------------------
+// The one-frame-per-wave kernel above keeps 25 / 40 of 64 lanes busy in the radix-8 / radix-5 stages and
+// 201 / 80 in the split / mel loops, so it is VALU-issue bound at ~40 % lane occupancy.  Here a wave
+// transforms LM_F = 4 frames together: every stage's (frame, butterfly) tasks are spread over the 64
+// lanes (radix 8: 100 tasks, radix 5: 160, split: 804, mel: 4 n_mels), each stage runs in place in one
+// [LM_F][200] complex LDS buffer per wave -- all of a stage's inputs are read into registers, a wave
+// barrier, then the outputs written (Stockham order, no ping-pong buffer) -- and the radix-5 butterfly
+// is the 5-point Winograd form (~36 flops instead of 80).  Block = 5 waves = 20 frames, the same grid.
+constexpr int LM_F = 4, LM_W = 5;
+static_assert(LM_F * LM_W == MEL_FR, "block = 20 frames");
+
+// 5-point DFT, W = exp(-2 pi i / 5): y_q = sum_r x_r W^(q r)
+SSE_DEV void dft5(const float2 (&x)[5], float2 (&y)[5]) {
+  const float c1 = 0.30901699437494742f, c2 = -0.80901699437494742f;   // cos 72, cos 144
+  const float s1 = 0.95105651629515357f, s2 = 0.58778525229247313f;    // sin 72, sin 144
+  const float2 t1 = make_float2(x[1].x + x[4].x, x[1].y + x[4].y), t2 = make_float2(x[2].x + x[3].x, x[2].y + x[3].y);
+  const float2 t3 = make_float2(x[1].x - x[4].x, x[1].y - x[4].y), t4 = make_float2(x[2].x - x[3].x, x[2].y - x[3].y);
+  y[0] = make_float2(x[0].x + t1.x + t2.x, x[0].y + t1.y + t2.y);
+  const float2 a = make_float2(fmaf(c2, t2.x, fmaf(c1, t1.x, x[0].x)), fmaf(c2, t2.y, fmaf(c1, t1.y, x[0].y)));
+  const float2 b = make_float2(fmaf(c1, t2.x, fmaf(c2, t1.x, x[0].x)), fmaf(c1, t2.y, fmaf(c2, t1.y, x[0].y)));
+  const float2 d = make_float2(fmaf(s2, t4.x, s1 * t3.x), fmaf(s2, t4.y, s1 * t3.y));     // s1 t3 + s2 t4
+  const float2 e = make_float2(fmaf(-s1, t4.x, s2 * t3.x), fmaf(-s1, t4.y, s2 * t3.y));   // s2 t3 - s1 t4
+  // y1 = a - i d, y4 = a + i d, y2 = b - i e, y3 = b + i e
+  y[1] = make_float2(a.x + d.y, a.y - d.x);
+  y[4] = make_float2(a.x - d.y, a.y + d.x);
+  y[2] = make_float2(b.x + e.y, b.y - e.x);
+  y[3] = make_float2(b.x - e.y, b.y + e.x);
+}
+
+SSE_DEV void dft8(const float2 (&v)[8], float2 (&o)[8]) {   // radix 2 x 2 x 2 (constant twiddles)
+  const float h = 0.70710678118654752f;
+  float2 a[8];
+  #pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    a[r] = make_float2(v[r].x + v[r + 4].x, v[r].y + v[r + 4].y);
+    a[r + 4] = make_float2(v[r].x - v[r + 4].x, v[r].y - v[r + 4].y);
+  }
+  a[5] = make_float2((a[5].x + a[5].y) * h, (a[5].y - a[5].x) * h);
+  a[6] = make_float2(a[6].y, -a[6].x);
+  a[7] = make_float2((a[7].y - a[7].x) * h, -(a[7].x + a[7].y) * h);
+  float2 c[8];
+  #pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int b0 = 4 * g;
+    c[b0 + 0] = make_float2(a[b0].x + a[b0 + 2].x, a[b0].y + a[b0 + 2].y);
+    c[b0 + 2] = make_float2(a[b0].x - a[b0 + 2].x, a[b0].y - a[b0 + 2].y);
+    c[b0 + 1] = make_float2(a[b0 + 1].x + a[b0 + 3].x, a[b0 + 1].y + a[b0 + 3].y);
+    const float2 t = make_float2(a[b0 + 1].x - a[b0 + 3].x, a[b0 + 1].y - a[b0 + 3].y);
+    c[b0 + 3] = make_float2(t.y, -t.x);
+  }
+  o[0] = make_float2(c[0].x + c[1].x, c[0].y + c[1].y);
+  o[4] = make_float2(c[0].x - c[1].x, c[0].y - c[1].y);
+  o[2] = make_float2(c[2].x + c[3].x, c[2].y + c[3].y);
+  o[6] = make_float2(c[2].x - c[3].x, c[2].y - c[3].y);
+  o[1] = make_float2(c[4].x + c[5].x, c[4].y + c[5].y);
+  o[5] = make_float2(c[4].x - c[5].x, c[4].y - c[5].y);
+  o[3] = make_float2(c[6].x + c[7].x, c[6].y + c[7].y);
+  o[7] = make_float2(c[6].x - c[7].x, c[6].y - c[7].y);
+}
+
+SSE_DEV void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// one radix-R Stockham stage (span Ns so far) over the wave's LM_F frames, in place: task = (frame,
+// butterfly j), lane-strided; inputs into registers, wave barrier, outputs
+template <int R>
+SSE_DEV void fft_stage4(float2* __restrict__ z, int Ns, const float2* __restrict__ tw, int lane) {
+  constexpr int NB = NZ / R, NT = LM_F * NB, IT = (NT + 63) / 64;
+  float2 v[IT][R];
+  #pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int task = lane + 64 * it;
+    if (task < NT) {
+      const int f = task / NB, j = task - f * NB, k = j % Ns;
+      const float2* zf = z + f * NZ;
+      #pragma unroll
+      for (int r = 0; r < R; ++r) {
+        v[it][r] = zf[j + r * NB];
+        if (r) v[it][r] = cmul(v[it][r], tw[(k * r * (NZ / (Ns * R))) % NZ]);   // W_{Ns R}^{k r}
+      }
+    }
+  }
+  wave_lds_sync();
+  #pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int task = lane + 64 * it;
+    if (task < NT) {
+      const int f = task / NB, j = task - f * NB, k = j % Ns;
+      float2 o[R];
+      if constexpr (R == 8) dft8(v[it], o);
+      else dft5(v[it], o);
+      float2* zf = z + f * NZ + (j / Ns) * Ns * R + k;
+      #pragma unroll
+      for (int q = 0; q < R; ++q) zf[q * Ns] = o[q];
+    }
+  }
+  wave_lds_sync();
+}
+
+// Block = one 20-frame chunk (a persistent form walking chunks with the next chunk's samples prefetched
+// into registers measured slower: 0.78 vs 0.61 ms for 128 x 30 s -- its per-chunk block barriers
+// serialise the waves that separate blocks on a CU keep out of phase).
+constexpr int LM_CPC = NFR / MEL_FR;   // chunks per clip
+__global__ __launch_bounds__(64 * LM_W) void lm_stft_mel4_kernel(const float* __restrict__ wave, int B, int L, int Lv0,
+                                                                 const int* __restrict__ lens,
+                                                                 const float2* __restrict__ twg,
+                                                                 const float* __restrict__ fbp,
+                                                                 const int2* __restrict__ sup, int n_mels,
+                                                                 float* __restrict__ logv, unsigned* __restrict__ mx) {
+  constexpr int NTH = 64 * LM_W;
+  // dynamic LDS (47.7 KB at 80 mels: three blocks per CU): the frame buffers, whose first 13.8 KB also
+  // hold the chunk's samples until every wave has read its window (one block barrier) | twiddles |
+  // filter weights transposed [i][m] (lanes of consecutive m read consecutive words; the [m][i] image
+  // is a 32-word stride, every lane of a pass on one bank) | each filter's first bin and support length
+  extern __shared__ __attribute__((aligned(16))) char lsm[];
+  float2 (*zbuf)[LM_F * NZ] = (float2 (*)[LM_F * NZ])lsm;
+  float* xs = (float*)lsm;
+  static_assert(SPAN * 4 <= LM_W * LM_F * NZ * 8, "samples alias the frame buffers");
+  float2* tw = (float2*)(lsm + LM_W * LM_F * NZ * 8);   // W_200^k | W_400^k | Hann pairs
+  float* fwt = (float*)(tw + 3 * NZ);
+  int* fs = (int*)(fwt + MAXSUP * n_mels);
+  int* fsn = fs + n_mels;
+  static_assert(LM_F == 4, "mel task split m = task >> 2");
+  const float2* win = tw + 2 * NZ;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nch = B * LM_CPC;
+  constexpr int NX = (SPAN + NTH - 1) / NTH;
+  float xr[NX];
+  // samples of chunk c (zero-pad / truncate to 480000, reflect-pad 200) into registers
+  auto load_chunk = [&](int c) {
+    const int b = c / LM_CPC, t0 = (c - b * LM_CPC) * MEL_FR;
+    const int Lv = lens ? (lens[b] < NS ? lens[b] : NS) : Lv0;
+    const float* xw = wave + (long long)b * L;
+    #pragma unroll
+    for (int u = 0; u < NX; ++u) {
+      const int i = threadIdx.x + u * NTH;
+      int j = HOP * t0 + i - PAD;
+      if (j < 0) j = -j;
+      if (j >= NS) j = 2 * (NS - 1) - j;
+      xr[u] = (i < SPAN && j < Lv) ? xw[j] : 0.f;
+    }
+  };
+  const int c = blockIdx.x;
+  if (c >= nch) return;
+  load_chunk(c);
+  {   // tables: every global load issued before the first LDS write
+    constexpr int NTW = (3 * NZ + NTH - 1) / NTH, NFW = (LM_MAXMEL * MAXSUP + NTH - 1) / NTH;
+    float fr[NFW];
+    float2 tr[NTW];
+    #pragma unroll
+    for (int u = 0; u < NTW; ++u) {
+      const int i = threadIdx.x + u * NTH;
+      tr[u] = i < 3 * NZ ? twg[i] : make_float2(0.f, 0.f);
+    }
+    #pragma unroll
+    for (int u = 0; u < NFW; ++u) {
+      const int i = threadIdx.x + u * NTH;
+      fr[u] = i < n_mels * MAXSUP ? fbp[i] : 0.f;
+    }
+    const int2 sv = threadIdx.x < n_mels ? sup[threadIdx.x] : make_int2(0, -1);
+    #pragma unroll
+    for (int u = 0; u < NTW; ++u) {
+      const int i = threadIdx.x + u * NTH;
+      if (i < 3 * NZ) tw[i] = tr[u];
+    }
+    #pragma unroll
+    for (int u = 0; u < NFW; ++u) {
+      const int i = threadIdx.x + u * NTH;
+      if (i < n_mels * MAXSUP) fwt[(i % MAXSUP) * n_mels + i / MAXSUP] = fr[u];
+    }
+    if (threadIdx.x < n_mels) {
+      fs[threadIdx.x] = sv.x;
+      fsn[threadIdx.x] = sv.y - sv.x + 1;   // lm_support_kernel: hi - lo + 1 <= MAXSUP, 0 for an empty filter
+    }
+  }
+  float2* z = zbuf[wv];
+  const int fr0 = wv * LM_F;   // the wave's first frame within the chunk
+  {
+    const int b = c / LM_CPC, t0 = (c - b * LM_CPC) * MEL_FR;
+    #pragma unroll
+    for (int u = 0; u < NX; ++u) {
+      const int i = threadIdx.x + u * NTH;
+      if (i < SPAN) xs[i] = xr[u];
+    }
+    __syncthreads();
+    // z_f[n] = w[2n] x[2n] + i w[2n+1] x[2n+1]: windowed into registers, then (every wave done with the
+    // samples the frame buffers alias) stored
+    constexpr int NWT = (LM_F * NZ + 63) / 64;
+    float2 zw[NWT];
+    #pragma unroll
+    for (int it = 0; it < NWT; ++it) {
+      const int task = lane + 64 * it;
+      if (task < LM_F * NZ) {
+        const int f = task / NZ, n = task - f * NZ;
+        const float2 x2 = *(const float2*)(xs + HOP * (fr0 + f) + 2 * n);
+        const float2 w = win[n];
+        zw[it] = make_float2(w.x * x2.x, w.y * x2.y);
+      }
+    }
+    __syncthreads();
+    #pragma unroll
+    for (int it = 0; it < NWT; ++it) {
+      const int task = lane + 64 * it;
+      if (task < LM_F * NZ) z[task] = zw[it];
+    }
+    wave_lds_sync();
+    fft_stage4<8>(z, 1, tw, lane);
+    fft_stage4<5>(z, 8, tw, lane);
+    fft_stage4<5>(z, 40, tw, lane);
+    // real split + |X|^2 (201 bins per frame) into the same buffer, as floats [LM_F][NF + 3]
+    constexpr int NSP = LM_F * NF, ISP = (NSP + 63) / 64;
+    float pw[ISP];
+    #pragma unroll
+    for (int it = 0; it < ISP; ++it) {
+      const int task = lane + 64 * it;
+      pw[it] = 0.f;
+      if (task < NSP) {
+        const int f = task / NF, k = task - f * NF;
+        const float2* zf = z + f * NZ;
+        if (k == 0 || k == NZ) {
+          const float2 z0 = zf[0];
+          const float xr0 = k == 0 ? z0.x + z0.y : z0.x - z0.y;
+          pw[it] = xr0 * xr0;
+        } else {
+          const float2 a = zf[k], cc = zf[NZ - k];
+          const float2 e = make_float2(0.5f * (a.x + cc.x), 0.5f * (a.y - cc.y));
+          const float2 o = make_float2(0.5f * (a.x - cc.x), 0.5f * (a.y + cc.y));
+          const float2 wo = cmul(tw[NZ + k], o);
+          const float xre = e.x + wo.y, xim = e.y - wo.x;
+          pw[it] = xre * xre + xim * xim;
+        }
+      }
+    }
+    wave_lds_sync();
+    float* P = (float*)z;
+    constexpr int PST = NF + 3;
+    #pragma unroll
+    for (int it = 0; it < ISP; ++it) {
+      const int task = lane + 64 * it;
+      if (task < NSP) {
+        const int f = task / NF, k = task - f * NF;
+        P[f * PST + k] = pw[it];
+      }
+    }
+    wave_lds_sync();
+    // mel: task = (mel m, frame f), m-major, so a 64-lane pass holds 16 neighbouring filters of similar
+    // width; each lane sums only its filter's support [lo, hi] (in order: the same fp32 chain as the dense
+    // 201-bin sum, whose other terms are fma(0, P, acc) = acc), the pass runs as long as its widest filter
+    float lmax = -INFINITY;
+    for (int task = lane; task < LM_F * n_mels; task += 64) {
+      const int m = task >> 2, f = task & (LM_F - 1);
+      const float* Pf = P + f * PST + fs[m];
+      const int n = fsn[m];
+      float acc = 0.f;
+      for (int i = 0; i < n; ++i) acc = fmaf(fwt[i * n_mels + m], Pf[i], acc);
+      const float v = log10f(fmaxf(acc, 1e-10f));
+      logv[((long long)b * NFR + t0 + fr0 + f) * n_mels + m] = v;
+      lmax = fmaxf(lmax, v);
+    }
+    lmax = wave_max(lmax);
+    if (lane == 0) atomicMax(mx + b, ord_f32(lmax));
+  }
+}
+
 // 64 frames x n_mels per block: channels-last output straight through (coalesced), the HF layout
 // [B][n_mels][3000] through an LDS transpose so its 64-frame rows are coalesced too
 constexpr int FIN_T = 64;
@@ -317,12 +589,18 @@ int launch_logmel(const float* x, int B, int L, int n_mels, float* out_hf, TO* o
   unsigned* mx = (unsigned*)p; p += al((size_t)B * 4);
   int2* sup = (int2*)p; p += al((size_t)n_mels * 8);
   float* fbp = (float*)p;
-  if (hipMemsetAsync(mx, 0, (size_t)B * 4, s) != hipSuccess) return -2;
-  hipLaunchKernelGGL(lm_twiddle_kernel, dim3((3 * NZ + 255) / 256), dim3(256), 0, s, tw);
+  hipLaunchKernelGGL(lm_twiddle_kernel, dim3((3 * NZ + 255) / 256), dim3(256), 0, s, tw, mx, B);
   hipLaunchKernelGGL(lm_filters_kernel, dim3((NF * n_mels + 255) / 256), dim3(256), 0, s, fb, n_mels);
-  hipLaunchKernelGGL(lm_support_kernel, dim3((n_mels + 63) / 64), dim3(64), 0, s, fb, n_mels, sup, fbp);
-  hipLaunchKernelGGL(lm_stft_mel_kernel, dim3(NFR / MEL_FR, B), dim3(256), 0, s, x, L, L < NS ? L : NS, lens, tw, fbp,
-                     sup, n_mels, logv, mx);
+  hipLaunchKernelGGL(lm_support_kernel, dim3(n_mels), dim3(256), 0, s, fb, n_mels, sup, fbp);
+  if (sse_opt(OPT_LOGMEL_V1))
+    hipLaunchKernelGGL(lm_stft_mel_kernel, dim3(NFR / MEL_FR, B), dim3(256), 0, s, x, L, L < NS ? L : NS, lens, tw, fbp,
+                       sup, n_mels, logv, mx);
+  else
+  {
+    const size_t lds = (size_t)LM_W * LM_F * NZ * 8 + 3 * NZ * 8 + (size_t)MAXSUP * n_mels * 4 + (size_t)n_mels * 8;
+    hipLaunchKernelGGL(lm_stft_mel4_kernel, dim3(B * LM_CPC), dim3(64 * LM_W), lds, s, x, B, L, L < NS ? L : NS, lens, tw,
+                       fbp, sup, n_mels, logv, mx);
+  }
   hipLaunchKernelGGL((lm_final_kernel<TO>), dim3((NFR + FIN_T - 1) / FIN_T, B), dim3(256), 0, s, logv, mx, n_mels,
                      out_hf, out_cl);
   return hipGetLastError() == hipSuccess ? 0 : -2;

@@ -57,6 +57,23 @@ def test_logmel_batched_ragged():
     assert np.isfinite(z).all() and np.allclose(z, z.flat[0])
 
 
+def test_logmel_four_frame_kernel_matches_one_frame_kernel():
+    """The 4-frames-per-wave STFT kernel (Winograd radix-5, in-place stages) against the round-2
+    one-frame-per-wave kernel (logmel_v1=1): the same transform in another fp32 rounding order, both
+    within the reference bar; a 128-clip batch at the bench shape, ragged lengths, silence."""
+    from ssr_amd import _lib, synth
+    from ssr_amd.model import logmel
+    w = torch.from_numpy(synth.synth_clips(128, 480000, seed=3)).cuda()
+    w[5, 100000:] = 0.0
+    w[7] = 0.0
+    a = logmel(w)
+    with _lib.option("logmel_v1", 1):
+        b = logmel(w)
+    d = (a - b).abs().max().item()
+    print("logmel v4 vs v1 max abs diff", d)
+    assert torch.isfinite(a).all() and d <= 2e-5
+
+
 @pytest.mark.parametrize("dtype,tol", [("fp32", 1e-4), ("bf16", 3e-2)])
 def test_whisper_tiny_embed(tiny, dtype, tol):
     from ssr_amd import config as C, synth
