@@ -126,8 +126,8 @@ int sse_embed(sse_model* m, const float* d_in, int B, int L, const int32_t* laye
  * >= 400 samples, the conv receptive field).  Each clip's embedding equals that clip run alone:
  * WavLM's GroupNorm statistics, attention keys, positional-conv padding and time-means cover the
  * clip's own frames; Whisper pads each clip with zeros to 30 s as the feature extractor does.
- * Bit-identical to the per-clip call when the batch's longest clip selects the same attention
- * kernel (WavLM: all clips <= 160 frames, or all > 160).  The library clamps each length to [0, L]
+ * Bit-identical to the per-clip call (a batch with clips on both sides of WavLM's 160-frame
+ * attention split runs each clip on the kernel it runs alone).  The library clamps each length to [0, L]
  * on the device (no kernel reads past its clip's row whatever the caller passes); a WavLM clip
  * under 400 samples has no frames and its embedding slots are written as zeros (the Python
  * wrapper rejects such clips before the call, as the reference's forward would raise). */

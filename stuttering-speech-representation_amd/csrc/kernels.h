@@ -69,6 +69,8 @@ struct AttnArgs {
   const float* relb;     // [nh][2*maxd+1], index d + maxd
   int maxd;
   const int* tlen;       // ragged batch: frames of each clip [B] (T is then the per-clip row stride)
+  int min_t;             // flash kernel: clips of at most min_t frames are skipped (ragged batches whose
+                         // short clips run on the short-T kernel, exactly as when run alone)
 };
 template <typename T>
 int launch_attention(const AttnArgs& a, int B, hipStream_t s);

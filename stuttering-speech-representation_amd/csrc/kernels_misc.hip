@@ -1391,6 +1391,7 @@ __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
   int qc, h, b;
   attn_block_xcd(qc, h, b);
   const int TS = a.T, T = a.tlen ? a.tlen[b] : a.T, H = a.H, LQ = a.ldq;   // frames of this clip / row stride
+  if (T <= a.min_t) return;   // a short clip of a mixed ragged batch: the short-T kernel's
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
@@ -1593,6 +1594,7 @@ __global__ __launch_bounds__(32 * NKB, 3) void attention_full_kernel(AttnArgs a,
 
   const int h0 = blockIdx.x * hpb, b = blockIdx.y;
   const int TS = a.T, T = a.tlen ? a.tlen[b] : a.T, H = a.H, H3 = a.ldq;   // frames of this clip / row stride
+  if (T > TP) return;   // a long clip of a mixed ragged batch: the flash kernel's
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
@@ -1810,14 +1812,24 @@ int launch_attention(const AttnArgs& a, int B, hipStream_t s) {
       if (a.relb) return a.tlen ? dispatch_full<true, true, H>(a, B, s) : dispatch_full<true, false, H>(a, B, s);
       return a.tlen ? dispatch_full<false, true, H>(a, B, s) : dispatch_full<false, false, H>(a, B, s);
     }
+    AttnArgs af = a;
+    if (a.tlen) {
+      // ragged batch with clips on both sides of 160 frames: each clip runs the kernel it would run
+      // alone (the short-T kernel at 10 key blocks skips the long clips, the flash kernel the short
+      // ones), so every clip's result is bit-identical to its solo call
+      const int rc = a.relb ? launch_attention_full<true, 10, true, H>(a, B, s)
+                            : launch_attention_full<false, 10, true, H>(a, B, s);
+      if (rc) return rc;
+      af.min_t = 160;
+    }
     const int Tk = ((a.T + F2_K - 1) / F2_K) * F2_K;
     const size_t lds2 = 2 * F2_BUF + F2_Q * 4 + (a.relb ? (size_t)2 * Tk * 4 : 0);
     if (lds2 > 160 * 1024) return -3;
     dim3 g2((a.T + F2_Q - 1) / F2_Q, a.nh, B);
     if (a.relb)
-      hipLaunchKernelGGL((attention_flash2_kernel<true, H>), g2, dim3(256), lds2, s, a);
+      hipLaunchKernelGGL((attention_flash2_kernel<true, H>), g2, dim3(256), lds2, s, af);
     else
-      hipLaunchKernelGGL((attention_flash2_kernel<false, H>), g2, dim3(256), lds2, s, a);
+      hipLaunchKernelGGL((attention_flash2_kernel<false, H>), g2, dim3(256), lds2, s, af);
     return hipGetLastError() == hipSuccess ? 0 : -2;
   }
   if constexpr (!is_f16_v<T>) {   // fp32 (and the bf16 grid's unused tail)

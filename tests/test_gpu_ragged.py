@@ -49,18 +49,20 @@ def test_wavlm_ragged_equals_per_clip(wavlm_sd, dtype, lens):
             assert _rel(got[i:i + 1].cpu().numpy(), ref).max() <= 1e-4
 
 
-def test_wavlm_ragged_mixed_attention_paths(wavlm_sd):
-    """Clips on both sides of the 160-frame attention split: equal to per-clip runs within the
-    bf16 path's own noise (different attention kernels, same math)."""
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_wavlm_ragged_mixed_attention_paths(wavlm_sd, dtype):
+    """Clips on both sides of the 160-frame attention split in one batch: each clip runs the attention
+    kernel it runs alone (short-T kernel for <= 160 frames, flash kernel above), so every clip equals
+    its per-clip call bit for bit."""
     from ssr_amd import config as C
     from ssr_amd.model import SSEModel
-    m = SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype="bf16")
-    lens = [48000, 80000, 3000]
+    m = SSEModel(C.WAVLM_BASE, wavlm_sd, device="cuda:0", dtype=dtype)
+    lens = [48000, 80000, 3000, 51840, 51199, 160000]   # 149, 249, 9, 161, 159, 499 frames
     wave, clips = _batch(lens, 77)
-    got = m.embed(wave, [12, 6], lengths=lens).cpu().numpy()
+    got = m.embed(wave, [12, 6], lengths=lens)
     for i, c in enumerate(clips):
-        one = m.embed(torch.from_numpy(c).cuda()[None], [12, 6]).cpu().numpy()
-        assert _rel(got[i:i + 1], one).max() <= 1e-2, (i, lens[i])
+        one = m.embed(torch.from_numpy(c).cuda()[None], [12, 6])
+        assert torch.equal(got[i:i + 1], one), (i, lens[i])
 
 
 def test_wavlm_ragged_normalize_and_embed_clips(wavlm_sd):
