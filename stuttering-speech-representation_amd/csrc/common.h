@@ -198,6 +198,7 @@ enum {
   OPT_GEMM_MX_STAGED,   // 1: LDS-staged epilogue for every MX-fp8 GEMM
   OPT_NO_SPLIT,         // 1: WavLM batches run as one stream (no two-stream half-batch split)
   OPT_LOGMEL_V1,        // 1: the round-2 log-mel kernel (one frame per wave) instead of 4 frames per wave
+  OPT_SPLIT_PARTS,      // 3 or 4: WavLM batches split into that many streams (default 2)
   OPT_COUNT
 };
 int sse_opt(int id);

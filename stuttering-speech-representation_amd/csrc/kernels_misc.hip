@@ -1350,6 +1350,13 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
     if constexpr (BF) {
       bf16x4 ov = {(bf16)(o[db][0] * inv), (bf16)(o[db][1] * inv), (bf16)(o[db][2] * inv), (bf16)(o[db][3] * inv)};
       *(bf16x4*)(orow + db * 16 + 4 * g) = ov;
+    } else if (a.out3) {   // the out-projection's split-fp16 operand row [hi | lo' | hi] directly
+      f16x4 hi, lo;
+      x3_split4(o[db] * inv, hi, lo);
+      f16* o3 = (f16*)a.out + ((long long)b * TS + qi) * 3 * H + h * AT_HD + db * 16 + 4 * g;
+      *(f16x4*)o3 = hi;
+      *(f16x4*)(o3 + H) = lo;
+      *(f16x4*)(o3 + 2 * H) = hi;
     } else {
       *(f32x4*)((float*)orow + db * 16 + 4 * g) = o[db] * inv;
     }

@@ -34,7 +34,7 @@
 static int g_opt[OPT_COUNT] = {0};
 static const char* const g_opt_name[OPT_COUNT] = {"gemm_cfg", "gemm_nonpersist", "gelu_exact", "conv0_valu",
                                                    "posconv_gemm", "no_lnfold", "gemm_mx_staged", "no_split",
-                                                   "logmel_v1"};
+                                                   "logmel_v1", "split_parts"};
 int sse_opt(int id) { return __atomic_load_n(&g_opt[id], __ATOMIC_RELAXED); }
 
 namespace {
@@ -259,8 +259,9 @@ struct sse_model {
   // two-stream half-batch split of WavLM embedding calls (split_forward): the second half runs on
   // aux, forked from / joined to the caller's stream by events (created on first use, on the model's
   // device); the mutex serialises the host-side fork / join of concurrent callers
-  hipStream_t aux = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  static constexpr int MAX_PARTS = 4;
+  hipStream_t aux[MAX_PARTS - 1] = {};
+  hipEvent_t ev_fork = nullptr, ev_join[MAX_PARTS - 1] = {};
   std::mutex split_mu;
 
   template <typename X = void> const X* ptr(size_t off) const { return (const X*)(dmem + off); }
@@ -977,7 +978,7 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
 // positional conv and the attention core (scores, softmax, P.V) run in exact fp32 as in the fp32
 // path; LayerNorms read / write fp32 and tripled rows.
 struct X3Ws {
-  size_t zero, norm, part, ss, c0, bufA, bufB, x, xt, xb, qkv, ctx, ctx3, ff, fr;
+  size_t zero, norm, part, ss, c0, bufA, bufB, x, xt, xb, qkv, ctx3, ff, fr;
 };
 
 X3Ws x3_plan(const sse_model* m, int B, int L, Plan& p) {
@@ -1004,7 +1005,6 @@ X3Ws x3_plan(const sse_model* m, int B, int L, Plan& p) {
   w.xt = p.add(M * H * 4);
   w.xb = p.add(M * (size_t)(H > Cl ? H : Cl) * 6);
   w.qkv = p.add(M * (size_t)(((3 * H + 8 * c.heads + 255) / 256) * 256) * 4);
-  w.ctx = p.add(M * H * 4);
   w.ctx3 = p.add(M * H * 6);
   w.ff = p.add(M * (size_t)c.ffn * 6);
   w.fr = p.add((size_t)B * 8);
@@ -1088,7 +1088,6 @@ int wavlm_forward_x3(sse_model* m, const float* wave, int B, int L, const Sink& 
   RC(launch_layernorm_x3(x, false, m->ptr<float>(m->enc_ln_w), m->ptr<float>(m->enc_ln_b), M, H, eps, x, xb, s));
   RC(sink.emit(0, x));
   float* qkv = (float*)(ws + w.qkv);
-  float* ctx = (float*)(ws + w.ctx);
   f16* ctx3 = (f16*)(ws + w.ctx3);
   f16* ff = (f16*)(ws + w.ff);
   for (int l = 0; l < c.layers; ++l) {
@@ -1102,11 +1101,11 @@ int wavlm_forward_x3(sse_model* m, const float* wave, int B, int L, const Sink& 
     RC(prof(m, s, "gemm:qkv", 2.0 * M * (3.0 * H + 8.0 * nh) * H, gbytes<bf16>(g),
             [&] { return launch_gemm8_bf16(g, s); }));
     AttnArgs a{};
-    a.qkv = qkv; a.out = ctx; a.T = Tf; a.H = H; a.nh = nh; a.ldq = m->ldq; a.scale = 0.125f;
+    a.qkv = qkv; a.out = ctx3; a.out3 = 1; a.T = Tf; a.H = H; a.nh = nh; a.ldq = m->ldq; a.scale = 0.125f;
     a.gconst = m->ptr<float>(Lw.g_const); a.relb = m->ptr<float>(m->relb); a.maxd = MAXD; a.tlen = tflen;
-    RC(prof(m, s, "attn", 4.0 * B * (double)Tf * Tf * H, (double)B * Tf * (4.0 * H + 8.0 * nh) * 4.0,
+    // the attention writes the out-projection's tripled operand itself (no fp32 context round trip)
+    RC(prof(m, s, "attn", 4.0 * B * (double)Tf * Tf * H, (double)B * Tf * ((3.0 * H + 8.0 * nh) * 4.0 + 6.0 * H),
             [&] { return launch_attention<float>(a, B, s); }));
-    RC(launch_split3(ctx, M, H, ctx3, s));
     g = GemmArgs{};
     g.A = ctx3; g.B = m->ptr(Lw.o_w); g.M = M; g.N = H; g.K = 3 * H; g.rows_per_seg = M; g.lda = 3 * H;
     g.bias = m->ptr<float>(Lw.o_b); g.resid = x; g.Cf = x; g.ldc = H;
@@ -1314,9 +1313,19 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
 // single-stream call (every clip's result is independent of the batch it is in).  Not for hidden-state
 // calls, Whisper (1500-frame clips already give full rounds) or when OPT_NO_SPLIT is set.
 constexpr int SPLIT_MIN = 128;
+// parts of a split call: 2 (sse_set_option "split_parts" 3 or 4 for A/B runs), at least 64 clips each
+int split_parts(int B) {
+  const int o = sse_opt(OPT_SPLIT_PARTS);
+  int P = o >= 2 && o <= sse_model::MAX_PARTS ? o : 2;
+  while (P > 2 && B / P < 64) --P;
+  return P;
+}
 bool split_applies(const sse_model* m, int B, const Sink* sink) {
   return m->cfg.kind == SSE_KIND_WAVLM && B >= SPLIT_MIN && !sse_opt(OPT_NO_SPLIT) && (!sink || !sink->hs);
 }
+// clips of part i of P (the first B % P parts one more)
+inline int part_size(int B, int P, int i) { return B / P + (i < B % P ? 1 : 0); }
+size_t split_ws_bytes(const sse_model* m, int B, int L);
 size_t wavlm_ws(const sse_model* m, int B, int L) {
   Plan p;
   if (m->x3()) x3_plan(m, B, L, p); else wavlm_plan(m, B, L, p);
@@ -1329,28 +1338,48 @@ int forward_one(sse_model* m, const float* d_in, int B, int L, const Sink& sink,
 int split_forward(sse_model* m, const float* d_in, int B, int L, const Sink& sink, char* ws, hipStream_t s,
                   const int* lens) {
   std::lock_guard<std::mutex> lk(m->split_mu);
-  if (!m->aux) {
-    if (hipStreamCreateWithFlags(&m->aux, hipStreamNonBlocking) != hipSuccess) { m->aux = nullptr; return SSE_ERR_HIP; }
-    if (hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&m->ev_join, hipEventDisableTiming) != hipSuccess)
-      return SSE_ERR_HIP;
+  const int P = split_parts(B);
+  if (!m->ev_fork && hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming) != hipSuccess) {
+    m->ev_fork = nullptr;
+    return SSE_ERR_HIP;
   }
-  const int B1 = (B + 1) / 2, B2 = B - B1;
-  const size_t w1 = (wavlm_ws(m, B1, L) + 255) & ~(size_t)255;
-  Sink s1 = sink, s2 = sink;
-  s1.B = B1;
-  s2.B = B2;
-  s2.pooled = sink.pooled + (size_t)B1 * sink.n_ids * sink.H;
-  s2.s = m->aux;
-  if (hipEventRecord(m->ev_fork, s) != hipSuccess || hipStreamWaitEvent(m->aux, m->ev_fork, 0) != hipSuccess)
-    return SSE_ERR_HIP;
-  int rc = forward_one(m, d_in, B1, L, s1, ws, s, false, nullptr, lens);
-  const int rc2 = forward_one(m, d_in + (size_t)B1 * L, B2, L, s2, ws + w1, m->aux, false, nullptr,
-                              lens ? lens + B1 : nullptr);
-  // the join is recorded whatever happened, so the caller's stream never runs ahead of aux work
-  if (hipEventRecord(m->ev_join, m->aux) != hipSuccess || hipStreamWaitEvent(s, m->ev_join, 0) != hipSuccess)
-    return SSE_ERR_HIP;
-  return rc ? rc : rc2;
+  for (int i = 0; i < P - 1; ++i) {
+    if (!m->aux[i]) {
+      if (hipStreamCreateWithFlags(&m->aux[i], hipStreamNonBlocking) != hipSuccess) { m->aux[i] = nullptr; return SSE_ERR_HIP; }
+      if (hipEventCreateWithFlags(&m->ev_join[i], hipEventDisableTiming) != hipSuccess) {
+        m->ev_join[i] = nullptr;
+        return SSE_ERR_HIP;
+      }
+    }
+  }
+  if (hipEventRecord(m->ev_fork, s) != hipSuccess) return SSE_ERR_HIP;
+  int rc = 0, b0 = 0;
+  size_t off = 0;
+  for (int i = 0; i < P; ++i) {
+    const int Bi = part_size(B, P, i);
+    hipStream_t si = i ? m->aux[i - 1] : s;
+    if (i && hipStreamWaitEvent(si, m->ev_fork, 0) != hipSuccess) return SSE_ERR_HIP;
+    Sink sk = sink;
+    sk.B = Bi;
+    sk.pooled = sink.pooled + (size_t)b0 * sink.n_ids * sink.H;
+    sk.s = si;
+    const int r = forward_one(m, d_in + (size_t)b0 * L, Bi, L, sk, ws + off, si, false, nullptr, lens ? lens + b0 : nullptr);
+    rc = rc ? rc : r;
+    off += (wavlm_ws(m, Bi, L) + 255) & ~(size_t)255;
+    b0 += Bi;
+  }
+  // the joins are recorded whatever happened, so the caller's stream never runs ahead of aux work
+  for (int i = 0; i < P - 1; ++i)
+    if (hipEventRecord(m->ev_join[i], m->aux[i]) != hipSuccess || hipStreamWaitEvent(s, m->ev_join[i], 0) != hipSuccess)
+      return SSE_ERR_HIP;
+  return rc;
+}
+
+size_t split_ws_bytes(const sse_model* m, int B, int L) {
+  const int P = split_parts(B);
+  size_t t = 0;
+  for (int i = 0; i < P; ++i) t += (wavlm_ws(m, part_size(B, P, i), L) + 255) & ~(size_t)255;
+  return t;
 }
 
 int forward_any(sse_model* m, const float* d_in, int B, int L, const Sink& sink, void* d_ws, size_t ws_bytes,
@@ -1525,8 +1554,10 @@ void sse_model_destroy(sse_model* m) {
   if (!m) return;
   for (auto e : m->prof.ev) (void)hipEventDestroy(e);
   if (m->ev_fork) (void)hipEventDestroy(m->ev_fork);
-  if (m->ev_join) (void)hipEventDestroy(m->ev_join);
-  if (m->aux) (void)hipStreamDestroy(m->aux);
+  for (int i = 0; i < sse_model::MAX_PARTS - 1; ++i) {
+    if (m->ev_join[i]) (void)hipEventDestroy(m->ev_join[i]);
+    if (m->aux[i]) (void)hipStreamDestroy(m->aux[i]);
+  }
   if (m->dmem) {
     int prev = -1;
     (void)hipGetDevice(&prev);
@@ -1548,10 +1579,9 @@ size_t sse_workspace_bytes(const sse_model* m, int B, int L) {
   if (m->cfg.kind == SSE_KIND_WAVLM) {
     if (wavlm_frames(m->cfg, L, nullptr) <= 0) return 0;
     const size_t one = wavlm_ws(m, B, L);
-    if (split_applies(m, B, nullptr)) {   // two half-batch workspaces (split_forward); also covers one stream
-      const int B1 = (B + 1) / 2;
-      const size_t two = ((wavlm_ws(m, B1, L) + 255) & ~(size_t)255) + wavlm_ws(m, B - B1, L);
-      return two > one ? two : one;
+    if (split_applies(m, B, nullptr)) {   // the parts' workspaces (split_forward); also covers one stream
+      const size_t parts = split_ws_bytes(m, B, L);
+      return parts > one ? parts : one;
     }
     return one;
   } else {
