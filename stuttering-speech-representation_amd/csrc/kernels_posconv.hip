@@ -19,16 +19,17 @@
 
 namespace {
 
-constexpr int PC_CG = 48;            // channels per group (WavLM: 768 / 16)
 constexpr int PC_KST = 128;          // K per weight stage
-constexpr int PC_STAGE = PC_CG * PC_KST * 2;   // 12 KiB
 
-template <int TP, bool H16 = false>   // H16: fp16 input window / weights (SSE_DTYPE_FP16) in bf16 containers
+// PC_CG: channels per group (WavLM-base 768 / 16 = 48, WavLM-large 1024 / 16 = 64)
+template <int TP, bool H16 = false, int PC_CG = 48>   // H16: fp16 window / weights (SSE_DTYPE_FP16) in bf16 containers
 __global__ __launch_bounds__(64 * (2 * TP / 64)) void posconv_kernel(const bf16* __restrict__ xt, const bf16* __restrict__ W,
                                                                     const float* __restrict__ bias, float* __restrict__ x,
                                                                     int B, int T, int H, int K, int pad) {
   constexpr int NW = 2 * TP / 64;                 // waves: 4 row blocks of 16 each
   constexpr int NT = 64 * NW;
+  constexpr int PC_STAGE = PC_CG * PC_KST * 2;    // 12 / 16 KiB
+  constexpr int NCB = PC_CG / 16;                 // column blocks per wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int WF = TP + K - 1;                      // window frames per clip
   char* win = smem;                               // [2][WF][cg] bf16
@@ -64,9 +65,10 @@ __global__ __launch_bounds__(64 * (2 * TP / 64)) void posconv_kernel(const bf16*
   load_w(0);
   // ---- input windows: frame f of clip c holds xt[b0 + c][f - pad][grp*cg + 0..47] (zero outside) ----
   {
-    const int n16 = 2 * WF * (PC_CG / 8);
+    const int n16 = 2 * WF * (PC_CG / 8);   // 16-B chunks of both clips' windows
     for (int i = tid; i < n16; i += NT) {
-      const int c = i / (WF * 6), r = i - c * WF * 6, f = r / 6, ch = r - f * 6;
+      constexpr int CPF = PC_CG / 8;   // 16-B chunks per frame
+      const int c = i / (WF * CPF), r = i - c * WF * CPF, f = r / CPF, ch = r - f * CPF;
       const int tt = f0 + f - pad, b = b0 + c;
       bf16x8 v = bf16x8{};
       if (b < B && tt >= 0 && tt < T) v = *(const bf16x8*)(xt + ((long long)b * T + tt) * H + grp * PC_CG + ch * 8);
@@ -77,11 +79,11 @@ __global__ __launch_bounds__(64 * (2 * TP / 64)) void posconv_kernel(const bf16*
   __syncthreads();
 
   // ---- per wave: row blocks rb = 4*wave .. 4*wave+3 of the block's 2*TP rows ----
-  f32x4 acc[4][3];
+  f32x4 acc[4][NCB];
   #pragma unroll
   for (int i = 0; i < 4; ++i)
     #pragma unroll
-    for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NCB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   int abase[4];   // byte offset of frame t (row r16 of the row block) in its clip's window
   #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -94,9 +96,9 @@ __global__ __launch_bounds__(64 * (2 * TP / 64)) void posconv_kernel(const bf16*
     const char* wb = wst + (st & 1) * PC_STAGE;
     #pragma unroll
     for (int ss = 0; ss < PC_KST / 32; ++ss) {
-      bf16x8 bf[3], af[4];
+      bf16x8 bf[NCB], af[4];
       #pragma unroll
-      for (int j = 0; j < 3; ++j) {
+      for (int j = 0; j < NCB; ++j) {
         const int row = j * 16 + r16, chunk = ss * 4 + q;
         bf[j] = *(const bf16x8*)(wb + row * (PC_KST * 2) + ((chunk ^ (row & 15)) * 16));
       }
@@ -106,7 +108,7 @@ __global__ __launch_bounds__(64 * (2 * TP / 64)) void posconv_kernel(const bf16*
       #pragma unroll
       for (int i = 0; i < 4; ++i)
         #pragma unroll
-        for (int j = 0; j < 3; ++j) acc[i][j] = mfma_h<H16>(bf[j], af[i], acc[i][j]);
+        for (int j = 0; j < NCB; ++j) acc[i][j] = mfma_h<H16>(bf[j], af[i], acc[i][j]);
       ch += 32;
       if (ch >= PC_CG) { ch -= PC_CG; ++tap; }
     }
@@ -121,7 +123,7 @@ __global__ __launch_bounds__(64 * (2 * TP / 64)) void posconv_kernel(const bf16*
     if (b >= B || t >= T) continue;
     float* xr = x + ((long long)b * T + t) * H + grp * PC_CG;
     #pragma unroll
-    for (int j = 0; j < 3; ++j) {
+    for (int j = 0; j < NCB; ++j) {
       const int n = j * 16 + 4 * q;
       const f32x4 bv = *(const f32x4*)(bias + grp * PC_CG + n);
       f32x4 r = *(const f32x4*)(xr + n);
@@ -133,20 +135,42 @@ __global__ __launch_bounds__(64 * (2 * TP / 64)) void posconv_kernel(const bf16*
   }
 }
 
-template <int TP>
+template <int TP, int CG>
 int launch_tp(const bf16* xt, const bf16* W, const float* bias, float* x, int B, int T, int H, int G, int K, int pad,
               hipStream_t s, bool h16) {
   const int WF = TP + K - 1;
-  const size_t lds = ((size_t)(2 * WF * PC_CG * 2 + 15) & ~(size_t)15) + 2 * (size_t)PC_STAGE;
+  const size_t lds = ((size_t)(2 * WF * CG * 2 + 15) & ~(size_t)15) + 2 * (size_t)(CG * PC_KST * 2);
   if (lds > 160 * 1024) return -3;
   constexpr int NT = 64 * (2 * TP / 64);
   if (h16)
-    hipLaunchKernelGGL((posconv_kernel<TP, true>), dim3((B + 1) / 2, G, (T + TP - 1) / TP), dim3(NT), lds, s, xt, W, bias,
-                       x, B, T, H, K, pad);
+    hipLaunchKernelGGL((posconv_kernel<TP, true, CG>), dim3((B + 1) / 2, G, (T + TP - 1) / TP), dim3(NT), lds, s, xt, W,
+                       bias, x, B, T, H, K, pad);
   else
-    hipLaunchKernelGGL((posconv_kernel<TP>), dim3((B + 1) / 2, G, (T + TP - 1) / TP), dim3(NT), lds, s, xt, W, bias, x,
-                       B, T, H, K, pad);
+    hipLaunchKernelGGL((posconv_kernel<TP, false, CG>), dim3((B + 1) / 2, G, (T + TP - 1) / TP), dim3(NT), lds, s, xt, W,
+                       bias, x, B, T, H, K, pad);
   return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+template <int CG>
+int launch_cg(const bf16* xt, const bf16* W, const float* bias, float* x, int B, int T, int H, int G, int K, int pad,
+              hipStream_t s, bool h16) {
+  if ((K * CG) % PC_KST) return -3;
+  // 2*TP rows per block, 4 row blocks per wave; clips longer than 256 frames in 256-frame chunks
+  // (blockIdx.z), each chunk's input window staged with its own pad-frame borders (64-channel groups:
+  // at most 192 frames per chunk, so the window and the weight stages fit the LDS)
+  const int tmax = CG > 48 ? 192 : 256;
+  const int tp = T > tmax ? tmax : ((T + 31) / 32) * 32;
+  switch (tp) {
+    case 32: return launch_tp<32, CG>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
+    case 64: return launch_tp<64, CG>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
+    case 96: return launch_tp<96, CG>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
+    case 128: return launch_tp<128, CG>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
+    case 160: return launch_tp<160, CG>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
+    case 192: return launch_tp<192, CG>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
+    case 224: return launch_tp<224, CG>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
+    case 256: return launch_tp<256, CG>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
+    default: return -3;
+  }
 }
 
 }  // namespace
@@ -154,19 +178,10 @@ int launch_tp(const bf16* xt, const bf16* W, const float* bias, float* x, int B,
 // -3: shape outside this kernel (the caller falls back to the grouped GEMM)
 int launch_posconv_bf16(const bf16* xt, const bf16* W, const float* bias, float* x, int B, int T, int H, int G, int K,
                         int pad, hipStream_t s, bool h16) {
-  if (H != G * PC_CG || (K * PC_CG) % PC_KST || T <= 0 || pad < 0 || pad >= K) return -3;
-  // 2*TP rows per block, 4 row blocks per wave; clips longer than 256 frames in 256-frame chunks
-  // (blockIdx.z), each chunk's input window staged with its own pad-frame borders
-  const int tp = T > 256 ? 256 : ((T + 31) / 32) * 32;
-  switch (tp) {
-    case 32: return launch_tp<32>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
-    case 64: return launch_tp<64>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
-    case 96: return launch_tp<96>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
-    case 128: return launch_tp<128>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
-    case 160: return launch_tp<160>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
-    case 192: return launch_tp<192>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
-    case 224: return launch_tp<224>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
-    case 256: return launch_tp<256>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
+  if (G <= 0 || H % G || T <= 0 || pad < 0 || pad >= K) return -3;
+  switch (H / G) {
+    case 48: return launch_cg<48>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
+    case 64: return launch_cg<64>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
     default: return -3;
   }
 }

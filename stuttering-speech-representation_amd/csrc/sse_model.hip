@@ -1505,10 +1505,11 @@ int sse_model_create(const sse_cfg* cfg, const float* host_weights, size_t nbyte
       (dtype != SSE_DTYPE_F32 && dtype != SSE_DTYPE_BF16 && dtype != SSE_DTYPE_FP8 && dtype != SSE_DTYPE_FP16X3 &&
        dtype != SSE_DTYPE_FP16))
     return SSE_ERR_INVALID;
-  // fp16: WavLM whose every GEMM fits the 8-phase kernels and whose positional conv has 48-channel
-  // groups (the dedicated kernel; WavLM-base) -- the grouped-GEMM fallback has no fp16 form
+  // fp16: WavLM whose every GEMM fits the 8-phase kernels and whose positional conv has 48- or 64-channel
+  // groups (the dedicated kernel; WavLM-base / -large) -- the grouped-GEMM fallback has no fp16 form
   if (dtype == SSE_DTYPE_FP16 &&
-      (cfg->kind != SSE_KIND_WAVLM || cfg->hidden % 256 || cfg->ffn % 256 || cfg->hidden / cfg->pos_groups != 48))
+      (cfg->kind != SSE_KIND_WAVLM || cfg->hidden % 256 || cfg->ffn % 256 ||
+       (cfg->hidden / cfg->pos_groups != 48 && cfg->hidden / cfg->pos_groups != 64)))
     return SSE_ERR_UNSUPPORTED;
   // split-fp16: WavLM "group" frontend + post-LN encoder (WavLM-base); every GEMM N % 256 == 0
   if (dtype == SSE_DTYPE_FP16X3 &&

@@ -122,7 +122,7 @@ def test_edge_lengths(m32, wavlm_sd):
         m32.embed(torch.zeros((1, 399), device="cuda:0"), [12])    # shorter than the receptive field (T = 0)
 
 
-@pytest.mark.parametrize("dtype,tol", [("fp32", FP32_TOL), ("bf16", BF16_TOL)])
+@pytest.mark.parametrize("dtype,tol", [("fp32", FP32_TOL), ("bf16", BF16_TOL), ("fp16", 5e-3)])
 def test_wavlm_large_matches_reference(dtype, tol):
     """WavLM-large shape (layer-norm conv frontend, stable-LN encoder, do_normalize=True)."""
     import os
@@ -299,3 +299,25 @@ def test_two_stream_split_equals_one_stream(wavlm_sd, dtype):
     with _lib.option("no_split", 1):
         b = m.embed(w, idx, lengths=lens)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_wavlm_large_posconv_kernel_matches_grouped_gemm(dtype):
+    """WavLM-large's 64-channel positional-conv groups on the dedicated kernel (kernels_posconv.hip,
+    CG = 64) against the grouped GEMM (posconv_gemm=1; bf16 only -- the grouped GEMM has no fp16 form,
+    so fp16 is checked against the fp32 path), 3 s and 10 s clips (one chunk / 192-frame chunks)."""
+    from ssr_amd import _lib, config as C, synth
+    from ssr_amd.model import SSEModel
+    sd = synth.synth_wavlm_state_dict(C.WAVLM_LARGE, seed=9)
+    m = SSEModel(C.WAVLM_LARGE, sd, device="cuda:0", dtype=dtype)
+    for L in (48000, 160000):
+        w = torch.from_numpy(synth.synth_clips(3, L, seed=5)).cuda()
+        h0 = m.hidden_states(w[:1])[0].cpu().numpy()
+        if dtype == "bf16":
+            with _lib.option("posconv_gemm", 1):
+                g0 = m.hidden_states(w[:1])[0].cpu().numpy()
+            assert _rel(h0.reshape(-1), g0.reshape(-1)) <= 1e-5, L
+        else:
+            f0 = SSEModel(C.WAVLM_LARGE, sd, device="cuda:0", dtype="fp32").hidden_states(w[:1])[0].cpu().numpy()
+            assert _rel(h0.reshape(-1), f0.reshape(-1)) <= 5e-3, L
+
