@@ -301,11 +301,11 @@ def test_two_stream_split_equals_one_stream(wavlm_sd, dtype):
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+@pytest.mark.parametrize("dtype", ["fp16"])
 def test_wavlm_large_posconv_kernel_matches_grouped_gemm(dtype):
     """WavLM-large's 64-channel positional-conv groups on the dedicated kernel (kernels_posconv.hip,
-    CG = 64) against the grouped GEMM (posconv_gemm=1; bf16 only -- the grouped GEMM has no fp16 form,
-    so fp16 is checked against the fp32 path), 3 s and 10 s clips (one chunk / 192-frame chunks)."""
+    CG = 64; the fp16 path's only form -- bf16 keeps the grouped GEMM, measured faster there) against
+    the fp32 path, 3 s and 10 s clips (one chunk / 192-frame chunks)."""
     from ssr_amd import _lib, config as C, synth
     from ssr_amd.model import SSEModel
     sd = synth.synth_wavlm_state_dict(C.WAVLM_LARGE, seed=9)
