@@ -44,7 +44,7 @@ enum sse_kind { SSE_KIND_WAVLM = 0, SSE_KIND_WHISPER = 1 };
  * ~1/3 of the bf16 GEMM rate, with conv0, the positional conv and the attention core in exact fp32.
  * Activations must stay inside the fp16 range (|x| < 65504): a non-finite output is reported by
  * sse_check_range as SSE_ERR_RANGE. */
-/* SSE_DTYPE_FP16 (WavLM): the bf16 path's kernels and data flow with fp16 instead of bf16 activations,
+/* SSE_DTYPE_FP16 (WavLM-base / -large): the bf16 path's kernels and data flow with fp16 instead of bf16 activations,
  * weights and MFMA operands -- the same matrix-core rate, 8 more mantissa bits per operand (emulated
  * ideal-operand error on outlier-channel weights 0.017 rel-L2 vs 0.226 for bf16, oracle/emulate.py).
  * Range as FP16X3 (|x| < 65504, checked by sse_check_range). */
