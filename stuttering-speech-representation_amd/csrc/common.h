@@ -103,6 +103,26 @@ SSE_DEV f32x2 gelu_fast2(f32x2 x) {
   return x * __builtin_elementwise_fma(xc, p, f32x2{0.5f, 0.5f});
 }
 
+// GELU for a bf16 OUTPUT (round 3): the same clamped odd form at clamp 4.0 and degree 6 in xc^2
+// (tools/fit_gelu.py C_CLAMP = 4.0, DEG = 7; constant nudged by whole ulps so Phi(4) = 1 exactly in fp32),
+// max abs error 2.2e-4 -- 1/18 of the bf16 half-ulp at |y| = 1 -- for 2 fewer packed fma per pair than
+// gelu_fast2, which keeps the fp16 outputs (3 more mantissa bits: 7.3e-5 there is 1/7 of the half-ulp).
+SSE_DEV f32x2 gelu_bf2(f32x2 x) {
+  const f32x2 xc = {__builtin_amdgcn_fmed3f(x.x, -4.0f, 4.0f), __builtin_amdgcn_fmed3f(x.y, -4.0f, 4.0f)};
+  const f32x2 s = xc * xc;
+  f32x2 p = {2.368073737e-08f, 2.368073737e-08f};
+  p = __builtin_elementwise_fma(p, s, f32x2{-1.652635206e-06f, -1.652635206e-06f});
+  p = __builtin_elementwise_fma(p, s, f32x2{4.923747110e-05f, 4.923747110e-05f});
+  p = __builtin_elementwise_fma(p, s, f32x2{-8.292031125e-04f, -8.292031125e-04f});
+  p = __builtin_elementwise_fma(p, s, f32x2{8.865549229e-03f, 8.865549229e-03f});
+  p = __builtin_elementwise_fma(p, s, f32x2{-6.484667212e-02f, -6.484667212e-02f});
+  p = __builtin_elementwise_fma(p, s, f32x2{3.981720209e-01f, 3.981720209e-01f});
+  return x * __builtin_elementwise_fma(xc, p, f32x2{0.5f, 0.5f});
+}
+// the output's polynomial GELU: bf16 only -> gelu_bf2; fp16, fp32 or an fp32 copy (Cf) -> gelu_fast2
+template <bool H16> SSE_DEV f32x2 gelu_out2(f32x2 x) { return H16 ? gelu_fast2(x) : gelu_bf2(x); }
+SSE_DEV f32x2 gelu_out2(f32x2 x, bool bf_only) { return bf_only ? gelu_bf2(x) : gelu_fast2(x); }
+
 // GELU for an MX-fp8 output (the fc1 epilogue of the fp8 path, whose result is rounded to e4m3: 3
 // mantissa bits, half-step 3 %): the same clamped odd polynomial at degree 5 in xc^2 and clamp 3.5
 // (tools/fit_gelu.py C_CLAMP = 3.5, DEG = 6), max abs error 8.2e-4 -- 5 packed fma instead of 8.

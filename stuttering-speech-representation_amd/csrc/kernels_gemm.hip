@@ -293,7 +293,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
           o = f32x4{lo.x, lo.y, hi.x, hi.y};
         }
         if (gelu_fast) {
-          const f32x2 lo = gelu_fast2(f32x2{o[0], o[1]}), hi = gelu_fast2(f32x2{o[2], o[3]});
+          const bool bfo = !g.Cf;   // bf16-only output: the degree-6 form
+          const f32x2 lo = gelu_out2(f32x2{o[0], o[1]}, bfo), hi = gelu_out2(f32x2{o[2], o[3]}, bfo);
           o = f32x4{lo.x, lo.y, hi.x, hi.y};
         }
         o += rv[u];

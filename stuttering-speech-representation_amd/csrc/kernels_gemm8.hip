@@ -488,7 +488,8 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
           o = f32x4{lo.x, lo.y, hi.x, hi.y};
         }
         if (gelu_fast) {
-          const f32x2 lo = gelu_fast2(f32x2{o[0], o[1]}), hi = gelu_fast2(f32x2{o[2], o[3]});
+          const bool bfo = !g.Cf;   // bf16-only output: the degree-6 form
+          const f32x2 lo = gelu_out2(f32x2{o[0], o[1]}, bfo), hi = gelu_out2(f32x2{o[2], o[3]}, bfo);
           o = f32x4{lo.x, lo.y, hi.x, hi.y};
         }
         f32x4 r = rv[u];
@@ -611,8 +612,8 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
             o = f32x4{lo.x, lo.y, hi.x, hi.y};
           }
           if (gelu_fast) {   // fp8 out (Q8): the lower-degree form, its error far below e4m3 rounding
-            const f32x2 lo = Q8 ? gelu_fp8out2(f32x2{o[0], o[1]}) : gelu_fast2(f32x2{o[0], o[1]});
-            const f32x2 hi = Q8 ? gelu_fp8out2(f32x2{o[2], o[3]}) : gelu_fast2(f32x2{o[2], o[3]});
+            const f32x2 lo = Q8 ? gelu_fp8out2(f32x2{o[0], o[1]}) : gelu_out2(f32x2{o[0], o[1]}, !g.Cf);
+            const f32x2 hi = Q8 ? gelu_fp8out2(f32x2{o[2], o[3]}) : gelu_out2(f32x2{o[2], o[3]}, !g.Cf);
             o = f32x4{lo.x, lo.y, hi.x, hi.y};
           }
           if (has_res) {
@@ -760,7 +761,8 @@ SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, i
             const f32x2 lo = gelu_erf2(f32x2{o[0], o[1]}), hi = gelu_erf2(f32x2{o[2], o[3]});
             o = f32x4{lo.x, lo.y, hi.x, hi.y};
           } else if constexpr (ACT == ACT_GELU_FAST) {
-            const f32x2 lo = gelu_fast2(f32x2{o[0], o[1]}), hi = gelu_fast2(f32x2{o[2], o[3]});
+            // bf16-only output (the launcher sends a GELU_FAST GEMM with an fp32 copy to the staged kernel)
+            const f32x2 lo = gelu_out2<F16 || CT3>(f32x2{o[0], o[1]}), hi = gelu_out2<F16 || CT3>(f32x2{o[2], o[3]});
             o = f32x4{lo.x, lo.y, hi.x, hi.y};
           }
           acc[mi][ni][i][j] = o;
@@ -1400,7 +1402,9 @@ int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
       return hipGetLastError() == hipSuccess ? 0 : -2;
     }
   }
-  if (sse_opt(OPT_GEMM_NONPERSIST) && !a.resid_t && !a.f16 && !a.h16) {
+  // (a bf16 GELU_FAST GEMM with an fp32 copy too: the persistent kernel's bf16 GELU is the degree-6 form)
+  if ((sse_opt(OPT_GEMM_NONPERSIST) || (a.act == ACT_GELU_FAST && a.Cf && !a.resid && !a.resid_t)) && !a.resid_t &&
+      !a.f16 && !a.h16) {
     hipLaunchKernelGGL((gemm8_kernel<0, false, false>), grid, dim3(512), 0, s, a);
   } else if (a.resid_t) {
     // bf16 residual stream (folded post-LN path): bf16 out only

@@ -56,11 +56,19 @@ constexpr int K0 = 10;                   // conv0 kernel (WavLM)
 constexpr int NG = K0 * (K0 + 1) / 2;    // unique Gram entries
 constexpr int NMOM = K0 + NG;            // 65 moments per clip
 
+// One block per (clip, frame chunk): a clip's frames in MOM_NCH chunks, each block's partial moments
+// written to mom[b][chunk]; gn_finalize sums the chunks in chunk order (deterministic, and every clip's
+// result independent of the batch).  One block per clip walked ~38 dependent load rounds per thread
+// (latency-bound, 72 us at B = 128 while the GPU was otherwise idle at the step's start).
+constexpr int MOM_NCH = 8;
+
 __global__ __launch_bounds__(256) void conv0_moments_kernel(const float* __restrict__ x, int L,
                                                             const float* __restrict__ norm, int s0, int T0S,
                                                             double* __restrict__ mom, const int* __restrict__ t0len) {
-  const int b = blockIdx.x;
+  const int ch = blockIdx.x, b = blockIdx.y;
   const int T0 = t0len ? t0len[b] : T0S;
+  const int per = (T0S + MOM_NCH - 1) / MOM_NCH;
+  const int te = min(ch * per + per, T0);
   const float* xb = x + (long long)b * L;
   float mu = 0.f, rs = 1.f;
   if (norm) { mu = norm[2 * b]; rs = norm[2 * b + 1]; }
@@ -69,7 +77,8 @@ __global__ __launch_bounds__(256) void conv0_moments_kernel(const float* __restr
   for (int j = 0; j < K0; ++j) S[j] = 0.0;
   #pragma unroll
   for (int j = 0; j < NG; ++j) G[j] = 0.0;
-  for (int t = threadIdx.x; t < T0; t += 256) {
+  #pragma unroll 2
+  for (int t = ch * per + threadIdx.x; t < te; t += 256) {
     double w[K0];
     #pragma unroll
     for (int j = 0; j < K0; ++j) {
@@ -92,20 +101,59 @@ __global__ __launch_bounds__(256) void conv0_moments_kernel(const float* __restr
   }
   __syncthreads();
   if (threadIdx.x < NMOM)
-    mom[(long long)b * NMOM + threadIdx.x] =
+    mom[((long long)b * MOM_NCH + ch) * NMOM + threadIdx.x] =
         red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
 }
 
-__global__ void gn_finalize_kernel(const double* __restrict__ mom, int B, int C, int T0S,
-                                   const float* __restrict__ w0, const float* __restrict__ b0,
-                                   const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
-                                   float2* __restrict__ ss, const int* __restrict__ t0len) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B * C) return;
-  const int b = i / C, c = i - b * C;
+SSE_DEV void c0m_split(float v, bf16& h, bf16& l) {
+  h = (bf16)v;
+  l = (bf16)(v - (float)h);
+}
+
+// wf[cb][lane]: A fragment of channel block cb (16 channels) for lane (q, r16) of the matrix-core
+// conv0 (conv0_mfma_kernel): split-bf16 weights, the lane-group order of its B fragments
+SSE_DEV void conv0_wfrag(const float* __restrict__ w0, int i, bf16x8* __restrict__ wf) {
+  const int cb = i >> 6, lane = i & 63, q = lane >> 4, c = cb * 16 + (lane & 15);
+  bf16 h[K0], l[K0];
+  #pragma unroll
+  for (int j = 0; j < K0; ++j) c0m_split(w0[c * K0 + j], h[j], l[j]);
+  const bf16 z = (bf16)0.f;
+  bf16x8 f;
+  if (q == 0) f = bf16x8{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]};
+  else if (q == 1) f = bf16x8{h[8], h[9], h[0], h[1], h[2], h[3], h[4], h[5]};
+  else if (q == 2) f = bf16x8{h[6], h[7], h[8], h[9], l[0], l[1], l[2], l[3]};
+  else f = bf16x8{l[4], l[5], l[6], l[7], l[8], l[9], z, z};
+  wf[i] = f;
+}
+
+// grid (ceil(C / 256), B): the block's clip moments summed over the chunks (fixed order) into LDS, then
+// one (clip, channel) affine per thread; the blocks also write the matrix-core conv0's weight
+// fragments when wf is given (C / 16 x 64 lanes, one launch fewer)
+__global__ __launch_bounds__(256) void gn_finalize_kernel(const double* __restrict__ mom, int B, int C, int T0S,
+                                                          const float* __restrict__ w0, const float* __restrict__ b0,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float eps,
+                                                          float2* __restrict__ ss, const int* __restrict__ t0len,
+                                                          bf16x8* __restrict__ wf) {
+  const int b = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
+  if (wf) {
+    const int nb = gridDim.x * gridDim.y;
+    for (int i = (blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x; i < C / 16 * 64; i += nb * 256)
+      conv0_wfrag(w0, i, wf);
+  }
+  __shared__ double M[NMOM];
+  if (threadIdx.x < NMOM) {
+    const double* p = mom + (long long)b * MOM_NCH * NMOM + threadIdx.x;
+    double v = p[0];
+    #pragma unroll
+    for (int k = 1; k < MOM_NCH; ++k) v += p[k * NMOM];
+    M[threadIdx.x] = v;
+  }
+  __syncthreads();
+  if (c >= C) return;
   const int T0 = t0len ? t0len[b] : T0S;
-  const double* S = mom + (long long)b * NMOM;
-  const double* G = S + K0;
+  const double* S = M;
+  const double* G = M + K0;
   double w[K0];
   #pragma unroll
   for (int j = 0; j < K0; ++j) w[j] = w0[c * K0 + j];
@@ -124,7 +172,7 @@ __global__ void gn_finalize_kernel(const double* __restrict__ mom, int B, int C,
   const double mean = m0 + (b0 ? (double)b0[c] : 0.0);
   const float rstd = (float)(1.0 / sqrt(var + (double)eps));
   const float sc = gamma[c] * rstd;
-  ss[i] = make_float2(sc, beta[c] - (float)mean * sc);
+  ss[(long long)b * C + c] = make_float2(sc, beta[c] - (float)mean * sc);
 }
 
 // LNG (WavLM-large "layer" frontend, C == 512): the frame's 512 channels are exactly the wave's 64
@@ -220,7 +268,7 @@ __global__ __launch_bounds__(256) void conv0_apply_kernel(const float* __restric
           for (int p = 0; p < 4; ++p) {
             const f32x2 z = {fmaf((y[f][p].x - mean[f]) * rstd[f], gw[p].x, gb[p].x),
                              fmaf((y[f][p].y - mean[f]) * rstd[f], gw[p].y, gb[p].y)};
-            o[p] = FAST ? gelu_fast2(z) : gelu_erf2(z);
+            o[p] = FAST ? gelu_out2<!__is_same(TO, bf16)>(z) : gelu_erf2(z);
           }
           const long long row = (long long)(t + 4 * f) * C;
           if constexpr (sizeof(TO) == 2) {
@@ -246,7 +294,7 @@ __global__ __launch_bounds__(256) void conv0_apply_kernel(const float* __restric
         #pragma unroll
         for (int p = 0; p < 4; ++p) {
           const f32x2 z = __builtin_elementwise_fma(y[p], sc[p], sh[p]);
-          y[p] = FAST ? gelu_fast2(z) : gelu_erf2(z);
+          y[p] = FAST ? gelu_out2<!__is_same(TO, bf16)>(z) : gelu_erf2(z);
         }
       }
       if constexpr (sizeof(TO) == 2) {
@@ -271,29 +319,7 @@ __global__ __launch_bounds__(256) void conv0_apply_kernel(const float* __restric
 // MFMAs compute C^T (channels x frames), so a lane holds 4 consecutive channels of one frame; two
 // channel blocks per step and a v_permlane16_swap give every lane 8 consecutive bf16 = one 16-B store.
 constexpr int C0M_T = 32;
-constexpr int C0M_C = 512;               // channels of the matrix-core conv0 (conv0_wfrag_kernel fragments)                // frames per block (2 blocks of 16)
-
-SSE_DEV void c0m_split(float v, bf16& h, bf16& l) {
-  h = (bf16)v;
-  l = (bf16)(v - (float)h);
-}
-
-// wf[cb][lane]: A fragment of channel block cb (16 channels) for lane (q, r16)
-__global__ void conv0_wfrag_kernel(const float* __restrict__ w0, int C, bf16x8* __restrict__ wf) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= (C / 16) * 64) return;
-  const int cb = i >> 6, lane = i & 63, q = lane >> 4, c = cb * 16 + (lane & 15);
-  bf16 h[K0], l[K0];
-  #pragma unroll
-  for (int j = 0; j < K0; ++j) c0m_split(w0[c * K0 + j], h[j], l[j]);
-  const bf16 z = (bf16)0.f;
-  bf16x8 f;
-  if (q == 0) f = bf16x8{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]};
-  else if (q == 1) f = bf16x8{h[8], h[9], h[0], h[1], h[2], h[3], h[4], h[5]};
-  else if (q == 2) f = bf16x8{h[6], h[7], h[8], h[9], l[0], l[1], l[2], l[3]};
-  else f = bf16x8{l[4], l[5], l[6], l[7], l[8], l[9], z, z};
-  wf[i] = f;
-}
+constexpr int C0M_C = 512;               // channels of the matrix-core conv0 (conv0_wfrag fragments)
 
 // A block owns one clip and walks its 32-frame chunks (blockIdx.x, + gridDim.x, ...): the clip's
 // weights and GroupNorm affine stay in registers, the next chunk's waveform is fetched while this
@@ -366,8 +392,8 @@ __global__ __launch_bounds__(256) void conv0_mfma_kernel(const float* __restrict
       #pragma unroll
       for (int fb = 0; fb < C0M_T / 16; ++fb) {
         const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[i], xf[fb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        const f32x2 o0 = gelu_fast2(__builtin_elementwise_fma(f32x2{acc[0], acc[1]}, sc0[i], sh0[i]));
-        const f32x2 o1 = gelu_fast2(__builtin_elementwise_fma(f32x2{acc[2], acc[3]}, sc1[i], sh1[i]));
+        const f32x2 o0 = gelu_out2<!__is_same(TO, bf16)>(__builtin_elementwise_fma(f32x2{acc[0], acc[1]}, sc0[i], sh0[i]));
+        const f32x2 o1 = gelu_out2<!__is_same(TO, bf16)>(__builtin_elementwise_fma(f32x2{acc[2], acc[3]}, sc1[i], sh1[i]));
         *(uint2*)&tile[fb * 16 + r16][c] = pack_h4<is_f16_v<TO>>(f32x4{o0.x, o0.y, o1.x, o1.y});
       }
     }
@@ -377,8 +403,10 @@ __global__ __launch_bounds__(256) void conv0_mfma_kernel(const float* __restrict
   }
 }
 
-// moments [B][NMOM] fp64 | the matrix-core conv0's weight fragments (C0M_C / 16 x 64 lanes x 16 B)
-size_t conv0_moments_bytes(int B) { return ((size_t)B * NMOM * sizeof(double) + 255) / 256 * 256 + C0M_C / 16 * 64 * 16; }
+// moments [B][MOM_NCH][NMOM] fp64 | the matrix-core conv0's weight fragments (C0M_C / 16 x 64 lanes x 16 B)
+size_t conv0_moments_bytes(int B) {
+  return ((size_t)B * MOM_NCH * NMOM * sizeof(double) + 255) / 256 * 256 + C0M_C / 16 * 64 * 16;
+}
 
 
 template <typename TO>
@@ -386,16 +414,17 @@ int launch_conv0_gn(const float* x, int B, int L, const float* norm, const float
                     int C, int k0, int s0, int T0, const float* gamma, const float* beta, float eps,
                     double* mom, float2* ss, TO* out, hipStream_t s, const int* t0len) {
   if (k0 != K0 || s0 != 5) return -3;
-  hipLaunchKernelGGL(conv0_moments_kernel, dim3(B), dim3(256), 0, s, x, L, norm, s0, T0, mom, t0len);
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3((B * C + 255) / 256), dim3(256), 0, s, mom, B, C, T0, w0, b0, gamma,
-                     beta, eps, ss, t0len);
   if (C % 8) return -3;
   dim3 grid((T0 + C0_T - 1) / C0_T, B), block(256);
   const bool valu = sse_opt(OPT_CONV0_VALU) != 0;   // A/B and tests: the VALU kernel below
   // matrix-core conv0: C == C0M_C channels, whose weight fragments conv0_moments_bytes reserves
-  if (sizeof(TO) == 2 && !gelu_exact_env() && C == C0M_C && !valu) {
-    bf16x8* wf = (bf16x8*)((char*)mom + ((size_t)B * NMOM * sizeof(double) + 255) / 256 * 256);
-    hipLaunchKernelGGL(conv0_wfrag_kernel, dim3((C / 16 * 64 + 255) / 256), dim3(256), 0, s, w0, C, wf);
+  const bool mfma = sizeof(TO) == 2 && !gelu_exact_env() && C == C0M_C && !valu;
+  bf16x8* wf = mfma ? (bf16x8*)((char*)mom + ((size_t)B * MOM_NCH * NMOM * sizeof(double) + 255) / 256 * 256)
+                    : nullptr;
+  hipLaunchKernelGGL(conv0_moments_kernel, dim3(MOM_NCH, B), dim3(256), 0, s, x, L, norm, s0, T0, mom, t0len);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3((C + 255) / 256, B), dim3(256), 0, s, mom, B, C, T0, w0, b0, gamma,
+                     beta, eps, ss, t0len, wf);
+  if (mfma) {
     // 3 resident blocks per CU (168 VGPRs): spread each clip's chunks over G blocks, G * B ~ 3 * CUs
     static int cus[64] = {0};
     int dev = 0;
@@ -631,7 +660,7 @@ __global__ __launch_bounds__(256) void layernorm_bf16_rows_kernel(const bf16* __
     if (act != ACT_NONE) {
       #pragma unroll
       for (int e = 0; e < 8; e += 2) {
-        const f32x2 g2 = act == ACT_GELU ? gelu_erf2(f32x2{y[e], y[e + 1]}) : gelu_fast2(f32x2{y[e], y[e + 1]});
+        const f32x2 g2 = act == ACT_GELU ? gelu_erf2(f32x2{y[e], y[e + 1]}) : gelu_out2<H16>(f32x2{y[e], y[e + 1]});
         y[e] = g2.x;
         y[e + 1] = g2.y;
       }
@@ -955,19 +984,21 @@ int launch_mx_quantize(const float* x, int R, int K, int role, unsigned char* q,
 
 // ---------------------------------------------------------------------------------------
 // K8/K12: out[b*out_stride + n] = mean_t x[b][t][n]  (torch.mean(hs, dim=1), fp64 accumulation).
-// Block = (256 columns, clip), 4 waves; lane owns 4 consecutive columns (16-B loads, one 1 KiB row
-// piece per wave-instruction), wave w sums frames t = w, w+4, ... with 4 frames' loads in flight,
-// then an LDS combine.  With per-row LayerNorm statistics (st: (mean, rstd); or lpart: per-256-column
+// Block = (256 columns, clip), POOL_W = 16 waves; lane owns 4 consecutive columns (16-B loads, one
+// 1 KiB row piece per wave-instruction), wave w sums frames t = w, w+16, ... with 4 frames' loads in
+// flight, then an LDS combine in wave order (4 waves walked ~9 dependent load rounds per 149-frame
+// clip: 27 us per launch at B = 128, 7x the HBM time of its bytes).  With per-row LayerNorm statistics (st: (mean, rstd); or lpart: per-256-column
 // partials, ln_part_stats), each element is first normalised exactly as layernorm_kernel would have
 // written it; the clip's per-frame statistics are formed once into LDS.
 constexpr int POOL_TMAX = 1024;   // frames whose statistics fit the LDS table (longer clips: per-frame loads)
+constexpr int POOL_W = 16;
 template <typename TI>
-__global__ __launch_bounds__(256) void pool_mean_kernel(const TI* __restrict__ x, int T, int H,
+__global__ __launch_bounds__(64 * POOL_W) void pool_mean_kernel(const TI* __restrict__ x, int T, int H,
                                                         float* __restrict__ out, long long out_stride,
                                                         const float2* __restrict__ st, const float* __restrict__ w,
                                                         const float* __restrict__ bb, const float2* __restrict__ lpart,
                                                         int nt, float eps, const int* __restrict__ tlen) {
-  __shared__ double part[4][256];
+  __shared__ double part[POOL_W][256];
   __shared__ float2 fst[POOL_TMAX];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int n = blockIdx.x * 256 + lane * 4, b = blockIdx.y;
@@ -976,7 +1007,7 @@ __global__ __launch_bounds__(256) void pool_mean_kernel(const TI* __restrict__ x
   const bool ln = st || lpart;
   const bool tab = ln && T <= POOL_TMAX;
   if (tab) {
-    for (int t = threadIdx.x; t < T; t += 256)
+    for (int t = threadIdx.x; t < T; t += 64 * POOL_W)
       fst[t] = st ? st[(long long)b * TS + t] : ln_part_stats(lpart, nt, (long long)b * TS + t, eps);
     __syncthreads();
   }
@@ -997,15 +1028,16 @@ __global__ __launch_bounds__(256) void pool_mean_kernel(const TI* __restrict__ x
       s3 += v[3];
     };
     int t = wv;
-    for (; t + 12 < T; t += 16) {   // 4 frames of this wave in flight
-      const f32x4 v0 = load4<TI>(xb + (long long)t * H), v1 = load4<TI>(xb + (long long)(t + 4) * H);
-      const f32x4 v2 = load4<TI>(xb + (long long)(t + 8) * H), v3 = load4<TI>(xb + (long long)(t + 12) * H);
+    constexpr int W = POOL_W;
+    for (; t + 3 * W < T; t += 4 * W) {   // 4 frames of this wave in flight
+      const f32x4 v0 = load4<TI>(xb + (long long)t * H), v1 = load4<TI>(xb + (long long)(t + W) * H);
+      const f32x4 v2 = load4<TI>(xb + (long long)(t + 2 * W) * H), v3 = load4<TI>(xb + (long long)(t + 3 * W) * H);
       add(v0, t);
-      add(v1, t + 4);
-      add(v2, t + 8);
-      add(v3, t + 12);
+      add(v1, t + W);
+      add(v2, t + 2 * W);
+      add(v3, t + 3 * W);
     }
-    for (; t < T; t += 4) add(load4<TI>(xb + (long long)t * H), t);
+    for (; t < T; t += W) add(load4<TI>(xb + (long long)t * H), t);
   }
   part[wv][lane * 4 + 0] = s0;
   part[wv][lane * 4 + 1] = s1;
@@ -1015,7 +1047,12 @@ __global__ __launch_bounds__(256) void pool_mean_kernel(const TI* __restrict__ x
   const int c = threadIdx.x, nc = blockIdx.x * 256 + c;
   // a clip with no frames (ragged batch, shorter than the receptive field) pools to zeros, never
   // 0/0; the host wrapper rejects such clips before the call (SSEModel.embed)
-  if (nc < H) out[b * out_stride + nc] = T > 0 ? (float)((part[0][c] + part[1][c] + part[2][c] + part[3][c]) / T) : 0.f;
+  if (c < 256 && nc < H) {
+    double v = part[0][c];
+    #pragma unroll
+    for (int k = 1; k < POOL_W; ++k) v += part[k][c];
+    out[b * out_stride + nc] = T > 0 ? (float)(v / T) : 0.f;
+  }
 }
 
 template <typename TI>
@@ -1023,7 +1060,7 @@ int launch_pool_mean(const TI* x, int B, int T, int H, float* out, long long out
                      const float2* st, const float* w, const float* b, const float2* part, int nt, float eps,
                      const int* tlen) {
   if (H % 4) return -3;
-  hipLaunchKernelGGL(pool_mean_kernel<TI>, dim3((H + 255) / 256, B), dim3(256), 0, s, x, T, H, out, out_stride, st, w,
+  hipLaunchKernelGGL(pool_mean_kernel<TI>, dim3((H + 255) / 256, B), dim3(64 * POOL_W), 0, s, x, T, H, out, out_stride, st, w,
                      b, part, nt, eps, tlen);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -113,6 +113,43 @@ def test_fast_gelu_pointwise():
     assert (got[neg].abs() <= 1e-7 * xe[neg].abs()).all()              # Phi(-4.5) = 3e-8
 
 
+def test_fast_gelu_pointwise_bf16_out():
+    """A bf16-only output takes the degree-6 form (common.h gelu_bf2: clamp 4, max abs error 2.2e-4,
+    1/18 of the bf16 half-ulp at |y| = 1): every bf16 x in [-12, 12] through the persistent GEMM
+    (b = 1 in one K column, so the pre-activation is x exactly) against the fp32 restatement below
+    (fused multiply-adds as on the GPU), rounded to bf16 -- equal up to one bf16 step where the fp64
+    emulation of an fp32 fma double-rounds -- and against fp64 erf within the fit error plus half a
+    bf16 ulp."""
+    from ssr_amd.model import gemm
+    x = torch.unique(torch.linspace(-12, 12, 1 << 20).bfloat16().float())
+    M = x.numel()
+    a = torch.zeros(M, 64, dtype=torch.bfloat16)
+    a[:, 0] = x.bfloat16()
+    b = torch.zeros(256, 64, dtype=torch.bfloat16)
+    b[:, 0] = 1.0
+    got = gemm(a.cuda(), b.cuda(), None, None, "gelu_fast", out_dtype=torch.bfloat16)[:, 0].float().cpu()
+    c = [2.368073737e-08, -1.652635206e-06, 4.923747110e-05, -8.292031125e-04, 8.865549229e-03,
+         -6.484667212e-02, 3.981720209e-01]
+
+    def fma32(a, b, d):   # fp32 fused multiply-add: the fp64 product of two fp32 values is exact
+        return (a.double() * b.double() + d.double()).float()
+
+    xc = x.clamp(-4.0, 4.0)
+    s = xc * xc
+    p = torch.full_like(x, c[0])
+    for k in c[1:]:
+        p = fma32(p, s, torch.full_like(x, k))
+    poly = (x * fma32(xc, p, torch.full_like(x, 0.5))).bfloat16().float()
+    step = (got.view(torch.int32) - poly.view(torch.int32)).abs() >> 16   # bf16 code distance
+    step[got == poly] = 0                                                  # -0 == +0
+    assert (step <= 1).all() and (step == 0).float().mean().item() >= 0.999
+    xd = x.double()
+    ref = xd * 0.5 * (1.0 + torch.erf(xd / 2 ** 0.5))
+    half_ulp = torch.ldexp(torch.ones_like(ref), torch.frexp(ref.abs())[1] - 9)   # bf16: 8 mantissa bits
+    assert ((got.double() - ref).abs() <= 2.2e-4 + half_ulp).all()
+    assert torch.equal(got[x > 4.0], x[x > 4.0])   # Phi(4) = 1 exactly
+
+
 @pytest.mark.parametrize("M,N,K", [(16421, 1024, 64), (16421, 1024, 128), (16421, 768, 192), (16384, 1024, 256),
                                    (16421, 1024, 768), (9000, 2560, 768), (300, 512, 512)])
 @pytest.mark.parametrize("epi", ["plain", "bias_gelu_fast", "bias_f32_and_bf16"])
