@@ -78,6 +78,15 @@ def emulated_product(fn, x: torch.Tensor, w: torch.Tensor, fmt: str) -> torch.Te
         wm = _ftz16(_f16(wh / 2048.0))
         wl = _ftz16(_f16(ws - wh))
         return (fn(xh, wh) + fn(xl, wm) + fn(xh, wl)) / s
+    if fmt in ("fp16x2a", "fp16x2w"):   # two products: split activations (a) or split weights (w)
+        s = _pow2_scale(w)
+        ws = w * s
+        xh = _ftz16(_f16(x))
+        wh = _ftz16(_f16(ws))
+        if fmt == "fp16x2a":
+            xl = _ftz16(_f16((x - xh) * 2048.0))
+            return (fn(xh, wh) + fn(xl, _ftz16(_f16(wh / 2048.0)))) / s
+        return (fn(xh, wh) + fn(xh, _ftz16(_f16(ws - wh)))) / s
     raise ValueError(fmt)
 
 

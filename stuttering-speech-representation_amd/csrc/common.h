@@ -219,6 +219,7 @@ enum {
   OPT_NO_SPLIT,         // 1: WavLM batches run as one stream (no two-stream half-batch split)
   OPT_LOGMEL_V1,        // 1: the round-2 log-mel kernel (one frame per wave) instead of 4 frames per wave
   OPT_SPLIT_PARTS,      // 3 or 4: WavLM batches split into that many streams (default 2)
+  OPT_LN_X3_V1,         // 1: the one-row-per-wave split-fp16 LayerNorm (A/B, bit-identity test)
   OPT_COUNT
 };
 int sse_opt(int id);

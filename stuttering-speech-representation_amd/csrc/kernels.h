@@ -39,6 +39,9 @@ int launch_layernorm(const TI* in, const float* w, const float* b, int rows, int
 int launch_layernorm_x3(const void* in, bool in3, const float* w, const float* b, int rows, int H, float eps,
                         float* out_f, f16* out3, hipStream_t s);
 int launch_split3(const float* x, long long rows, int C, f16* y, hipStream_t s);
+int launch_conv0_gn_x3(const float* x, int B, int L, const float* norm, const float* w0, const float* b0, int C,
+                       int k0, int s0, int T0, const float* gamma, const float* beta, float eps, double* mom,
+                       float2* ss, f16* out3, hipStream_t s, const int* t0len);
 
 // MX-fp8 (e4m3 + E8M0 per 32 K-elements) GEMM operands, layouts in common.h
 template <typename TI>

@@ -179,7 +179,9 @@ __global__ __launch_bounds__(256) void gn_finalize_kernel(const double* __restri
 // lanes x 8, so LayerNorm over channels (layernorm_kernel's expression, statistics from the fp32
 // conv values) and GELU are applied before the single store -- no second pass over the
 // [B][T0][512] activation.
-template <typename TO, bool RAW, bool FAST, bool LNG = false>
+// OUT3 (split-fp16 path, TO = float): the fp32 result written as tripled f16 rows [hi | lo' | hi] of 3C
+// (x3_split4) -- the conv1 GEMM's operand, no fp32 [B][T0][C] round trip through split3.
+template <typename TO, bool RAW, bool FAST, bool LNG = false, bool OUT3 = false>
 __global__ __launch_bounds__(256) void conv0_apply_kernel(const float* __restrict__ x, int L,
                                                           const float* __restrict__ norm,
                                                           const float* __restrict__ w0, const float* __restrict__ b0,
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(256) void conv0_apply_kernel(const float* __restric
         gb[p] = f32x2{lnb[c0], lnb[c0 + 1]};
       }
     }
-    TO* ob = out + ((long long)b * T0 + t0) * C + c;
+    TO* ob = out + ((long long)b * T0 + t0) * C + c;   // (OUT3 stores address the tripled rows below)
     if constexpr (LNG) {
       // two frames (t, t + 4) per trip: their reduction chains (DPP / permlane, each step dependent
       // on the previous) interleave instead of stalling one after the other
@@ -297,7 +299,16 @@ __global__ __launch_bounds__(256) void conv0_apply_kernel(const float* __restric
           y[p] = FAST ? gelu_out2<!__is_same(TO, bf16)>(z) : gelu_erf2(z);
         }
       }
-      if constexpr (sizeof(TO) == 2) {
+      if constexpr (OUT3) {
+        f16x4 h0, l0, h1, l1;
+        x3_split4(f32x4{y[0].x, y[0].y, y[1].x, y[1].y}, h0, l0);
+        x3_split4(f32x4{y[2].x, y[2].y, y[3].x, y[3].y}, h1, l1);
+        f16* o3 = (f16*)(void*)out + ((long long)b * T0 + t0 + t) * 3 * C + c;
+        const f16x8 h = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        *(f16x8*)o3 = h;
+        *(f16x8*)(o3 + C) = f16x8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+        *(f16x8*)(o3 + 2 * C) = h;
+      } else if constexpr (sizeof(TO) == 2) {
         *(uint4*)(ob + (long long)t * C) = pack_h8<is_f16_v<TO>>(f32x4{y[0].x, y[0].y, y[1].x, y[1].y},
                                                                    f32x4{y[2].x, y[2].y, y[3].x, y[3].y});
       } else {
@@ -440,6 +451,19 @@ int launch_conv0_gn(const float* x, int B, int L, const float* norm, const float
     hipLaunchKernelGGL((conv0_apply_kernel<TO, false, true>), grid, block, 0, s, x, L, norm, w0, b0, C, T0, ss, out);
   else
     hipLaunchKernelGGL((conv0_apply_kernel<TO, false, false>), grid, block, 0, s, x, L, norm, w0, b0, C, T0, ss, out);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// split-fp16 path: conv0 + GroupNorm + erf-GELU in fp32, written as tripled f16 rows (OUT3)
+int launch_conv0_gn_x3(const float* x, int B, int L, const float* norm, const float* w0, const float* b0, int C,
+                       int k0, int s0, int T0, const float* gamma, const float* beta, float eps, double* mom,
+                       float2* ss, f16* out3, hipStream_t s, const int* t0len) {
+  if (k0 != K0 || s0 != 5 || C % 8) return -3;
+  hipLaunchKernelGGL(conv0_moments_kernel, dim3(MOM_NCH, B), dim3(256), 0, s, x, L, norm, s0, T0, mom, t0len);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3((C + 255) / 256, B), dim3(256), 0, s, mom, B, C, T0, w0, b0, gamma,
+                     beta, eps, ss, t0len, (bf16x8*)nullptr);
+  hipLaunchKernelGGL((conv0_apply_kernel<float, false, false, false, true>), dim3((T0 + C0_T - 1) / C0_T, B),
+                     dim3(256), 0, s, x, L, norm, w0, b0, C, T0, ss, (float*)out3);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -692,12 +716,79 @@ int launch_layernorm(const TI* in, const float* w, const float* b, int rows, int
 template int launch_layernorm<float, float>(const float*, const float*, const float*, int, int, float, int,
                                             float*, float*, hipStream_t, float2*);
 
+// split-fp16 LayerNorm of fp32 rows, H = 256 NI: R rows per wave with every load issued first (the
+// one-row-per-wave layernorm_kernel keeps 3 KiB in flight per wave and ran at ~1.3 TB/s on the
+// fp16x3 path's 50 launches per step); the same per-lane sums, wave_sum and expressions as
+// layernorm_kernel<float, f16, false, true>, so the outputs are bit-identical to it.
+template <int R, int NI>
+__global__ __launch_bounds__(256) void layernorm_x3_rows_kernel(const float* __restrict__ in, const float* __restrict__ w,
+                                                                const float* __restrict__ bta, int rows, float eps,
+                                                                float* __restrict__ out_f, f16* __restrict__ out3) {
+  constexpr int H = NI * 256;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long long r0 = ((long long)blockIdx.x * 4 + wave) * R;
+  f32x4 v[R][NI];
+  #pragma unroll
+  for (int i = 0; i < R; ++i)
+    #pragma unroll
+    for (int k = 0; k < NI; ++k)
+      v[i][k] = r0 + i < rows ? *(const f32x4*)(in + (r0 + i) * H + 4 * (lane + 64 * k)) : f32x4{0.f, 0.f, 0.f, 0.f};
+  float mean[R], rstd[R];
+  #pragma unroll
+  for (int i = 0; i < R; ++i) {
+    float sm = 0.f;
+    #pragma unroll
+    for (int k = 0; k < NI; ++k) sm += v[i][k][0] + v[i][k][1] + v[i][k][2] + v[i][k][3];
+    mean[i] = sm;
+  }
+  #pragma unroll
+  for (int i = 0; i < R; ++i) mean[i] = wave_sum(mean[i]) / H;
+  #pragma unroll
+  for (int i = 0; i < R; ++i) {
+    float q = 0.f;
+    #pragma unroll
+    for (int k = 0; k < NI; ++k)
+      #pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = v[i][k][e] - mean[i];
+        q = fmaf(d, d, q);
+      }
+    rstd[i] = q;
+  }
+  #pragma unroll
+  for (int i = 0; i < R; ++i) rstd[i] = 1.0f / sqrtf(wave_sum(rstd[i]) / H + eps);
+  #pragma unroll
+  for (int k = 0; k < NI; ++k) {
+    const int c = 4 * (lane + 64 * k);
+    const f32x4 wv = *(const f32x4*)(w + c), bv = *(const f32x4*)(bta + c);
+    #pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const long long row = r0 + i;
+      if (row >= rows) break;
+      f32x4 o;
+      #pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = fmaf((v[i][k][e] - mean[i]) * rstd[i], wv[e], bv[e]);   // = ln_apply4
+      if (out_f) *(f32x4*)(out_f + row * H + c) = o;
+      f16x4 hi, lo;
+      x3_split4(o, hi, lo);
+      f16* o3 = out3 + row * 3 * H + c;
+      *(f16x4*)o3 = hi;
+      *(f16x4*)(o3 + H) = lo;
+      *(f16x4*)(o3 + 2 * H) = hi;
+    }
+  }
+}
+
 // split-fp16 LayerNorm: input fp32 [rows][H] or tripled f16 [rows][3H] (in3), output fp32 (optional)
 // and tripled f16 [rows][3H]
 int launch_layernorm_x3(const void* in, bool in3, const float* w, const float* b, int rows, int H, float eps,
                         float* out_f, f16* out3, hipStream_t s) {
   if (H % 4 || H > 2048 || !out3) return -3;
-  if (in3)
+  constexpr int R = 4;
+  if (!in3 && H == 768 && !sse_opt(OPT_LN_X3_V1))
+    hipLaunchKernelGGL((layernorm_x3_rows_kernel<R, 3>), dim3((rows + 4 * R - 1) / (4 * R)), dim3(256), 0, s,
+                       (const float*)in, w, b, rows, eps, out_f, out3);
+  else if (in3)
     hipLaunchKernelGGL((layernorm_kernel<f16, f16, true, true>), dim3((rows + 3) / 4), dim3(256), 0, s,
                        (const f16*)in, w, b, rows, H, eps, (int)ACT_NONE, out_f, out3, (float2*)nullptr);
   else

@@ -34,7 +34,7 @@
 static int g_opt[OPT_COUNT] = {0};
 static const char* const g_opt_name[OPT_COUNT] = {"gemm_cfg", "gemm_nonpersist", "gelu_exact", "conv0_valu",
                                                    "posconv_gemm", "no_lnfold", "gemm_mx_staged", "no_split",
-                                                   "logmel_v1", "split_parts"};
+                                                   "logmel_v1", "split_parts", "ln_x3_v1"};
 int sse_opt(int id) { return __atomic_load_n(&g_opt[id], __ATOMIC_RELAXED); }
 
 namespace {
@@ -978,7 +978,7 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
 // positional conv and the attention core (scores, softmax, P.V) run in exact fp32 as in the fp32
 // path; LayerNorms read / write fp32 and tripled rows.
 struct X3Ws {
-  size_t zero, norm, part, ss, c0, bufA, bufB, x, xt, xb, qkv, ctx3, ff, fr;
+  size_t zero, norm, part, ss, bufA, bufB, x, xt, xb, qkv, ctx3, ff, fr;
 };
 
 X3Ws x3_plan(const sse_model* m, int B, int L, Plan& p) {
@@ -998,7 +998,6 @@ X3Ws x3_plan(const sse_model* m, int B, int L, Plan& p) {
   w.norm = p.add((size_t)B * 8);
   w.part = p.add(conv0_moments_bytes(B));
   w.ss = p.add((size_t)B * C0 * 8);
-  w.c0 = p.add((size_t)B * Ts[0] * C0 * 4);
   w.bufA = p.add(maxA);
   w.bufB = p.add(maxB);
   w.x = p.add(M * H * 4);
@@ -1042,14 +1041,12 @@ int wavlm_forward_x3(sse_model* m, const float* wave, int B, int L, const Sink& 
   };
   // ---- conv feature encoder: conv0 + GroupNorm + GELU in fp32, then tripled ----
   const int C0 = c.conv_dim[0];
-  float* c0 = (float*)(ws + w.c0);
   const float* b0 = m->conv_b[0] ? m->ptr<float>(m->conv_b[0]) : nullptr;
   f16* bufs[2] = {(f16*)(ws + w.bufA), (f16*)(ws + w.bufB)};
   RC(prof(m, s, "conv0_gn", 2.0 * B * (double)Ts[0] * C0 * c.conv_kernel[0], 0, [&] {
-    return launch_conv0_gn<float>(wave, B, L, norm, m->ptr<float>(m->conv_w[0]), b0, C0, c.conv_kernel[0],
-                                  c.conv_stride[0], Ts[0], m->ptr<float>(m->conv_ln_w[0]), m->ptr<float>(m->conv_ln_b[0]),
-                                  1e-5f, (double*)(ws + w.part), (float2*)(ws + w.ss), c0, s, t0len); }));
-  RC(launch_split3(c0, (long long)B * Ts[0], C0, bufs[0], s));
+    return launch_conv0_gn_x3(wave, B, L, norm, m->ptr<float>(m->conv_w[0]), b0, C0, c.conv_kernel[0],
+                              c.conv_stride[0], Ts[0], m->ptr<float>(m->conv_ln_w[0]), m->ptr<float>(m->conv_ln_b[0]),
+                              1e-5f, (double*)(ws + w.part), (float2*)(ws + w.ss), bufs[0], s, t0len); }));
   for (int i = 1; i < c.n_conv; ++i) {
     const int cin = c.conv_dim[i - 1], co = c.conv_dim[i], k = c.conv_kernel[i], st = c.conv_stride[i];
     GemmArgs g{};

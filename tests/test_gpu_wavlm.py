@@ -279,6 +279,23 @@ def test_fp16x3_normalize_and_batch_invariance(wavlm_sd, golden_wavlm):
         assert torch.equal(full[i:i + 1], m.embed(w[i:i + 1], idx))
 
 
+def test_fp16x3_multirow_layernorm_is_bit_identical(mx3):
+    """The R-rows-per-wave split-fp16 LayerNorm (layernorm_x3_rows_kernel) against the one-row-per-wave
+    kernel it replaced (option ln_x3_v1): the same sums and expressions, so embeddings and every hidden
+    state agree bit for bit (17 clips: a ragged last block of rows)."""
+    from ssr_amd import _lib, synth
+    w = torch.from_numpy(synth.synth_clips(17, 48000, seed=21)).cuda()
+    idx = [12, 7, 0]
+    new = mx3.embed(w, idx)
+    hs_new = mx3.hidden_states(w[:3])
+    with _lib.option("ln_x3_v1", 1):
+        old = mx3.embed(w, idx)
+        hs_old = mx3.hidden_states(w[:3])
+    assert torch.equal(new, old)
+    for a, b in zip(hs_new, hs_old):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "fp16x3", "fp16"])
 def test_two_stream_split_equals_one_stream(wavlm_sd, dtype):
     """Batches of >= 128 WavLM clips run as two half-batches on two streams (split_forward): bit-identical
