@@ -50,6 +50,9 @@ int launch_layernorm_mx(const TI* in, const float* w, const float* b, int rows, 
 int launch_mx_quantize(const float* x, int R, int K, int role, unsigned char* q, unsigned char* scale, hipStream_t s);
 
 // kernels_posconv.hip: WavLM positional conv (bf16 path); -3 = shape not covered (use the GEMM)
+// split-fp16 positional conv (SSE_DTYPE_FP16X3): fp32 xt / x, W = planes [wh][wl] of w / alpha
+int launch_posconv_x3(const float* xt, const f16* W, float alpha, const float* bias, float* x, int B, int T, int H,
+                      int G, int K, int pad, hipStream_t s);
 int launch_posconv_bf16(const bf16* xt, const bf16* W, const float* bias, float* x, int B, int T, int H, int G, int K,
                         int pad, hipStream_t s, bool h16 = false);   // h16: xt / W are fp16
 

@@ -173,7 +173,184 @@ int launch_cg(const bf16* xt, const bf16* W, const float* bias, float* x, int B,
   }
 }
 
+// ---- split-fp16 (SSE_DTYPE_FP16X3) form, 48-channel groups ----
+// The fp32 path's conv on the fp16 matrix cores: the input window is split while it is staged
+// (x = xh + xl' 2^-11, x3_split4: xt stays fp32 in HBM), the weights are two planes [wh | wl] of
+// w 2^e (Arena put_pos_x3), and per K step
+//   acc1 += wh xh + wl xh,   acc2 += wh xl'
+// out = (acc1 + acc2 2^-11) 2^-e: the three products of the split GEMMs (the dropped wl xl' is
+// ~2^-22 relative), with the lo-activation term in its own accumulator instead of a wh 2^-11 weight
+// plane.  LDS at TP = 160: two clips' hi + lo windows (2 x 55 KiB) + two double-buffered weight
+// planes (48 KiB) = 156 KiB, so longer clips go in 160-frame chunks (blockIdx.z).
+constexpr int PX_CG = 48;
+
+template <int TP>
+__global__ __launch_bounds__(64 * (2 * TP / 64)) void posconv_x3_kernel(const float* __restrict__ xt, const f16* __restrict__ W,
+                                                                       float alpha, const float* __restrict__ bias,
+                                                                       float* __restrict__ x, int B, int T, int H, int K,
+                                                                       int pad) {
+  constexpr int NW = 2 * TP / 64;
+  constexpr int NT = 64 * NW;
+  constexpr int CG = PX_CG, NCB = CG / 16;
+  constexpr int PSTAGE = CG * PC_KST * 2;         // one plane of one stage: 12 KiB
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int WF = TP + K - 1;
+  const int WIN = (2 * WF * CG * 2 + 15) & ~15;   // one window plane (both clips)
+  char* winh = smem;
+  char* winl = smem + WIN;
+  char* wst = smem + 2 * WIN;                     // [buf][plane h, l][cg][PC_KST] f16, swizzled
+  const int grp = blockIdx.y, b0 = blockIdx.x * 2;
+  const int f0 = blockIdx.z * TP;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane >> 4, r16 = lane & 15;
+  const int Ktot = K * CG, nst = Ktot / PC_KST;
+  const long long plane = (long long)H * Ktot;
+  const f16* wg = W + (long long)grp * CG * Ktot;
+
+  constexpr int WCH = CG * (PC_KST / 8);
+  constexpr int WIT = (WCH + NT - 1) / NT;
+  f16x8 wrh[WIT], wrl[WIT];
+  auto load_w = [&](int st) {
+    #pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      const int i = tid + it * NT;
+      if (i < WCH) {
+        const long long o = (long long)(i >> 4) * Ktot + st * PC_KST + (i & 15) * 8;
+        wrh[it] = *(const f16x8*)(wg + o);
+        wrl[it] = *(const f16x8*)(wg + plane + o);
+      }
+    }
+  };
+  auto store_w = [&](int buf) {
+    #pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      const int i = tid + it * NT;
+      const int row = i >> 4, ch = i & 15;
+      if (i < WCH) {
+        char* d = wst + buf * 2 * PSTAGE + row * (PC_KST * 2) + ((ch ^ (row & 15)) * 16);
+        *(f16x8*)d = wrh[it];
+        *(f16x8*)(d + PSTAGE) = wrl[it];
+      }
+    }
+  };
+
+  load_w(0);
+  {
+    constexpr int CPF = CG / 8;
+    const int n16 = 2 * WF * CPF;
+    for (int i = tid; i < n16; i += NT) {
+      const int c = i / (WF * CPF), r = i - c * WF * CPF, f = r / CPF, ch = r - f * CPF;
+      const int tt = f0 + f - pad, b = b0 + c;
+      f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0;
+      if (b < B && tt >= 0 && tt < T) {
+        const float* src = xt + ((long long)b * T + tt) * H + grp * CG + ch * 8;
+        v0 = *(const f32x4*)src;
+        v1 = *(const f32x4*)(src + 4);
+      }
+      f16x4 h0, l0, h1, l1;
+      x3_split4(v0, h0, l0);
+      x3_split4(v1, h1, l1);
+      const int o = ((c * WF + f) * CG + ch * 8) * 2;
+      *(f16x8*)(winh + o) = f16x8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+      *(f16x8*)(winl + o) = f16x8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+    }
+  }
+  store_w(0);
+  __syncthreads();
+
+  f32x4 acc1[4][NCB], acc2[4][NCB];
+  #pragma unroll
+  for (int i = 0; i < 4; ++i)
+    #pragma unroll
+    for (int j = 0; j < NCB; ++j) acc1[i][j] = acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int abase[4];
+  #pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rb = wave * 4 + i, c = (rb * 16) / TP, t = rb * 16 - c * TP + r16;
+    abase[i] = ((c * WF + t) * CG) * 2;
+  }
+  int tap = (8 * q) / CG, ch = (8 * q) % CG;
+  for (int st = 0; st < nst; ++st) {
+    if (st + 1 < nst) load_w(st + 1);
+    const char* wb = wst + (st & 1) * 2 * PSTAGE;
+    #pragma unroll
+    for (int ss = 0; ss < PC_KST / 32; ++ss) {
+      f16x8 bh[NCB], bl[NCB], ah[4], al[4];
+      #pragma unroll
+      for (int j = 0; j < NCB; ++j) {
+        const int row = j * 16 + r16, chunk = ss * 4 + q;
+        const int o = row * (PC_KST * 2) + ((chunk ^ (row & 15)) * 16);
+        bh[j] = *(const f16x8*)(wb + o);
+        bl[j] = *(const f16x8*)(wb + PSTAGE + o);
+      }
+      const int aoff = (tap * CG + ch) * 2;
+      #pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        ah[i] = *(const f16x8*)(winh + abase[i] + aoff);
+        al[i] = *(const f16x8*)(winl + abase[i] + aoff);
+      }
+      #pragma unroll
+      for (int i = 0; i < 4; ++i)
+        #pragma unroll
+        for (int j = 0; j < NCB; ++j) {
+          acc1[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j], ah[i], acc1[i][j], 0, 0, 0);
+          acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[j], al[i], acc2[i][j], 0, 0, 0);
+          acc1[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl[j], ah[i], acc1[i][j], 0, 0, 0);
+        }
+      ch += 32;
+      if (ch >= CG) { ch -= CG; ++tap; }
+    }
+    if (st + 1 < nst) store_w((st + 1) & 1);
+    __syncthreads();
+  }
+
+  #pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rb = wave * 4 + i, c = (rb * 16) / TP, t = f0 + rb * 16 - c * TP + r16, b = b0 + c;
+    if (b >= B || t >= T) continue;
+    float* xr = x + ((long long)b * T + t) * H + grp * CG;
+    #pragma unroll
+    for (int j = 0; j < NCB; ++j) {
+      const int n = j * 16 + 4 * q;
+      const f32x4 bv = *(const f32x4*)(bias + grp * CG + n);
+      f32x4 r = *(const f32x4*)(xr + n);
+      #pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] += gelu_erf(fmaf(fmaf(acc2[i][j][e], 1.f / X3_LO_SCALE, acc1[i][j][e]), alpha, bv[e]));
+      *(f32x4*)(xr + n) = r;
+    }
+  }
+}
+
+template <int TP>
+int launch_x3_tp(const float* xt, const f16* W, float alpha, const float* bias, float* x, int B, int T, int H, int G,
+                 int K, int pad, hipStream_t s) {
+  const int WF = TP + K - 1;
+  const size_t lds = 2 * ((size_t)(2 * WF * PX_CG * 2 + 15) & ~(size_t)15) + 4 * (size_t)(PX_CG * PC_KST * 2);
+  if (lds > 160 * 1024) return -3;
+  constexpr int NT = 64 * (2 * TP / 64);
+  hipLaunchKernelGGL((posconv_x3_kernel<TP>), dim3((B + 1) / 2, G, (T + TP - 1) / TP), dim3(NT), lds, s, xt, W, alpha,
+                     bias, x, B, T, H, K, pad);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 }  // namespace
+
+// split-fp16 positional conv (W: planes [wh][wl] of [H][K * cg] f16, scaled by 1 / alpha); -3: shape
+// outside the kernel (the caller keeps the fp32 grouped GEMM)
+int launch_posconv_x3(const float* xt, const f16* W, float alpha, const float* bias, float* x, int B, int T, int H,
+                      int G, int K, int pad, hipStream_t s) {
+  if (G <= 0 || H % G || H / G != PX_CG || T <= 0 || pad < 0 || pad >= K || (K * PX_CG) % PC_KST) return -3;
+  const int tp = T > 160 ? 160 : ((T + 31) / 32) * 32;
+  switch (tp) {
+    case 32: return launch_x3_tp<32>(xt, W, alpha, bias, x, B, T, H, G, K, pad, s);
+    case 64: return launch_x3_tp<64>(xt, W, alpha, bias, x, B, T, H, G, K, pad, s);
+    case 96: return launch_x3_tp<96>(xt, W, alpha, bias, x, B, T, H, G, K, pad, s);
+    case 128: return launch_x3_tp<128>(xt, W, alpha, bias, x, B, T, H, G, K, pad, s);
+    case 160: return launch_x3_tp<160>(xt, W, alpha, bias, x, B, T, H, G, K, pad, s);
+    default: return -3;
+  }
+}
 
 // -3: shape outside this kernel (the caller falls back to the grouped GEMM)
 int launch_posconv_bf16(const bf16* xt, const bf16* W, const float* bias, float* x, int B, int T, int H, int G, int K,

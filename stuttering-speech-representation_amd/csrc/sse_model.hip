@@ -163,6 +163,25 @@ struct Arena {
     alpha[off] = std::ldexp(1.f, -e);
     return off;
   }
+  // split-fp16 positional-conv weight (posconv_x3_kernel): two planes [wh][wl] of w 2^e, wh = f16(w 2^e),
+  // wl = f16(w 2^e - wh), e as put_x3; alpha[offset] = 2^-e
+  size_t put_pos_x3(const std::vector<float>& v) {
+    float amax = 0.f;
+    for (float w : v) amax = std::fmax(amax, std::fabs(w));
+    int e = 0;
+    if (amax > 0.f && std::isfinite(amax)) e = std::min(60, std::max(-60, (int)std::floor(std::log2(16384.0 / amax))));
+    const float sc = std::ldexp(1.f, e);
+    std::vector<f16> h(v.size() * 2);
+    for (size_t i = 0; i < v.size(); ++i) {
+      const float w = v[i] * sc;
+      const f16 hi = (f16)w;
+      h[i] = hi;
+      h[v.size() + i] = (f16)(w - (float)hi);
+    }
+    const size_t off = put(h.data(), h.size() * 2);
+    alpha[off] = std::ldexp(1.f, -e);
+    return off;
+  }
   // kind 0: fp32, 1: bf16, 2: fp16 (SSE_DTYPE_FP16)
   size_t put_elem(const std::vector<float>& v, int kind) {
     if (!kind) return put(v.data(), v.size() * 4);
@@ -238,6 +257,7 @@ struct sse_model {
   size_t conv_w[8], conv_b[8], conv_ln_w[8], conv_ln_b[8];
   bool has_conv_b = false;
   size_t fp_ln_w, fp_ln_b, fp_w, fp_b, pos_w, pos_b, enc_ln_w, enc_ln_b, relb, zero;
+  size_t pos_w3 = 0;        // fp16x3: positional-conv weight planes [wh][wl] (Arena::put_pos_x3)
   size_t status = 0;   // device int: raised when an fp16-range call wrote a non-finite value (sse_check_range)
   // Whisper
   size_t c1_w, c1_b, c2_w, c2_b, positions;
@@ -356,6 +376,7 @@ int build_wavlm(sse_model* m, Blob& bl, Arena& ar) {
         for (int j = 0; j < K; ++j)
           t[((size_t)o * K + j) * cg + ci] = (float)((double)pg[j] * ((double)pv[((size_t)o * cg + ci) * K + j] / nrm[j]));
     m->pos_w = ar.put_elem(t, BF);
+    if (m->x3()) m->pos_w3 = ar.put_pos_x3(t);
     m->pos_b = ar.put_f32(pb, H);
     m->enc_ln_w = ar.put_f32(elw, H);
     m->enc_ln_b = ar.put_f32(elb, H);
@@ -1072,8 +1093,16 @@ int wavlm_forward_x3(sse_model* m, const float* wave, int B, int L, const Sink& 
   }
   if (hipMemcpyAsync(xt, x, (size_t)M * H * 4, hipMemcpyDeviceToDevice, s) != hipSuccess) return SSE_ERR_HIP;
   if (lens) RC(launch_mask_rows<float>(xt, B, Tf, H, tflen, s));
-  // ---- positional conv embedding in exact fp32: x = x + gelu(conv(x) + b) ----
-  {
+  // ---- positional conv embedding: x = x + gelu(conv(x) + b), split-fp16 matrix cores (the fp32
+  // grouped GEMM for shapes outside posconv_x3_kernel or under OPT_POSCONV_GEMM) ----
+  int prc = -3;
+  if (!sse_opt(OPT_POSCONV_GEMM))
+    RC(prof(m, s, "gemm_conv:posconv", 2.0 * B * (double)Tf * H * c.pos_kernel * (H / c.pos_groups),
+            (double)B * Tf * H * 8 + (double)H * c.pos_kernel * (H / c.pos_groups) * 4, [&] {
+      prc = launch_posconv_x3(xt, m->ptr<f16>(m->pos_w3), m->alpha(m->pos_w3), m->ptr<float>(m->pos_b), x, B, Tf, H,
+                              c.pos_groups, c.pos_kernel, c.pos_kernel / 2, s);
+      return prc == -3 ? 0 : prc; }));
+  if (prc == -3) {
     const int G = c.pos_groups, cg = H / G, K = c.pos_kernel;
     GemmArgs g{};
     g.A = xt; g.B = m->ptr(m->pos_w); g.M = M; g.N = cg; g.K = K * cg;

@@ -296,6 +296,22 @@ def test_fp16x3_multirow_layernorm_is_bit_identical(mx3):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("shape", [(3, 48000), (2, 160000), (3, 5000)])
+def test_fp16x3_posconv_kernel_matches_fp32_grouped_gemm(mx3, shape):
+    """The split-fp16 positional conv (posconv_x3_kernel: three fp16 products per term, ~22 bits per
+    operand) against the exact-fp32 grouped GEMM it replaced (option posconv_gemm): every hidden state
+    within 1e-5 rel-L2 -- 149 frames (one 160-frame chunk), 499 (four, the last partial), 15 (32-frame
+    tile)."""
+    from ssr_amd import _lib, synth
+    w = torch.from_numpy(synth.synth_clips(shape[0], shape[1], seed=33)).cuda()
+    new = mx3.hidden_states(w)
+    with _lib.option("posconv_gemm", 1):
+        ref = mx3.hidden_states(w)
+    for a, b in zip(new, ref):
+        rel = ((a - b).norm() / b.norm()).item()
+        assert rel <= 1e-5, rel
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "fp16x3", "fp16"])
 def test_two_stream_split_equals_one_stream(wavlm_sd, dtype):
     """Batches of >= 128 WavLM clips run as two half-batches on two streams (split_forward): bit-identical
