@@ -1283,11 +1283,17 @@ SSE_DEV float wavlm_gate_v(const bf16x8& r, float c) {
   return ga * (gb * c - 1.0f) + 2.0f;
 }
 
-template <typename TE, bool BIAS>
+// X3 (split-fp16 path, TE = float, a.out3): fp32 q/k/v from the QKV GEMM, split while loaded / staged
+// (x3_split4) into hi and lo' 2^-11 planes, and both products on the f16 matrix cores with the bf16
+// form's fragment layout: S = qh.kh + 2^-11 (qh.kl' + ql'.kh), O = ph.vh + 2^-11 (ph.vl' + pl'.vh), the
+// 2^-11 terms in their own accumulators (the dropped lo.lo' is ~2^-22 relative); the softmax in fp32.
+// The exact-f32 form (16x16x4 f32 MFMAs, scalar V reads) ran at ~30 TF/s.
+template <typename TE, bool BIAS, bool X3 = false>
 __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
   constexpr bool BF = sizeof(TE) == 2;
-  constexpr int KS_BYTES = BF ? AT_K * 128 : AT_K * 256;
-  constexpr int VS_BYTES = BF ? AT_HD * VT_STRIDE * 2 : AT_K * VF_STRIDE * 4;
+  static_assert(!(BF && X3), "X3: fp32 q/k/v");
+  constexpr int KS_BYTES = X3 ? 2 * AT_K * 128 : BF ? AT_K * 128 : AT_K * 256;
+  constexpr int VS_BYTES = X3 ? 2 * AT_HD * VT_STRIDE * 2 : BF ? AT_HD * VT_STRIDE * 2 : AT_K * VF_STRIDE * 4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ks = smem;
   char* Vs = smem + KS_BYTES;
@@ -1329,7 +1335,19 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
   const TE* qrow = qkv + (long long)(qv ? qi : 0) * H3 + h * AT_HD;
   bf16x8 qb[2];
   f32x4 qf[4];
-  if constexpr (BF) {
+  f16x8 qh[2], ql[2];
+  if constexpr (X3) {
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      f32x4 v0 = *(const f32x4*)((const float*)qrow + ks * 32 + g * 8), v1 = *(const f32x4*)((const float*)qrow + ks * 32 + g * 8 + 4);
+      if (!qv) v0 = v1 = f32x4{0.f, 0.f, 0.f, 0.f};
+      f16x4 h0, l0, h1, l1;
+      x3_split4(v0, h0, l0);
+      x3_split4(v1, h1, l1);
+      qh[ks] = f16x8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+      ql[ks] = f16x8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+    }
+  } else if constexpr (BF) {
     #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       qb[ks] = *(const bf16x8*)(qrow + ks * 32 + g * 8);
@@ -1343,9 +1361,9 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
     }
   }
 
-  f32x4 o[4];
+  f32x4 o[4], o2[4];   // o2: the 2^-11 terms (X3)
   #pragma unroll
-  for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < 4; ++i) o[i] = o2[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m_run = -INFINITY, l_run = 0.f;
   const float LOG2E = 1.4426950408889634f;
 
@@ -1353,7 +1371,36 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
     __syncthreads();   // previous tile fully consumed
     // ---- stage K (swizzled rows) and V (transposed for bf16) ----
     const int kbase = kt * AT_K;
-    if constexpr (BF) {
+    if constexpr (X3) {
+      for (int i = tid; i < AT_K * 8; i += 256) {
+        const int kr = i >> 3, ch = i & 7;
+        const int key = kbase + kr;
+        f32x4 k0 = f32x4{0.f, 0.f, 0.f, 0.f}, k1 = k0, v0 = k0, v1 = k0;
+        if (key < T) {
+          const float* kp = (const float*)(qkv + (long long)key * H3 + H + h * AT_HD) + ch * 8;
+          const float* vp = (const float*)(qkv + (long long)key * H3 + 2 * H + h * AT_HD) + ch * 8;
+          k0 = *(const f32x4*)kp; k1 = *(const f32x4*)(kp + 4);
+          v0 = *(const f32x4*)vp; v1 = *(const f32x4*)(vp + 4);
+        }
+        f16x4 h0, l0, h1, l1;
+        x3_split4(k0, h0, l0);
+        x3_split4(k1, h1, l1);
+        char* kd = Ks + kr * 128 + ((ch ^ ((kr >> 1) & 7)) * 16);
+        *(f16x8*)kd = f16x8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        *(f16x8*)(kd + AT_K * 128) = f16x8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+        x3_split4(v0, h0, l0);
+        x3_split4(v1, h1, l1);
+        f16* vth = (f16*)Vs;
+        f16* vtl = vth + AT_HD * VT_STRIDE;
+        #pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          vth[(ch * 8 + e) * VT_STRIDE + kr] = h0[e];
+          vth[(ch * 8 + 4 + e) * VT_STRIDE + kr] = h1[e];
+          vtl[(ch * 8 + e) * VT_STRIDE + kr] = l0[e];
+          vtl[(ch * 8 + 4 + e) * VT_STRIDE + kr] = l1[e];
+        }
+      }
+    } else if constexpr (BF) {
       for (int i = tid; i < AT_K * 8; i += 256) {
         const int kr = i >> 3, ch = i & 7;
         const int key = kbase + kr;
@@ -1388,7 +1435,19 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
     for (int kb = 0; kb < 4; ++kb) {
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
       const int kr = kb * 16 + r16;
-      if constexpr (BF) {
+      if constexpr (X3) {
+        f32x4 acc2 = f32x4{0.f, 0.f, 0.f, 0.f};
+        #pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const char* kp = Ks + kr * 128 + (((g + 4 * ks) ^ ((kr >> 1) & 7)) * 16);
+          const f16x8 kh = *(const f16x8*)kp, kl = *(const f16x8*)(kp + AT_K * 128);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, qh[ks], acc, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(kl, qh[ks], acc2, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(kh, ql[ks], acc2, 0, 0, 0);
+        }
+        #pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] = fmaf(acc2[e], 1.f / X3_LO_SCALE, acc[e]);
+      } else if constexpr (BF) {
         #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
           const bf16x8 kf = *(const bf16x8*)(Ks + kr * 128 + (((g + 4 * ks) ^ ((kr >> 1) & 7)) * 16));
@@ -1425,6 +1484,10 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
     l_run *= alpha;
     #pragma unroll
     for (int i = 0; i < 4; ++i) o[i] *= alpha;
+    if constexpr (X3) {
+      #pragma unroll
+      for (int i = 0; i < 4; ++i) o2[i] *= alpha;
+    }
     const float mb = m_new * LOG2E;
     #pragma unroll
     for (int kb = 0; kb < 4; ++kb)
@@ -1435,7 +1498,29 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
         l_run += p;
       }
     // ---- O^T += V^T . P^T ----
-    if constexpr (BF) {
+    if constexpr (X3) {
+      const f16* vth = (const f16*)Vs;
+      const f16* vtl = vth + AT_HD * VT_STRIDE;
+      #pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        f16x4 h0, l0, h1, l1;
+        x3_split4(s[2 * ks], h0, l0);
+        x3_split4(s[2 * ks + 1], h1, l1);
+        const f16x8 ph = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        const f16x8 pl = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+        #pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          const int vo = (db * 16 + r16) * VT_STRIDE + ks * 32 + 4 * g;
+          const f16x4 a0 = *(const f16x4*)(vth + vo), a1 = *(const f16x4*)(vth + vo + 16);
+          const f16x4 c0 = *(const f16x4*)(vtl + vo), c1 = *(const f16x4*)(vtl + vo + 16);
+          const f16x8 vh = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+          const f16x8 vl = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+          o[db] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, ph, o[db], 0, 0, 0);
+          o2[db] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vl, ph, o2[db], 0, 0, 0);
+          o2[db] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, pl, o2[db], 0, 0, 0);
+        }
+      }
+    } else if constexpr (BF) {
       const bf16* vt = (const bf16*)Vs;
       #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
@@ -1472,6 +1557,12 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
   l_run += __shfl_xor(l_run, 32, 64);
   if (!qv) return;
   const float inv = 1.0f / l_run;
+  if constexpr (X3) {
+    #pragma unroll
+    for (int db = 0; db < 4; ++db)
+      #pragma unroll
+      for (int e = 0; e < 4; ++e) o[db][e] = fmaf(o2[db][e], 1.f / X3_LO_SCALE, o[db][e]);
+  }
   TE* orow = (TE*)a.out + ((long long)b * TS + qi) * H + h * AT_HD;
   #pragma unroll
   for (int db = 0; db < 4; ++db) {
@@ -1969,6 +2060,17 @@ int launch_attention(const AttnArgs& a, int B, hipStream_t s) {
   }
   if constexpr (!is_f16_v<T>) {   // fp32 (and the bf16 grid's unused tail)
     dim3 grid((a.T + AT_Q - 1) / AT_Q, a.nh, B);
+    if constexpr (!BF) {
+      if (a.out3 && !sse_opt(OPT_ATTN_X3_F32)) {   // split-fp16 path: the f16 matrix cores
+        const size_t lx = 2 * AT_K * 128 + 2 * AT_HD * VT_STRIDE * 2 + AT_Q * 4 + (a.relb ? (size_t)(2 * nkt * AT_K) * 4 : 0);
+        if (lx > 160 * 1024) return -3;
+        if (a.relb)
+          hipLaunchKernelGGL((attention_kernel<T, true, true>), grid, dim3(256), lx, s, a);
+        else
+          hipLaunchKernelGGL((attention_kernel<T, false, true>), grid, dim3(256), lx, s, a);
+        return hipGetLastError() == hipSuccess ? 0 : -2;
+      }
+    }
     if (a.relb)
       hipLaunchKernelGGL((attention_kernel<T, true>), grid, dim3(256), lds, s, a);
     else

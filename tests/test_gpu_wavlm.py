@@ -312,6 +312,21 @@ def test_fp16x3_posconv_kernel_matches_fp32_grouped_gemm(mx3, shape):
         assert rel <= 1e-5, rel
 
 
+@pytest.mark.parametrize("shape", [(3, 48000), (2, 160000), (3, 5000)])
+def test_fp16x3_attention_matches_exact_fp32(mx3, shape):
+    """The split-fp16 attention (attention_kernel X3: q/k/v and P split into fp16 hi + lo', three f16
+    matrix-core products per term) against the exact-f32 MFMA form (option attn_x3_f32): every hidden
+    state within 1e-5 rel-L2 at 149, 499 (8 key tiles, ragged last) and 15 frames."""
+    from ssr_amd import _lib, synth
+    w = torch.from_numpy(synth.synth_clips(shape[0], shape[1], seed=34)).cuda()
+    new = mx3.hidden_states(w)
+    with _lib.option("attn_x3_f32", 1):
+        ref = mx3.hidden_states(w)
+    for a, b in zip(new, ref):
+        rel = ((a - b).norm() / b.norm()).item()
+        assert rel <= 1e-5, rel
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "fp16x3", "fp16"])
 def test_two_stream_split_equals_one_stream(wavlm_sd, dtype):
     """Batches of >= 128 WavLM clips run as two half-batches on two streams (split_forward): bit-identical
