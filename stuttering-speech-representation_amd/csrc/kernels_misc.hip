@@ -1238,6 +1238,7 @@ template int launch_mask_rows<f16>(f16*, int, int, int, const int*, hipStream_t)
 // [d][key]; f32 path: v_mfma_f32_16x16x4_f32 on K [key][d] (256-B rows, XOR swizzle) and
 // V [key][d] (68-float rows).  HF: modeling_wavlm.py:141-241, modeling_whisper.py:215-238.
 constexpr int AT_Q = 64, AT_K = 64, AT_HD = 64;
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 constexpr int VT_STRIDE = 72;     // bf16 V^T row stride (36 dwords = 16k+4: conflict-free b64 reads)
 constexpr int VF_STRIDE = 68;     // f32 V row stride (4 mod 8: conflict-free b32 reads)
 
@@ -1293,7 +1294,7 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
   constexpr bool BF = sizeof(TE) == 2;
   static_assert(!(BF && X3), "X3: fp32 q/k/v");
   constexpr int KS_BYTES = X3 ? 2 * AT_K * 128 : BF ? AT_K * 128 : AT_K * 256;
-  constexpr int VS_BYTES = X3 ? 2 * AT_HD * VT_STRIDE * 2 : BF ? AT_HD * VT_STRIDE * 2 : AT_K * VF_STRIDE * 4;
+  constexpr int VS_BYTES = X3 ? 2 * AT_K * 128 : BF ? AT_HD * VT_STRIDE * 2 : AT_K * VF_STRIDE * 4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ks = smem;
   char* Vs = smem + KS_BYTES;
@@ -1390,15 +1391,11 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
         *(f16x8*)(kd + AT_K * 128) = f16x8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
         x3_split4(v0, h0, l0);
         x3_split4(v1, h1, l1);
-        f16* vth = (f16*)Vs;
-        f16* vtl = vth + AT_HD * VT_STRIDE;
-        #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          vth[(ch * 8 + e) * VT_STRIDE + kr] = h0[e];
-          vth[(ch * 8 + 4 + e) * VT_STRIDE + kr] = h1[e];
-          vtl[(ch * 8 + e) * VT_STRIDE + kr] = l0[e];
-          vtl[(ch * 8 + 4 + e) * VT_STRIDE + kr] = l1[e];
-        }
+        // V row-major (128-B rows, 16-B chunks XOR 2 ((row >> 1) & 3)), read transposed by
+        // ds_read_b64_tr_b16 (attention_full_kernel's layout)
+        char* vd = Vs + kr * 128 + ((ch ^ (((kr >> 1) & 3) << 1)) << 4);
+        *(f16x8*)vd = f16x8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        *(f16x8*)(vd + AT_K * 128) = f16x8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
       }
     } else if constexpr (BF) {
       for (int i = tid; i < AT_K * 8; i += 256) {
@@ -1499,8 +1496,7 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
       }
     // ---- O^T += V^T . P^T ----
     if constexpr (X3) {
-      const f16* vth = (const f16*)Vs;
-      const f16* vtl = vth + AT_HD * VT_STRIDE;
+      const int rowv = 4 * g + (r16 >> 2), swv = ((rowv >> 1) & 3) << 1;
       #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         f16x4 h0, l0, h1, l1;
@@ -1510,11 +1506,13 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
         const f16x8 pl = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
         #pragma unroll
         for (int db = 0; db < 4; ++db) {
-          const int vo = (db * 16 + r16) * VT_STRIDE + ks * 32 + 4 * g;
-          const f16x4 a0 = *(const f16x4*)(vth + vo), a1 = *(const f16x4*)(vth + vo + 16);
-          const f16x4 c0 = *(const f16x4*)(vtl + vo), c1 = *(const f16x4*)(vtl + vo + 16);
-          const f16x8 vh = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-          const f16x8 vl = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+          const char* va = Vs + ks * 4096 + rowv * 128 + (((2 * db + ((r16 & 3) >> 1)) ^ swv) << 4) + 8 * (r16 & 1);
+          const bf16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)va);
+          const bf16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(va + 2048));
+          const bf16x4 c0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(va + AT_K * 128));
+          const bf16x4 c1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(va + AT_K * 128 + 2048));
+          const f16x8 vh = __builtin_bit_cast(f16x8, bf16x8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]});
+          const f16x8 vl = __builtin_bit_cast(f16x8, bf16x8{c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]});
           o[db] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, ph, o[db], 0, 0, 0);
           o2[db] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vl, ph, o2[db], 0, 0, 0);
           o2[db] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, pl, o2[db], 0, 0, 0);
@@ -1597,7 +1595,6 @@ constexpr int F2_QPW = 32, F2_Q = 128, F2_K = 64;
 constexpr int VR_STRIDE = 160;
 constexpr int F2_KS = F2_K * 128, F2_VS = F2_K * VR_STRIDE, F2_BUF = F2_KS + F2_VS;
 
-typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 // A operand of O^T += V^T . P^T for 32 keys from row-major V in LDS: lane (g, r16) gets dim
 // d0 + r16 of keys k0 + 4g + 0..3 (elements 0-3) and k0 + 16 + 4g + 0..3 (elements 4-7) -- the
 // key order of the P^T fragment built from the S^T accumulators.  Per 16-lane group, lane 4q+p
@@ -2062,7 +2059,7 @@ int launch_attention(const AttnArgs& a, int B, hipStream_t s) {
     dim3 grid((a.T + AT_Q - 1) / AT_Q, a.nh, B);
     if constexpr (!BF) {
       if (a.out3 && !sse_opt(OPT_ATTN_X3_F32)) {   // split-fp16 path: the f16 matrix cores
-        const size_t lx = 2 * AT_K * 128 + 2 * AT_HD * VT_STRIDE * 2 + AT_Q * 4 + (a.relb ? (size_t)(2 * nkt * AT_K) * 4 : 0);
+        const size_t lx = 4 * AT_K * 128 + AT_Q * 4 + (a.relb ? (size_t)(2 * nkt * AT_K) * 4 : 0);
         if (lx > 160 * 1024) return -3;
         if (a.relb)
           hipLaunchKernelGGL((attention_kernel<T, true, true>), grid, dim3(256), lx, s, a);
