@@ -937,6 +937,17 @@ __global__ __launch_bounds__(256) void layernorm_mx8_kernel(const bf16* __restri
     }
   };
   load(cur, r0 + wave);
+  // the LayerNorm weight / bias of the lane's columns, loaded once (per row they were 4x the row's
+  // own bytes through L1)
+  f32x4 wr[NC][2], br[NC][2];
+  #pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int c = 512 * i + 8 * lane, cc = c < H ? c : 0;
+    wr[i][0] = *(const f32x4*)(w + cc);
+    wr[i][1] = *(const f32x4*)(w + cc + 4);
+    br[i][0] = *(const f32x4*)(bta + cc);
+    br[i][1] = *(const f32x4*)(bta + cc + 4);
+  }
   for (int rr = wave; rr < 64; rr += 4) {
     const int row = r0 + rr;
     if (row >= rows) break;
@@ -961,9 +972,7 @@ __global__ __launch_bounds__(256) void layernorm_mx8_kernel(const bf16* __restri
     for (int i = 0; i < NC; ++i) {
       const int c = 512 * i + 8 * lane;
       const bool ok = c < H;   // wave-uniform per 4-lane block (H % 128 == 0)
-      const int cc = ok ? c : 0;
-      const f32x4 w0 = *(const f32x4*)(w + cc), w1 = *(const f32x4*)(w + cc + 4);
-      const f32x4 b0 = *(const f32x4*)(bta + cc), b1 = *(const f32x4*)(bta + cc + 4);
+      const f32x4 w0 = wr[i][0], w1 = wr[i][1], b0 = br[i][0], b1 = br[i][1];
       float o[8];
       #pragma unroll
       for (int e = 0; e < 4; ++e) {
