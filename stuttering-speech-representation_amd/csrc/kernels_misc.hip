@@ -626,36 +626,49 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TI* __restrict__ i
 // and the feature projection's LN): one 16-B load per lane per row, R rows per wave with every load
 // issued first (the one-row-per-wave kernel keeps only 1 KiB in flight per wave: ~2.4 TB/s on these
 // rows), DPP/permlane reductions for the R rows interleaved.  GELU: the bf16 path's gelu_fast2.
-template <int R, bool H16 = false>   // H16: fp16 rows (SSE_DTYPE_FP16) in bf16x8 containers
+// NC > 1 (round 3): rows of up to 512 NC columns (WavLM-large 1024, Whisper 1280 / 768) with R = 2 rows per
+// wave, the weight / bias of the lane's columns loaded once per wave (the one-row-per-wave
+// layernorm_kernel re-read them per row: 4x the row's own bytes through L1).
+template <int R, bool H16 = false, int NC = 1>   // H16: fp16 rows (SSE_DTYPE_FP16) in bf16x8 containers
 __global__ __launch_bounds__(256) void layernorm_bf16_rows_kernel(const bf16* __restrict__ in, const float* __restrict__ w,
                                                                   const float* __restrict__ bta, int rows, int H,
                                                                   float eps, int act, bf16* __restrict__ out) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const long long r0 = ((long long)blockIdx.x * 4 + wave) * R;
-  const int nch = H >> 3;
-  const bool on = lane < nch;
-  bf16x8 v[R];
+  bool on[NC];
+  #pragma unroll
+  for (int k = 0; k < NC; ++k) on[k] = 512 * k + 8 * lane < H;
+  bf16x8 v[R][NC];
   #pragma unroll
   for (int i = 0; i < R; ++i) {
     const long long row = r0 + i;
-    v[i] = (on && row < rows) ? *(const bf16x8*)(in + row * H + lane * 8) : bf16x8{};
+    #pragma unroll
+    for (int k = 0; k < NC; ++k)
+      v[i][k] = (on[k] && row < rows) ? *(const bf16x8*)(in + row * H + 512 * k + lane * 8) : bf16x8{};
   }
-  f32x4 w0 = {1.f, 1.f, 1.f, 1.f}, w1 = w0, b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0;
-  if (on) {
-    w0 = *(const f32x4*)(w + lane * 8);
-    w1 = *(const f32x4*)(w + lane * 8 + 4);
-    b0 = *(const f32x4*)(bta + lane * 8);
-    b1 = *(const f32x4*)(bta + lane * 8 + 4);
+  f32x4 w0[NC], w1[NC], b0[NC], b1[NC];
+  #pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    w0[k] = f32x4{1.f, 1.f, 1.f, 1.f}; w1[k] = w0[k]; b0[k] = f32x4{0.f, 0.f, 0.f, 0.f}; b1[k] = b0[k];
+    if (on[k]) {
+      const int c = 512 * k + lane * 8;
+      w0[k] = *(const f32x4*)(w + c);
+      w1[k] = *(const f32x4*)(w + c + 4);
+      b0[k] = *(const f32x4*)(bta + c);
+      b1[k] = *(const f32x4*)(bta + c + 4);
+    }
   }
-  float x[R][8], mean[R], rstd[R];
+  float x[R][NC][8], mean[R], rstd[R];
   #pragma unroll
   for (int i = 0; i < R; ++i) {
     float sm = 0.f;
     #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      x[i][e] = hval<H16>(v[i][e]);
-      sm += x[i][e];
-    }
+    for (int k = 0; k < NC; ++k)
+      #pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        x[i][k][e] = hval<H16>(v[i][k][e]);
+        sm += x[i][k][e];
+      }
     mean[i] = sm;
   }
   #pragma unroll
@@ -664,10 +677,12 @@ __global__ __launch_bounds__(256) void layernorm_bf16_rows_kernel(const bf16* __
   for (int i = 0; i < R; ++i) {
     float q = 0.f;
     #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float d = on ? x[i][e] - mean[i] : 0.f;
-      q = fmaf(d, d, q);
-    }
+    for (int k = 0; k < NC; ++k)
+      #pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = on[k] ? x[i][k][e] - mean[i] : 0.f;
+        q = fmaf(d, d, q);
+      }
     rstd[i] = q;
   }
   #pragma unroll
@@ -675,22 +690,26 @@ __global__ __launch_bounds__(256) void layernorm_bf16_rows_kernel(const bf16* __
   #pragma unroll
   for (int i = 0; i < R; ++i) {
     const long long row = r0 + i;
-    float y[8];
     #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float wv = e < 4 ? w0[e] : w1[e - 4], bv = e < 4 ? b0[e] : b1[e - 4];
-      y[e] = fmaf((x[i][e] - mean[i]) * rstd[i], wv, bv);   // = ln_apply4
-    }
-    if (act != ACT_NONE) {
+    for (int k = 0; k < NC; ++k) {
+      float y[8];
       #pragma unroll
-      for (int e = 0; e < 8; e += 2) {
-        const f32x2 g2 = act == ACT_GELU ? gelu_erf2(f32x2{y[e], y[e + 1]}) : gelu_out2<H16>(f32x2{y[e], y[e + 1]});
-        y[e] = g2.x;
-        y[e + 1] = g2.y;
+      for (int e = 0; e < 8; ++e) {
+        const float wv = e < 4 ? w0[k][e] : w1[k][e - 4], bv = e < 4 ? b0[k][e] : b1[k][e - 4];
+        y[e] = fmaf((x[i][k][e] - mean[i]) * rstd[i], wv, bv);   // = ln_apply4
       }
-    }
-    if (on && row < rows) {
-      *(uint4*)(out + row * H + lane * 8) = pack_h8<H16>(f32x4{y[0], y[1], y[2], y[3]}, f32x4{y[4], y[5], y[6], y[7]});
+      if (act != ACT_NONE) {
+        #pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          const f32x2 g2 = act == ACT_GELU ? gelu_erf2(f32x2{y[e], y[e + 1]}) : gelu_out2<H16>(f32x2{y[e], y[e + 1]});
+          y[e] = g2.x;
+          y[e + 1] = g2.y;
+        }
+      }
+      if (on[k] && row < rows) {
+        *(uint4*)(out + row * H + 512 * k + lane * 8) =
+            pack_h8<H16>(f32x4{y[0], y[1], y[2], y[3]}, f32x4{y[4], y[5], y[6], y[7]});
+      }
     }
   }
 }
@@ -706,6 +725,19 @@ int launch_layernorm(const TI* in, const float* w, const float* b, int rows, int
       const int a2 = act == ACT_GELU && !gelu_exact_env() ? (int)ACT_GELU_FAST : act;   // 16-bit output
       hipLaunchKernelGGL((layernorm_bf16_rows_kernel<R, is_f16_v<TO>>), dim3((rows + 4 * R - 1) / (4 * R)), dim3(256), 0,
                          s, (const bf16*)in, w, b, rows, H, eps, a2, (bf16*)out_t);
+      return hipGetLastError() == hipSuccess ? 0 : -2;
+    }
+    if (H % 8 == 0 && H > 512 && H <= 2048 && act == ACT_NONE && !out_f && !stats && out_t && !sse_opt(OPT_LN_ROWS_V1)) {
+      constexpr int R = 2;
+      const dim3 g((rows + 4 * R - 1) / (4 * R));
+      switch ((H + 511) / 512) {
+        case 2: hipLaunchKernelGGL((layernorm_bf16_rows_kernel<R, is_f16_v<TO>, 2>), g, dim3(256), 0, s, (const bf16*)in, w,
+                                   b, rows, H, eps, act, (bf16*)out_t); break;
+        case 3: hipLaunchKernelGGL((layernorm_bf16_rows_kernel<R, is_f16_v<TO>, 3>), g, dim3(256), 0, s, (const bf16*)in, w,
+                                   b, rows, H, eps, act, (bf16*)out_t); break;
+        default: hipLaunchKernelGGL((layernorm_bf16_rows_kernel<R, is_f16_v<TO>, 4>), g, dim3(256), 0, s, (const bf16*)in, w,
+                                    b, rows, H, eps, act, (bf16*)out_t); break;
+      }
       return hipGetLastError() == hipSuccess ? 0 : -2;
     }
   }

@@ -369,3 +369,22 @@ def test_wavlm_large_posconv_kernel_matches_grouped_gemm(dtype):
             f0 = SSEModel(C.WAVLM_LARGE, sd, device="cuda:0", dtype="fp32").hidden_states(w[:1])[0].cpu().numpy()
             assert _rel(h0.reshape(-1), f0.reshape(-1)) <= 5e-3, L
 
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_wide_row_layernorm_matches_one_row_kernel(dtype):
+    """WavLM-large's 1024-wide 16-bit LayerNorms (pre-LN stream) on the 2-rows-per-wave kernel
+    (layernorm_bf16_rows_kernel NC = 2, weights held per wave) against the one-row-per-wave kernel
+    (option ln_rows_v1): the same expression with the row sum in another order, so outputs agree to
+    the 16-bit rounding -- pooled embeddings within 2e-3 rel-L2, batch invariance bit for bit."""
+    from ssr_amd import _lib, config as C, synth
+    from ssr_amd.model import SSEModel
+    sd = synth.synth_wavlm_state_dict(C.WAVLM_LARGE, seed=9)
+    m = SSEModel(C.WAVLM_LARGE, sd, device="cuda:0", dtype=dtype)
+    w = torch.from_numpy(synth.synth_clips(5, 48000, seed=6)).cuda()
+    idx = [24, 12, 3]
+    new = m.embed(w, idx)
+    with _lib.option("ln_rows_v1", 1):
+        old = m.embed(w, idx)
+    rel = ((new - old).norm(dim=-1) / old.norm(dim=-1)).max().item()
+    assert rel <= 2e-3, rel
+    assert torch.equal(new[3:4], m.embed(w[3:4], idx))
