@@ -56,6 +56,22 @@ def _pow2_scale(w: torch.Tensor) -> float:
     return float(2.0 ** np.floor(np.log2(16384.0 / m))) if m > 0 else 1.0
 
 
+def _mx8(t: torch.Tensor, dim: int) -> torch.Tensor:
+    """MX-fp8 quantise-dequantise along `dim` (blocks of 32, E8M0 scale = smallest 2^E with
+    max|x| <= 448 2^E, e4m3 RNE; oracle/mx.py's rule)."""
+    x = t.movedim(dim, -1)
+    K = x.shape[-1]
+    pad = (-K) % 32
+    xp = torch.nn.functional.pad(x, (0, pad))
+    b = xp.reshape(*xp.shape[:-1], -1, 32)
+    amax = b.abs().amax(-1, keepdim=True)
+    e = torch.ceil(torch.log2(torch.clamp(amax, min=1e-38) / 448.0)).clamp(-127, 127)
+    sc = torch.exp2(e)
+    q = (b / sc).to(torch.float8_e4m3fn).float() * sc
+    q = q.reshape(xp.shape)[..., :K]
+    return q.movedim(-1, dim)
+
+
 def emulated_product(fn, x: torch.Tensor, w: torch.Tensor, fmt: str) -> torch.Tensor:
     """fn(a, b) = the fp32 linear / conv of already-rounded operands."""
     if fmt == "bf16":
@@ -78,6 +94,15 @@ def emulated_product(fn, x: torch.Tensor, w: torch.Tensor, fmt: str) -> torch.Te
         wm = _ftz16(_f16(wh / 2048.0))
         wl = _ftz16(_f16(ws - wh))
         return (fn(xh, wh) + fn(xl, wm) + fn(xh, wl)) / s
+    if fmt == "fp16x3f8":   # hi x hi in fp16, the two cross terms as MX-fp8 products (probe, not a GPU path)
+        s = _pow2_scale(w)
+        ws = w * s
+        xh = _ftz16(_f16(x))
+        xl = _ftz16(_f16((x - xh) * 2048.0))
+        wh = _ftz16(_f16(ws))
+        wl = _ftz16(_f16(ws - wh))
+        return (fn(xh, wh) + fn(_mx8(xl, 1 if x.dim() == 3 else -1), _mx8(wh, 1 if w.dim() == 3 else -1)) / 2048.0
+                + fn(_mx8(xh, 1 if x.dim() == 3 else -1), _mx8(wl, 1 if w.dim() == 3 else -1))) / s
     if fmt in ("fp16x2a", "fp16x2w"):   # two products: split activations (a) or split weights (w)
         s = _pow2_scale(w)
         ws = w * s
