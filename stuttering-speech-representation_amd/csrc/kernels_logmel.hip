@@ -56,7 +56,8 @@ constexpr int MAXSUP = 32;   // bins per Slaney filter (80 mels on 201 bins: at 
 // filter's weights over it packed [n_mels][MAXSUP] (staged in LDS by the STFT kernel).  Block = one
 // filter, a thread per bin (one load each, min / max of the nonzero bins in LDS).
 __global__ __launch_bounds__(256) void lm_support_kernel(const float* __restrict__ fb, int n_mels,
-                                                         int2* __restrict__ sup, float* __restrict__ fbp) {
+                                                         int2* __restrict__ sup, float* __restrict__ fbp,
+                                                         float* __restrict__ fbt) {
   __shared__ int lh[2];
   const int m = blockIdx.x, f = threadIdx.x;
   if (f == 0) { lh[0] = NF; lh[1] = -1; }
@@ -70,7 +71,11 @@ __global__ __launch_bounds__(256) void lm_support_kernel(const float* __restrict
   int hi = lh[1];
   if (hi - lo + 1 > MAXSUP) hi = lo + MAXSUP - 1;   // not reached for n_mels >= 64 (host checks n_mels)
   if (f == 0) sup[m] = make_int2(lo, hi);
-  if (f < MAXSUP) fbp[m * MAXSUP + f] = lo + f <= hi ? fb[(lo + f) * n_mels + m] : 0.f;
+  if (f < MAXSUP) {
+    const float v = lo + f <= hi ? fb[(lo + f) * n_mels + m] : 0.f;
+    fbp[m * MAXSUP + f] = v;
+    fbt[f * n_mels + m] = v;   // [i][m]: the 4-frame kernel's LDS image, copied linearly (no strided LDS stores)
+  }
 }
 
 constexpr int MEL_FR = 20;   // frames per block (3000 = 150 x 20), 5 per wave
@@ -416,7 +421,7 @@ __global__ __launch_bounds__(64 * LM_W) void lm_stft_mel4_kernel(const float* __
     #pragma unroll
     for (int u = 0; u < NFW; ++u) {
       const int i = threadIdx.x + u * NTH;
-      if (i < n_mels * MAXSUP) fwt[(i % MAXSUP) * n_mels + i / MAXSUP] = fr[u];
+      if (i < n_mels * MAXSUP) fwt[i] = fr[u];
     }
     if (threadIdx.x < n_mels) {
       fs[threadIdx.x] = sv.x;
@@ -573,7 +578,7 @@ int launch_normalize_apply(const float* x, int B, int L, const float* st, float*
 size_t logmel_workspace_bytes(int B, int n_mels) {
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   return al((size_t)3 * NZ * 8) + al((size_t)NF * n_mels * 4) + al((size_t)B * NFR * n_mels * 4) + al((size_t)B * 4) +
-         al((size_t)n_mels * 8) + al((size_t)n_mels * MAXSUP * 4);
+         al((size_t)n_mels * 8) + 2 * al((size_t)n_mels * MAXSUP * 4);
 }
 
 template <typename TO>
@@ -588,10 +593,11 @@ int launch_logmel(const float* x, int B, int L, int n_mels, float* out_hf, TO* o
   float* logv = (float*)p; p += al((size_t)B * NFR * n_mels * 4);
   unsigned* mx = (unsigned*)p; p += al((size_t)B * 4);
   int2* sup = (int2*)p; p += al((size_t)n_mels * 8);
-  float* fbp = (float*)p;
+  float* fbp = (float*)p; p += al((size_t)n_mels * MAXSUP * 4);
+  float* fbt = (float*)p;
   hipLaunchKernelGGL(lm_twiddle_kernel, dim3((3 * NZ + 255) / 256), dim3(256), 0, s, tw, mx, B);
   hipLaunchKernelGGL(lm_filters_kernel, dim3((NF * n_mels + 255) / 256), dim3(256), 0, s, fb, n_mels);
-  hipLaunchKernelGGL(lm_support_kernel, dim3(n_mels), dim3(256), 0, s, fb, n_mels, sup, fbp);
+  hipLaunchKernelGGL(lm_support_kernel, dim3(n_mels), dim3(256), 0, s, fb, n_mels, sup, fbp, fbt);
   if (sse_opt(OPT_LOGMEL_V1))
     hipLaunchKernelGGL(lm_stft_mel_kernel, dim3(NFR / MEL_FR, B), dim3(256), 0, s, x, L, L < NS ? L : NS, lens, tw, fbp,
                        sup, n_mels, logv, mx);
@@ -599,7 +605,7 @@ int launch_logmel(const float* x, int B, int L, int n_mels, float* out_hf, TO* o
   {
     const size_t lds = (size_t)LM_W * LM_F * NZ * 8 + 3 * NZ * 8 + (size_t)MAXSUP * n_mels * 4 + (size_t)n_mels * 8;
     hipLaunchKernelGGL(lm_stft_mel4_kernel, dim3(B * LM_CPC), dim3(64 * LM_W), lds, s, x, B, L, L < NS ? L : NS, lens, tw,
-                       fbp, sup, n_mels, logv, mx);
+                       fbt, sup, n_mels, logv, mx);
   }
   hipLaunchKernelGGL((lm_final_kernel<TO>), dim3((NFR + FIN_T - 1) / FIN_T, B), dim3(256), 0, s, logv, mx, n_mels,
                      out_hf, out_cl);

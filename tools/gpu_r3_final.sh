@@ -17,3 +17,11 @@ timeout -k 10 300 python -u bench.py --cpu-sample 0 --dtype fp16 > $O/bench_fp16
 tail -1 $O/bench_fp16.log | cut -c1-200
 timeout -k 10 300 python -u bench.py --cpu-sample 0 --dtype fp16x3 > $O/bench_fp16x3.log 2>&1 || exit 1
 tail -1 $O/bench_fp16x3.log | cut -c1-200
+timeout -k 10 400 python -u bench.py --cpu-sample 0 --model wavlm-large > $O/bench_wavlm_large_bf16.log 2>&1 || exit 1
+tail -1 $O/bench_wavlm_large_bf16.log | cut -c1-200
+timeout -k 10 400 python -u bench.py --cpu-sample 0 --model whisper-large-v2 > $O/bench_whisper_bf16.log 2>&1 || exit 1
+tail -1 $O/bench_whisper_bf16.log | cut -c1-200
+timeout -k 10 400 python -u bench.py --cpu-sample 0 --model whisper-large-v2 --dtype fp8 > $O/bench_whisper_fp8.log 2>&1 || exit 1
+tail -1 $O/bench_whisper_fp8.log | cut -c1-200
+timeout -k 10 300 python -u bench.py --cpu-sample 0 --logmel > $O/bench_logmel.log 2>&1 || exit 1
+tail -1 $O/bench_logmel.log | cut -c1-200
