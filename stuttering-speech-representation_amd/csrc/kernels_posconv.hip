@@ -22,19 +22,21 @@ namespace {
 constexpr int PC_KST = 128;          // K per weight stage
 
 // PC_CG: channels per group (WavLM-base 768 / 16 = 48, WavLM-large 1024 / 16 = 64)
-template <int TP, bool H16 = false, int PC_CG = 48>   // H16: fp16 window / weights (SSE_DTYPE_FP16) in bf16 containers
-__global__ __launch_bounds__(64 * (2 * TP / 64)) void posconv_kernel(const bf16* __restrict__ xt, const bf16* __restrict__ W,
-                                                                    const float* __restrict__ bias, float* __restrict__ x,
-                                                                    int B, int T, int H, int K, int pad) {
-  constexpr int NW = 2 * TP / 64;                 // waves: 4 row blocks of 16 each
+// NCL: clips per block (2; 4 for 48-channel groups up to 160 frames: each weight stage streamed from L2
+// feeds twice the MFMAs, so its one-stage-ahead prefetch is twice as well hidden)
+template <int TP, bool H16 = false, int PC_CG = 48, int NCL = 2>   // H16: fp16 window / weights (SSE_DTYPE_FP16) in bf16 containers
+__global__ __launch_bounds__(64 * (NCL * TP / 64)) void posconv_kernel(const bf16* __restrict__ xt, const bf16* __restrict__ W,
+                                                                      const float* __restrict__ bias, float* __restrict__ x,
+                                                                      int B, int T, int H, int K, int pad) {
+  constexpr int NW = NCL * TP / 64;               // waves: 4 row blocks of 16 each
   constexpr int NT = 64 * NW;
   constexpr int PC_STAGE = PC_CG * PC_KST * 2;    // 12 / 16 KiB
   constexpr int NCB = PC_CG / 16;                 // column blocks per wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int WF = TP + K - 1;                      // window frames per clip
-  char* win = smem;                               // [2][WF][cg] bf16
-  char* wst = smem + ((2 * WF * PC_CG * 2 + 15) & ~15);   // [2][cg][PC_KST] bf16, swizzled
-  const int grp = blockIdx.y, b0 = blockIdx.x * 2;
+  char* win = smem;                               // [NCL][WF][cg] bf16
+  char* wst = smem + ((NCL * WF * PC_CG * 2 + 15) & ~15);   // [2][cg][PC_KST] bf16, swizzled
+  const int grp = blockIdx.y, b0 = blockIdx.x * NCL;
   const int f0 = blockIdx.z * TP;                 // first output frame of this block (clips > 256 frames: chunks)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -65,7 +67,7 @@ __global__ __launch_bounds__(64 * (2 * TP / 64)) void posconv_kernel(const bf16*
   load_w(0);
   // ---- input windows: frame f of clip c holds xt[b0 + c][f - pad][grp*cg + 0..47] (zero outside) ----
   {
-    const int n16 = 2 * WF * (PC_CG / 8);   // 16-B chunks of both clips' windows
+    const int n16 = NCL * WF * (PC_CG / 8);   // 16-B chunks of the clips' windows
     for (int i = tid; i < n16; i += NT) {
       constexpr int CPF = PC_CG / 8;   // 16-B chunks per frame
       const int c = i / (WF * CPF), r = i - c * WF * CPF, f = r / CPF, ch = r - f * CPF;
@@ -135,20 +137,27 @@ __global__ __launch_bounds__(64 * (2 * TP / 64)) void posconv_kernel(const bf16*
   }
 }
 
+template <int TP, int CG, int NCL>
+int launch_ncl(const bf16* xt, const bf16* W, const float* bias, float* x, int B, int T, int H, int G, int K, int pad,
+               hipStream_t s, bool h16) {
+  const int WF = TP + K - 1;
+  const size_t lds = ((size_t)(NCL * WF * CG * 2 + 15) & ~(size_t)15) + 2 * (size_t)(CG * PC_KST * 2);
+  if (lds > 160 * 1024) return -3;
+  constexpr int NT = 64 * (NCL * TP / 64);
+  const dim3 grid((B + NCL - 1) / NCL, G, (T + TP - 1) / TP);
+  if (h16)
+    hipLaunchKernelGGL((posconv_kernel<TP, true, CG, NCL>), grid, dim3(NT), lds, s, xt, W, bias, x, B, T, H, K, pad);
+  else
+    hipLaunchKernelGGL((posconv_kernel<TP, false, CG, NCL>), grid, dim3(NT), lds, s, xt, W, bias, x, B, T, H, K, pad);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
 template <int TP, int CG>
 int launch_tp(const bf16* xt, const bf16* W, const float* bias, float* x, int B, int T, int H, int G, int K, int pad,
               hipStream_t s, bool h16) {
-  const int WF = TP + K - 1;
-  const size_t lds = ((size_t)(2 * WF * CG * 2 + 15) & ~(size_t)15) + 2 * (size_t)(CG * PC_KST * 2);
-  if (lds > 160 * 1024) return -3;
-  constexpr int NT = 64 * (2 * TP / 64);
-  if (h16)
-    hipLaunchKernelGGL((posconv_kernel<TP, true, CG>), dim3((B + 1) / 2, G, (T + TP - 1) / TP), dim3(NT), lds, s, xt, W,
-                       bias, x, B, T, H, K, pad);
-  else
-    hipLaunchKernelGGL((posconv_kernel<TP, false, CG>), dim3((B + 1) / 2, G, (T + TP - 1) / TP), dim3(NT), lds, s, xt, W,
-                       bias, x, B, T, H, K, pad);
-  return hipGetLastError() == hipSuccess ? 0 : -2;
+  if constexpr (CG == 48 && TP <= 160) {
+    if (!sse_opt(OPT_POSCONV_2CL)) return launch_ncl<TP, CG, 4>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
+  }
+  return launch_ncl<TP, CG, 2>(xt, W, bias, x, B, T, H, G, K, pad, s, h16);
 }
 
 template <int CG>

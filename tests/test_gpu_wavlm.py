@@ -192,6 +192,11 @@ def test_bf16_posconv_kernel_matches_grouped_gemm(wavlm_sd, n_clips, samples):
     assert _rel(h0.reshape(-1), g0.reshape(-1)) <= 1e-5
     assert _rel(a[:, 0], b[:, 0]).max() <= 1e-5
     assert _rel(a, b).max() <= 5e-3
+    # 4 clips per block (48-channel groups, <= 160 frames) vs 2 (option posconv_2cl): the same K order
+    # per output, so bit-identical; 7 / 3 / 2 clips leave partial 4-clip blocks
+    with _lib.option("posconv_2cl", 1):
+        c2 = m.embed(w, idx).cpu().numpy()
+    assert np.array_equal(a, c2)
 
 
 @pytest.mark.parametrize("samples", [16000, 20001, 48000])
