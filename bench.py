@@ -41,6 +41,7 @@ import torch  # noqa: E402
 importlib.import_module("stuttering-speech-representation_amd")
 from ssr_amd import config as C, synth  # noqa: E402
 from ssr_amd.model import SSEModel  # noqa: E402
+from ssr_amd.corpus import StepGather  # noqa: E402
 
 # Algorithmic FLOPs per clip: 2 x MACs of every GEMM/conv + QK^T, AV.
 FLOP_PER_CLIP = {"wavlm-base": 42.39e9, "wavlm-large": 109.6e9, "whisper-large-v2": 2272.67e9}
@@ -361,15 +362,8 @@ def main():
     del sd
     idx = spec.default_layer_indices()
     clips = torch.from_numpy(synth.synth_clips(B, L, seed=1234, first_clip=rank * B)).to(dev)
-    # two output slots: step k's all-gather (RCCL, async on its own stream) overlaps step k+1's compute
-    outs = [torch.empty((B, len(idx), spec.hidden), dtype=torch.float32, device=dev) for _ in range(2)]
-    gathered = [torch.empty((world * B, len(idx), spec.hidden), dtype=torch.float32, device=dev)
-                for _ in range(2)] if world > 1 else None
-    pending = [None, None]
-
     if a.corpus:
         return corpus_run(a, model, spec, idx, clips, B, L, world, rank, dev, dist)
-    it_slot = [0]
 
     # --stream (configs[4] "streaming extraction"): each step's clips come from pinned host memory,
     # copied on a side stream into the other of two device buffers while this step computes
@@ -388,13 +382,7 @@ def main():
             ready[0].record(cs)
         it = [0]
 
-    def step():
-        slot = it_slot[0] % 2
-        it_slot[0] += 1
-        out = outs[slot]
-        if pending[slot] is not None:        # the gather that last read this slot
-            pending[slot].wait()
-            pending[slot] = None
+    def embed_into(out):
         if a.stream:
             cur, nxt = it[0] % 2, (it[0] + 1) % 2
             it[0] += 1
@@ -407,14 +395,11 @@ def main():
             done[cur].record()
         else:
             model.embed(clips, idx, out=out)
-        if dist is not None:
-            pending[slot] = dist.all_gather_into_tensor(gathered[slot], out, async_op=True)
 
-    def drain():
-        for i in range(2):
-            if pending[i] is not None:
-                pending[i].wait()
-                pending[i] = None
+    # two output slots: step k's all-gather (RCCL, async on its own stream) overlaps step k+1's compute
+    # (corpus.StepGather; its gloo twin is tests/test_corpus_dist.py::test_step_gather_*)
+    pipe = StepGather(embed_into, (B, len(idx), spec.hidden), world, dev, dist)
+    step, drain = pipe.step, pipe.drain
 
     for _ in range(a.warmup):
         step()

@@ -152,9 +152,11 @@ def _recoverable(e: BaseException) -> bool:
     (shorter than the receptive field: SSE_ERR_INVALID, or the wrapper's ValueError) or a shape the
     kernels do not cover.  A HIP runtime failure (SSE_ERR_HIP: a fault or a sticky context error)
     and anything unexpected are NOT: after those every clip would fail again, so they propagate
-    instead of silently dropping every augmented sample."""
-    from ._lib import SSEError, SSEOutOfMemoryError
-    if isinstance(e, (SSEOutOfMemoryError, torch.OutOfMemoryError, ValueError)):
+    instead of silently dropping every augmented sample.  An fp16-range overflow
+    (SSERangeError, fp16 / fp16x3 models) is one clip's property: the range flag is cleared when it is
+    read, so the per-clip retry finds the offending clip and skips only it."""
+    from ._lib import SSEError, SSEOutOfMemoryError, SSERangeError
+    if isinstance(e, (SSEOutOfMemoryError, SSERangeError, torch.OutOfMemoryError, ValueError)):
         return True
     return isinstance(e, SSEError) and e.rc in (-1, -3, -4)
 

@@ -121,9 +121,13 @@ class WhisperSpec:
 
 WHISPER_LARGE_V2 = WhisperSpec()
 WHISPER_TINY = WhisperSpec(d_model=384, layers=4, heads=6, ffn=1536, name="whisper-tiny")
+# openai/whisper-small: the reference's default --model_name (REF/whisper_embeddings_large.py:34)
+WHISPER_SMALL = WhisperSpec(d_model=768, layers=12, heads=12, ffn=3072, name="whisper-small")
 # encoder + the reference's 1-token decoder pass (decoder_layer_* embeddings)
 WHISPER_LARGE_V2_DEC = WhisperSpec(decoder_layers=32, name="whisper-large-v2+decoder")
 WHISPER_TINY_DEC = WhisperSpec(d_model=384, layers=4, heads=6, ffn=1536, decoder_layers=4, name="whisper-tiny+decoder")
+WHISPER_SMALL_DEC = WhisperSpec(d_model=768, layers=12, heads=12, ffn=3072, decoder_layers=12,
+                                name="whisper-small+decoder")
 
 
 def param_specs(spec) -> list[tuple[str, tuple]]:

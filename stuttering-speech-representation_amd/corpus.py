@@ -45,6 +45,30 @@ def shard_bounds(n_items: int, world: int, rank: int) -> tuple[int, int, int]:
     return start, min(start + per, n_items), per
 
 
+def balanced_bounds(item_lengths, world: int) -> list[int]:
+    """Contiguous shard boundaries [b_0 = 0, b_1, ..., b_world = N] that split the corpus's total samples
+    (the work: the encoder's cost is linear in a clip's length to first order) as evenly as contiguity
+    allows: rank r owns [b_r, b_{r+1}).  Count-based shards of a corpus ordered by length (a sorted
+    manifest) give one rank all the long clips; these give every rank ~1/world of the samples.
+    Every rank gets at least one item while n >= world."""
+    lens = np.asarray([max(int(v), 0) for v in item_lengths], dtype=np.float64)
+    n = lens.size
+    if world <= 0:
+        raise ValueError(f"bad world {world}")
+    cum = np.concatenate([[0.0], np.cumsum(lens)])
+    total = cum[-1]
+    bounds = [0]
+    for r in range(1, world):
+        # first index whose prefix reaches r/world of the samples, kept strictly increasing with room
+        # for the remaining ranks (one item each) when possible
+        b = int(np.searchsorted(cum, total * r / world, side="left")) if total > 0 else (n * r) // world
+        lo = bounds[-1] + (1 if n - bounds[-1] > world - r else 0)
+        hi = n - (world - r) if n >= world else n
+        bounds.append(int(min(max(b, lo), max(hi, lo))))
+    bounds.append(n)
+    return bounds
+
+
 def _as_batch(src):
     """clip_source output -> (wave [b, L] tensor or ndarray, lengths list | None)."""
     if isinstance(src, tuple):
@@ -118,7 +142,8 @@ class _Stager:
 
 def extract_corpus(clip_source: Callable[[int, int], object], n_items: int,
                    embed_fn: Callable[..., torch.Tensor], out_shape: tuple[int, int],
-                   device, batch: int = 256, group=None, prefetch: bool = True) -> torch.Tensor:
+                   device, batch: int = 256, group=None, prefetch: bool = True,
+                   item_lengths=None) -> torch.Tensor:
     """Embed clips [0, n_items) across the process group; returns [n_items, *out_shape] fp32 on
     `device` on every rank (corpus order).
 
@@ -126,12 +151,24 @@ def extract_corpus(clip_source: Callable[[int, int], object], n_items: int,
     (host or device), a list of 1-D clips of any lengths, or (wave [b, L], lengths).
     embed_fn(wave [b, L] on device, lengths=None | list, out=None | [b, *out_shape]) ->
     [b, *out_shape] fp32 on device (``lengths`` / ``out`` are passed only if it accepts them;
-    without ``lengths`` a ragged batch is an error).
+    without ``lengths`` a ragged batch is an error).  If embed_fn has a ``finish()`` attribute it is
+    called once after the rank's last batch, before the exchange (sse_embed_fn: the fp16-range check).
+    item_lengths (optional, n_items sample counts): shards balanced by samples (balanced_bounds)
+    instead of by count; the exchange pads every shard to the longest one and the result is
+    restored to corpus order.
     """
     import torch.distributed as dist
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    start, stop, per = shard_bounds(n_items, world, rank)
+    if item_lengths is not None:
+        if len(item_lengths) != n_items:
+            raise ValueError(f"item_lengths has {len(item_lengths)} entries for {n_items} items")
+        bounds = balanced_bounds(item_lengths, world)
+        start, stop = bounds[rank], bounds[rank + 1]
+        per = max(bounds[r + 1] - bounds[r] for r in range(world))
+    else:
+        start, stop, per = shard_bounds(n_items, world, rank)
+        bounds = None
     dev = torch.device(device)
     local = torch.zeros((per,) + tuple(out_shape), dtype=torch.float32, device=dev)
     takes_len, takes_out = _accepts(embed_fn, "lengths"), _accepts(embed_fn, "out")
@@ -168,11 +205,16 @@ def extract_corpus(clip_source: Callable[[int, int], object], n_items: int,
             nxt = fetch(i + 1)             # staged (host pack + async copy) while batch i computes
         if res is not None and res.data_ptr() != local[s - start:e - start].data_ptr():
             local[s - start:e - start] = res
+    finish = getattr(embed_fn, "finish", None)
+    if callable(finish):
+        finish()
     if not dist.is_initialized():
         return local[:n_items]
     full = torch.empty((world * per,) + tuple(out_shape), dtype=torch.float32, device=dev)
     dist.all_gather_into_tensor(full, local, group=group)
-    return full[:n_items]
+    if bounds is None:
+        return full[:n_items]
+    return torch.cat([full[r * per:r * per + bounds[r + 1] - bounds[r]] for r in range(world)])
 
 
 def sse_embed_fn(model, layer_indices) -> Callable[..., torch.Tensor]:
@@ -180,6 +222,49 @@ def sse_embed_fn(model, layer_indices) -> Callable[..., torch.Tensor]:
     ragged batches through ``lengths``."""
     idx = [int(i) for i in layer_indices]
 
+    # no per-batch range check (it synchronises the stream and would cancel the staged copy / compute
+    # overlap): fp16 / fp16x3 models are checked once, by finish(), after the rank's last batch
     def fn(wave, lengths=None, out=None):
-        return model.embed(wave, idx, out=out, lengths=lengths)
+        return model.embed(wave, idx, out=out, lengths=lengths, check_range=False)
+    fn.finish = model.check_range_now
     return fn
+
+
+class StepGather:
+    """The weak-scaling step of bench.py --gpus N (BASELINE configs[3] per-step form): each step embeds
+    one local batch into one of two output slots, then issues the all-gather of that slot with
+    ``async_op=True`` (RCCL runs it on its own stream), so step k's exchange overlaps step k+1's
+    compute.  A slot is rewritten only after the gather that last read it has completed; ``drain()``
+    waits for every outstanding gather (before the closing barrier of a timed region).
+
+    embed(out) writes this rank's [B, ...] embeddings into ``out`` (on the compute stream)."""
+
+    def __init__(self, embed: Callable[[torch.Tensor], object], out_shape: tuple, world: int, device,
+                 dist=None, group=None):
+        self.embed = embed
+        self.dist = dist
+        self.group = group
+        dev = torch.device(device)
+        self.outs = [torch.empty(tuple(out_shape), dtype=torch.float32, device=dev) for _ in range(2)]
+        self.gathered = ([torch.empty((world * out_shape[0],) + tuple(out_shape[1:]), dtype=torch.float32, device=dev)
+                          for _ in range(2)] if dist is not None else None)
+        self.pending = [None, None]
+        self.steps = 0
+
+    def step(self) -> int:
+        slot = self.steps % 2
+        self.steps += 1
+        if self.pending[slot] is not None:     # the gather that last read this slot
+            self.pending[slot].wait()
+            self.pending[slot] = None
+        self.embed(self.outs[slot])
+        if self.dist is not None:
+            self.pending[slot] = self.dist.all_gather_into_tensor(self.gathered[slot], self.outs[slot],
+                                                                  group=self.group, async_op=True)
+        return slot
+
+    def drain(self) -> None:
+        for i in range(2):
+            if self.pending[i] is not None:
+                self.pending[i].wait()
+                self.pending[i] = None

@@ -721,7 +721,12 @@ constexpr int G8P_SMEM = G8_OPS + 2 * G8P_EP;
 //   o = act(rstd_m * acc + (bias[n] - rstd_m mean_m acol[n]))   (folded LayerNorm of A, GemmArgs.apart)
 //   o = act(acc + bias[n])                                        (otherwise: rstd = 1 and the acol term
 //                                                                  is not formed, bit-identical to a plain add)
-template <int ACT, bool CT3, bool F16, bool has_bias, bool fold>
+// DBG (timing probes only, tools/gemm8_probe.hip; the library launches DBG = 0): 1 = math without the
+// stores (results kept live by an empty asm), 3 = stores of the raw accumulators without the math,
+// 4 = stores in a full-line address pattern (wrong addresses: timing only), 5 = non-temporal stores,
+// 6 = every tile's stores into the same 128 KiB, 7 = half of the stores, 8 = math without the stores plus
+// one garbage 16-B store per lane in every steady main-loop phase (3x the tile's store count, spread).
+template <int ACT, bool CT3, bool F16, bool has_bias, bool fold, int DBG = 0>
 SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, int n0, int wm, int wn, int q,
                           int r16, const char* ep) {
   const float alpha = F16 ? g.alpha : 1.f;   // split-fp16: the weights' 2^s undone (exact)
@@ -747,6 +752,7 @@ SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, i
       ast[mi][i] = fold ? st : make_float2(0.f, alpha);
     }
   auto finish_half = [&](int mi) {
+    if constexpr (DBG == 3) return;
     #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float rs = ast[mi][i].y, nm = -ast[mi][i].x * ast[mi][i].y;
@@ -805,6 +811,32 @@ SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, i
           const auto s0 = __builtin_amdgcn_permlane16_swap(X.x, Y.x, false, false);
           const auto s1 = __builtin_amdgcn_permlane16_swap(X.y, Y.y, false, false);
           const long long c = n0 + ni * 128 + wn * 32 + (q & 1) * 16 + (q >> 1) * 8;
+          if constexpr (DBG == 1 || DBG == 8) {
+            asm volatile("" ::"v"(s0[0]), "v"(s0[1]), "v"(s1[0]), "v"(s1[1]));
+            continue;
+          }
+          if constexpr (DBG == 4) {   // same data and count, full-line pattern: 8 rows x 128 B per store
+            const int r = m0 + mi * 128 + wm * 64 + i * 16 + ni * 8 + (threadIdx.x & 63) / 8;
+            if (r < g.M)
+              *(uint4*)((bf16*)g.Ct + (long long)r * g.ldc + n0 + wn * 64 + (threadIdx.x & 7) * 8) =
+                  make_uint4(s0[0], s1[0], s0[1], s1[1]);
+            continue;
+          }
+          if constexpr (DBG == 6) {   // every tile into the same 128 KiB (L2-resident)
+            const long long c6 = ni * 128 + wn * 32 + (q & 1) * 16 + (q >> 1) * 8;
+            const long long r6 = (long long)(mi * 128 + wm * 64 + i * 16 + r16) * 256;
+            *(uint4*)((bf16*)g.Ct + r6 + c6) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+            continue;
+          }
+          if constexpr (DBG == 7) {   // half the stores (ni = 0 only)
+            if (ni == 0 && ok) *(uint4*)((bf16*)g.Ct + row + c) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+            else asm volatile("" ::"v"(s0[0]), "v"(s0[1]), "v"(s1[0]), "v"(s1[1]));
+            continue;
+          }
+          if constexpr (DBG == 5) {   // non-temporal stores
+            if (ok) __builtin_nontemporal_store(i32x4{(int)s0[0], (int)s1[0], (int)s0[1], (int)s1[1]}, (i32x4*)((bf16*)g.Ct + row + c));
+            continue;
+          }
           if (ok) {
             const uint4 v = make_uint4(s0[0], s1[0], s0[1], s1[1]);
             *(uint4*)((bf16*)g.Ct + row + c) = v;
@@ -835,7 +867,8 @@ SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, i
 // ======================================================================================
 // EP: bit 0 = bias present, bit 1 = folded LayerNorm (apart/acol) -- compile-time, so an absent term
 // costs no epilogue instruction (runtime selects measured +5-6 % on conv1 / ffn1 when removed).
-template <int ACT, bool CT3 = false, bool F16 = false, int EP = 1>
+// DBG (timing probes only): see g8p_epilogue; 2 = no epilogue at all (accumulators kept live).
+template <int ACT, bool CT3 = false, bool F16 = false, int EP = 1, int DBG = 0>
 __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
   __shared__ __attribute__((aligned(16))) char smem[G8P_SMEM];   // operands | 2 epilogue slots: the ONLY shared object
   const int lane = threadIdx.x & 63;
@@ -989,7 +1022,14 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
         if constexpr (FI) {
           g8_vmcnt_dyn<false>(g8_count<false>(kk, nk) + S);
         } else if constexpr (ST) {
-          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          if constexpr (DBG == 8) {   // probe: one 16-B store per lane per steady phase, after the wait
+            g8_vmcnt_dyn<true>(8 + min(3, kk - 4));
+            const int r8 = m0 + wave * 32 + (lane >> 1);
+            if (r8 < M)
+              *(bf16x8*)((bf16*)g.Ct + (long long)r8 * g.ldc + n0 + (lane & 1) * 8 + (kk & 15) * 16) = af[0][0];
+          } else {
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          }
         } else {
           g8_wait<false>(kk, nk);
         }
@@ -1028,10 +1068,19 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
       setup(next);
       for (int k = -6; k < 0; ++k) issue(k);
     }
-    g8p_epilogue<ACT, CT3, F16, has_bias, fold>(g, acc, m0, n0, wm, wn, q, r16, smem + G8_OPS + slot * G8P_EP);
+    if constexpr (DBG == 2) {
+      #pragma unroll
+      for (int a = 0; a < 2; ++a)
+        #pragma unroll
+        for (int c = 0; c < 2; ++c)
+          #pragma unroll
+          for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(acc[a][c][i][0]), "v"(acc[a][c][i][1]));
+    } else {
+      g8p_epilogue<ACT, CT3, F16, has_bias, fold, DBG>(g, acc, m0, n0, wm, wn, q, r16, smem + G8_OPS + slot * G8P_EP);
+    }
     if (next < 0) break;
     slot ^= 1;
-    S = m0 + 256 <= M ? s_full : 0;
+    S = (DBG == 1 || DBG == 2 || DBG == 8) ? 0 : (m0 + 256 <= M ? (DBG == 7 ? s_full / 2 : s_full) : 0);
     tile = next;
   }
 }

@@ -178,7 +178,7 @@ __global__ __launch_bounds__(256) void lm_stft_mel_kernel(const float* __restric
   __shared__ int2 fs[LM_MAXMEL];
   const int b = blockIdx.y, t0 = blockIdx.x * MEL_FR;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int Lv = lens ? (lens[b] < NS ? lens[b] : NS) : Lv0;   // the clip's samples, zeros after
+  const int Lv = lens ? min(max(lens[b], 0), Lv0) : Lv0;   // the clip's samples (clamped to [0, min(L, NS)]), zeros after
   const float* xw = wave + (long long)b * L;
   for (int i = threadIdx.x; i < SPAN; i += 256) {   // padded index HOP t0 + i -> reflect -> zero-pad
     int j = HOP * t0 + i - PAD;
@@ -384,7 +384,7 @@ __global__ __launch_bounds__(64 * LM_W) void lm_stft_mel4_kernel(const float* __
   // samples of chunk c (zero-pad / truncate to 480000, reflect-pad 200) into registers
   auto load_chunk = [&](int c) {
     const int b = c / LM_CPC, t0 = (c - b * LM_CPC) * MEL_FR;
-    const int Lv = lens ? (lens[b] < NS ? lens[b] : NS) : Lv0;
+    const int Lv = lens ? min(max(lens[b], 0), Lv0) : Lv0;   // clamped to [0, min(L, NS)]
     const float* xw = wave + (long long)b * L;
     #pragma unroll
     for (int u = 0; u < NX; ++u) {

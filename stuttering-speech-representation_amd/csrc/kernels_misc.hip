@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void conv0_moments_kernel(const float* __restr
                                                             double* __restrict__ mom, const int* __restrict__ t0len) {
   const int ch = blockIdx.x, b = blockIdx.y;
   const int T0 = t0len ? t0len[b] : T0S;
-  const int per = (T0S + MOM_NCH - 1) / MOM_NCH;
+  const int per = (T0 + MOM_NCH - 1) / MOM_NCH;   // the clip's own chunks: batch-independent grouping
   const int te = min(ch * per + per, T0);
   const float* xb = x + (long long)b * L;
   float mu = 0.f, rs = 1.f;

@@ -851,8 +851,8 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     g.rows_per_seg = Tf; g.T_in = Tf; g.stride = 1; g.pad = K / 2; g.cin = cg; g.ld_in = H;
     g.bias = m->ptr<float>(m->pos_b); g.resid = x; g.Cf = x; g.ldc = H; g.act = ACT_GELU; g.zero = zero;
     // bf16: the dedicated kernel (input window staged once per block, kernels_posconv.hip);
-    // OPT_POSCONV_GEMM keeps the grouped GEMM for A/B runs
-    const bool use_gemm = sizeof(T) != 2 || sse_opt(OPT_POSCONV_GEMM);
+    // OPT_POSCONV_GEMM keeps the grouped GEMM for bf16 A/B runs (the grouped GEMM has no fp16 form: ignored for fp16)
+    const bool use_gemm = sizeof(T) != 2 || (!is_f16_v<T> && sse_opt(OPT_POSCONV_GEMM));
     RC(prof(m, s, "gemm_conv:posconv", gflops(g, G), gbytes<T>(g, AMODE_CONV, G), [&] {
       if (!use_gemm) {
         const int rc = launch_posconv_bf16((const bf16*)xt, m->ptr<bf16>(m->pos_w), m->ptr<float>(m->pos_b), x, B, Tf, H,

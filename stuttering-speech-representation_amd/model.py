@@ -136,8 +136,8 @@ class SSEModel:
         non-finite value (fp16 / fp16x3 models; a no-op for the others)."""
         _lib.check(_lib.lib().sse_check_range(self._h, self._stream()), "sse_check_range")
 
-    def _after(self):
-        if self.check_range:
+    def _after(self, check_range: bool | None = None):
+        if self.check_range if check_range is None else (check_range and self.dtype in FP16_RANGE):
             self.check_range_now()
 
     def _check_wave(self, wave: torch.Tensor) -> torch.Tensor:
@@ -173,10 +173,11 @@ class SSEModel:
 
     # -- compute --------------------------------------------------------------------------
     def embed(self, wave: torch.Tensor, layer_indices, out: torch.Tensor | None = None,
-              lengths=None, workspace: torch.Tensor | None = None) -> torch.Tensor:
+              lengths=None, workspace: torch.Tensor | None = None, check_range: bool | None = None) -> torch.Tensor:
         """[B, L] fp32 16 kHz waves -> [B, len(layer_indices), H] fp32 time-means of hidden states.
         ``lengths`` (ragged batch): samples of each clip, its first lengths[b] samples of row b; each
-        clip is embedded at its own length (sse_embed_ragged)."""
+        clip is embedded at its own length (sse_embed_ragged).  ``check_range`` overrides the model's
+        per-call fp16-range check (False in throughput loops, which call check_range_now() once)."""
         wave = self._check_wave(wave)
         B, L = wave.shape
         ids = torch.tensor([int(i) for i in layer_indices], dtype=torch.int32)
@@ -192,7 +193,7 @@ class SSEModel:
         if lengths is None:
             _lib.check(_lib.lib().sse_embed(self._h, wave.data_ptr(), B, L, ids.data_ptr(), n, out.data_ptr(),
                                             ws.data_ptr(), ws.numel(), self._stream()), "sse_embed")
-            self._after()
+            self._after(check_range)
             return out
         lens = [int(v) for v in (lengths.tolist() if isinstance(lengths, torch.Tensor) else lengths)]
         if len(lens) != B or min(lens) < 1 or max(lens) > L:
@@ -206,7 +207,7 @@ class SSEModel:
         _lib.check(_lib.lib().sse_embed_ragged(self._h, wave.data_ptr(), d_len.data_ptr(), B, L, ids.data_ptr(), n,
                                                out.data_ptr(), ws.data_ptr(), ws.numel(), self._stream()),
                    "sse_embed_ragged")
-        self._after()
+        self._after(check_range)
         return out
 
     def embed_clips(self, clips, layer_indices) -> torch.Tensor:

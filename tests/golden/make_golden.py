@@ -268,7 +268,7 @@ def outlier_golden(ref_w, ref_h, manifest):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-large", action="store_true")
-    ap.add_argument("--only", default=None, help="wavlm | wavlm_large | whisper_tiny | outlier | whisper_large_v2")
+    ap.add_argument("--only", default=None, help="wavlm | wavlm_large | whisper_tiny | whisper_small | outlier | whisper_large_v2")
     args = ap.parse_args()
     torch.set_num_threads(os.cpu_count())
     manifest = {"transformers": transformers.__version__, "torch": torch.__version__, "numpy": np.__version__}
@@ -288,6 +288,8 @@ def main():
                 whisper_golden(ref_h, manifest, C.WHISPER_TINY_DEC, "whisper_tiny", 2, 11, [3.0, 30.0])
             if only in (None, "outlier"):
                 outlier_golden(ref_w, ref_h, manifest)
+            if only in (None, "whisper_small"):   # the reference's default Whisper (REF :34)
+                whisper_golden(ref_h, manifest, C.WHISPER_SMALL_DEC, "whisper_small", 2, 11, [3.0, 12.0])
             if not args.skip_large and only in (None, "whisper_large_v2"):
                 whisper_golden(ref_h, manifest, C.WHISPER_LARGE_V2_DEC, "whisper_large_v2", 1, 11, [3.0])
         finally:

@@ -132,3 +132,123 @@ def test_extract_corpus_out_and_lengths_protocol():
     assert seen[-1][0] is None
     with pytest.raises(ValueError):
         extract_corpus(lambda s, e: [_ragged_clip(i) for i in range(s, e)], 3, _embed, (2, 3), "cpu", batch=2)
+
+
+def _balanced_worker(rank, world, port, lens, batch, q):
+    import importlib
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    importlib.import_module("stuttering-speech-representation_amd")
+    import torch.distributed as dist
+    from ssr_amd.corpus import extract_corpus
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    calls = {"finish": 0, "samples": 0}
+
+    def fn(wave, lengths=None, out=None):
+        calls["samples"] += sum(lengths)
+        return _embed_ragged(wave, lengths=lengths, out=out)
+    fn.finish = lambda: calls.__setitem__("finish", calls["finish"] + 1)
+
+    def clip(i):
+        return np.sin(i * 0.37 + np.arange(lens[i], dtype=np.float32) * 0.11).astype(np.float32)
+    try:
+        out = extract_corpus(lambda s, e: [clip(i) for i in range(s, e)], len(lens), fn, (2, 3), "cpu", batch=batch,
+                             item_lengths=lens)
+        q.put((rank, (out.numpy(), calls["finish"], calls["samples"])))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,batch", [(2, 4), (3, 3)])
+def test_length_balanced_shards_restore_corpus_order(world, batch):
+    """a corpus ordered by length (a sorted manifest) sharded by samples, not by count:
+    every rank embeds ~1/world of the samples, finish() runs once per rank, and the gathered matrix is
+    each clip's own embedding in corpus order."""
+    lens = [20 + 3 * i for i in range(13)]          # ascending lengths: count shards would be unbalanced
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 33500 + (os.getpid() % 1000) + world * 13
+    procs = [ctx.Process(target=_balanced_worker, args=(r, world, port, lens, batch, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = torch.stack([_embed_one(torch.from_numpy(
+        np.sin(i * 0.37 + np.arange(n, dtype=np.float32) * 0.11).astype(np.float32))) for i, n in enumerate(lens)]).numpy()
+    total = sum(lens)
+    for r in range(world):
+        out, fin, samples = res[r]
+        assert np.array_equal(out, ref), r
+        assert fin == 1
+        assert abs(samples - total / world) <= max(lens), (r, samples, total / world)
+
+
+def test_balanced_bounds_cover_and_balance():
+    import importlib
+    importlib.import_module("stuttering-speech-representation_amd")
+    from ssr_amd.corpus import balanced_bounds
+    rng = np.random.default_rng(5)
+    for n, w in [(1, 1), (5, 8), (8, 8), (13, 3), (1000, 8)]:
+        for lens in (sorted(rng.integers(400, 480000, n).tolist()), [48000] * n, rng.integers(1, 10, n).tolist()):
+            b = balanced_bounds(lens, w)
+            assert b[0] == 0 and b[-1] == n and len(b) == w + 1
+            assert all(b[i] <= b[i + 1] for i in range(w))
+            if n >= w:
+                assert all(b[i] < b[i + 1] for i in range(w)), (n, w, b)
+                share = [sum(lens[b[i]:b[i + 1]]) for i in range(w)]
+                assert max(share) - sum(lens) / w <= 2 * max(lens)
+
+
+def _step_gather_worker(rank, world, port, steps, q):
+    import importlib
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    importlib.import_module("stuttering-speech-representation_amd")
+    import torch.distributed as dist
+    from ssr_amd.corpus import StepGather
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        k = [0]
+
+        def embed(out):      # step k on rank r writes r * 1000 + k + the row index
+            out.copy_(torch.arange(out.shape[0], dtype=torch.float32)[:, None, None].expand_as(out) + rank * 1000 + k[0])
+            k[0] += 1
+        pipe = StepGather(embed, (3, 2, 4), world, "cpu", dist)
+        seen = []
+        for _ in range(steps):
+            slot = pipe.step()
+            seen.append((slot, pipe.pending[1 - slot] is None or pipe.steps >= 2))
+        pipe.drain()
+        assert all(p is None for p in pipe.pending)
+        q.put((rank, ([s for s, _ in seen], [g.numpy().copy() for g in pipe.gathered], pipe.steps)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,steps", [(2, 5), (3, 4)])
+def test_step_gather_two_slots_and_drain(world, steps):
+    """bench.py's weak-scaling step (async all-gather into two slots, a slot reused
+    only after its gather completed, drain before the closing barrier) on gloo: after the drain each
+    slot holds the all-gather of the last step that wrote it, ranks in order."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 35500 + (os.getpid() % 1000) + world * 17 + steps
+    procs = [ctx.Process(target=_step_gather_worker, args=(r, world, port, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        slots, gathered, n = res[r]
+        assert n == steps and slots == [i % 2 for i in range(steps)]
+        for slot in (0, 1):
+            last = max(i for i in range(steps) if i % 2 == slot)
+            exp = np.concatenate([np.arange(3, dtype=np.float32)[:, None, None] + rr * 1000 + last
+                                  for rr in range(world)])
+            assert np.array_equal(gathered[slot], np.broadcast_to(exp, (world * 3, 2, 4))), (r, slot)

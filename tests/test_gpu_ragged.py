@@ -116,3 +116,29 @@ def test_wavlm_ragged_c_abi_clamps_out_of_range_lengths(wavlm_sd):
     full = m.embed(wave[:2], [12, 6, 0])
     assert torch.equal(out[0], full[0]) and torch.equal(out[1], full[1])
     assert (out[2:] == 0).all()
+
+
+def test_whisper_ragged_c_abi_clamps_out_of_range_lengths():
+    """the log-mel kernels clamp each ragged length to [0, min(L, 480000)], so a Whisper clip
+    whose length exceeds its row reads only its row (the same as lens = L) and a negative length is
+    silence (the same as an all-zero row)."""
+    from ssr_amd import _lib, config as C, synth
+    from ssr_amd.model import SSEModel
+    m = SSEModel(C.WHISPER_TINY, synth.synth_whisper_state_dict(C.WHISPER_TINY, seed=11), device="cuda:0",
+                 dtype="fp32")
+    L = 32000
+    wave = torch.from_numpy(synth.synth_clips(3, L, seed=43)).cuda()
+    lens = torch.tensor([10 * L, -5, L // 2], dtype=torch.int32, device="cuda")
+    ids = torch.tensor([C.WHISPER_TINY.layers, 0], dtype=torch.int32)
+    out = torch.full((3, 2, C.WHISPER_TINY.hidden), float("nan"), device="cuda")
+    ws = m.workspace(3, L)
+    rc = _lib.lib().sse_embed_ragged(m._h, wave.data_ptr(), lens.data_ptr(), 3, L, ids.data_ptr(), 2, out.data_ptr(),
+                                     ws.data_ptr(), ws.numel(), m._stream())
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    ref = wave.clone()
+    ref[1].zero_()
+    ref[2, L // 2:].zero_()
+    full = m.embed(ref, [C.WHISPER_TINY.layers, 0])
+    assert torch.equal(out, full)

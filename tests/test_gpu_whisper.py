@@ -222,3 +222,32 @@ def test_whisper_large_v2_bench_batch(dtype, B, tol, cos_min):
                                                   np.linalg.norm(g["emb"][0], axis=-1))).min()
         print(dtype, B, "pos", q, "rel-L2", rel, "cos", cos)
         assert rel <= tol and cos >= cos_min
+
+
+@pytest.mark.parametrize("dtype,tol,cos_min", [("fp32", 1e-4, 0.9999999), ("bf16", 3e-2, 0.999), ("fp8", 0.08, 0.995)])
+def test_whisper_small_matches_reference(dtype, tol, cos_min):
+    """openai/whisper-small (768 / 12 layers / 12 heads / 3072), the reference's
+    default Whisper (REF/whisper_embeddings_large.py:34), pinned by the reference's own
+    extract_whisper_embeddings_fixed on a 3 s and a 12 s clip (encoder_layer_{12,11,10} and the
+    1-token decoder's decoder_layer_{12,11,10,0}).  fp8 = MX-fp8 encoder GEMMs (the decoder runs bf16)."""
+    p = os.path.join(GOLDEN, "whisper_small.npz")
+    if not os.path.exists(p):
+        pytest.skip("whisper-small fixture not generated")
+    from ssr_amd import config as C, synth
+    from ssr_amd.model import SSEModel
+    g = np.load(p)
+    clips = _clips(None, [3.0, 12.0])
+    w = torch.zeros((2, 480000), device="cuda:0")
+    for i, c in enumerate(clips):
+        w[i, :c.shape[0]] = torch.from_numpy(c)
+    idx = [int(i) for i in g["layer_indices"]]
+    dec = [int(i) for i in g["decoder_indices"]]
+    m = SSEModel(C.WHISPER_SMALL_DEC, synth.synth_whisper_state_dict(C.WHISPER_SMALL_DEC, seed=11), device="cuda:0",
+                 dtype=dtype)
+    e, d = m.whisper_embed(w, idx, dec)
+    e, d = e.cpu().numpy(), d.cpu().numpy()
+    for name, got, ref in (("enc", e, g["emb"]), ("dec", d, g["dec_emb"])):
+        rel = _rel(got, ref).max()
+        cos = ((got * ref).sum(-1) / (np.linalg.norm(got, axis=-1) * np.linalg.norm(ref, axis=-1))).min()
+        print(dtype, "whisper-small", name, "rel-L2", rel, "cos", cos)
+        assert rel <= tol and cos >= cos_min, (name, rel, cos)

@@ -21,6 +21,15 @@ def test_recoverable_errors_only():
         return [f"e{j}" for j in part]
     assert _per_clip_fallback(bad_clip, [0, 1, 2]) == ["e0", None, "e2"]
 
+    from ssr_amd._lib import SSERangeError
+    assert _recoverable(SSERangeError(-7, "fp16 overflow"))
+
+    def overflow_clip(part):               # an fp16 overflow of clip 2 drops only clip 2
+        if 2 in part:
+            raise SSERangeError(-7, "non-finite output")
+        return [f"e{j}" for j in part]
+    assert _per_clip_fallback(overflow_clip, [0, 1, 2, 3]) == ["e0", "e1", None, "e3"]
+
     def dead_gpu(part):                    # a HIP failure is not swallowed clip by clip
         raise SSEError(-2, "hip error")
     with pytest.raises(SSEError):

@@ -1,0 +1,116 @@
+// Where the persistent bf16 GEMM's time goes outside the main loop (round-4 probe, not product code).
+// Times gemm8p_kernel in four builds on the WavLM-base B = 256 shapes, interleaved in one process:
+//   DBG 0 = the library kernel, 1 = epilogue math without stores, 2 = no epilogue, 3 = stores without math,
+//   4 = full math, stores in a full-cache-line pattern (8 rows x 128 B per instruction; timing only), 5 = nt stores,
+//   6 = every tile's stores into one 128 KiB region (L2-resident), 7 = half of the stores,
+//   8 = math without stores + 3x the tile's store count spread over the main loop (one per lane per phase),
+// plus a K sweep at fixed M, N (tile time = nk * T_ktile + F: the per-tile fixed cost F).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off tools/gemm8_probe.hip -o tools/_build/gemm8_probe
+#include "../stuttering-speech-representation_amd/csrc/kernels_gemm8.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+int sse_opt(int) { return 0; }
+
+#define CK(x)                                                                              \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) {                                                                \
+      printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__);        \
+      exit(1);                                                                             \
+    }                                                                                      \
+  } while (0)
+
+__global__ void fill_bf16(bf16* p, long long n, unsigned seed, float scale) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    unsigned h = (unsigned)i * 2654435761u ^ seed;
+    h ^= h >> 15; h *= 2246822519u; h ^= h >> 13; h *= 3266489917u; h ^= h >> 16;
+    p[i] = (bf16)(((float)(h >> 8) * (2.0f / 16777216.0f) - 1.0f) * scale);
+  }
+}
+
+typedef void (*kfn)(GemmArgs, int);
+
+template <int ACT, int EP>
+static kfn pick(int dbg) {
+  switch (dbg) {
+    case 1: return gemm8p_kernel<ACT, false, false, EP, 1>;
+    case 2: return gemm8p_kernel<ACT, false, false, EP, 2>;
+    case 3: return gemm8p_kernel<ACT, false, false, EP, 3>;
+    case 4: return gemm8p_kernel<ACT, false, false, EP, 4>;
+    case 5: return gemm8p_kernel<ACT, false, false, EP, 5>;
+    case 6: return gemm8p_kernel<ACT, false, false, EP, 6>;
+    case 7: return gemm8p_kernel<ACT, false, false, EP, 7>;
+    case 8: return gemm8p_kernel<ACT, false, false, EP, 8>;
+    default: return gemm8p_kernel<ACT, false, false, EP, 0>;
+  }
+}
+
+struct Shape { const char* name; int M, N, K, act, ep; };
+
+int main() {
+  int cus = 256;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  const Shape shapes[] = {
+      {"qkv", 38144, 2560, 768, ACT_NONE, 1},        {"qkv_fold", 38144, 2560, 768, ACT_NONE, 3},
+      {"ffn1", 38144, 3072, 768, ACT_GELU_FAST, 1},  {"ffn1_fold", 38144, 3072, 768, ACT_GELU_FAST, 3},
+      {"conv1", 1228544, 512, 1536, ACT_GELU_FAST, 0}, {"k1536", 38144, 2560, 1536, ACT_NONE, 1},
+      {"k3072", 38144, 2560, 3072, ACT_NONE, 1},     {"sq4096", 4096, 4096, 4096, ACT_NONE, 0},
+  };
+  const long long maxA = 1228544LL * 1536, maxB = 4096LL * 4096, maxC = 1228544LL * 512;
+  bf16 *a, *b, *c;
+  float *bias, *acol;
+  float2* apart;
+  void* zero;
+  CK(hipMalloc(&a, maxA * 2)); CK(hipMalloc(&b, maxB * 2 * 2)); CK(hipMalloc(&c, maxC * 2 * 2));
+  CK(hipMalloc(&bias, 4096 * 4)); CK(hipMalloc(&acol, 4096 * 4)); CK(hipMalloc(&apart, 38144LL * 3 * 8));
+  CK(hipMalloc(&zero, 256)); CK(hipMemset(zero, 0, 256));
+  hipLaunchKernelGGL(fill_bf16, dim3(2048), dim3(256), 0, 0, a, maxA, 17u, 1.0f);
+  hipLaunchKernelGGL(fill_bf16, dim3(2048), dim3(256), 0, 0, b, maxB * 2, 91u, 0.036f);
+  {
+    std::vector<float> h(4096, 0.01f);
+    CK(hipMemcpy(bias, h.data(), 4096 * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(acol, h.data(), 4096 * 4, hipMemcpyHostToDevice));
+    std::vector<float2> p(38144 * 3, make_float2(0.f, 256.f));
+    CK(hipMemcpy(apart, p.data(), p.size() * 8, hipMemcpyHostToDevice));
+  }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  const int ROUNDS = 3, IT = 20;
+  for (const Shape& s : shapes) {
+    GemmArgs g{};
+    g.A = a; g.B = b; g.M = s.M; g.N = s.N; g.K = s.K; g.rows_per_seg = s.M; g.lda = s.K;
+    g.bias = (s.ep & 1) ? bias : nullptr; g.Ct = c; g.ldc = s.N; g.act = s.act; g.zero = zero;
+    if (s.ep & 2) { g.apart = apart; g.apart_nt = 3; g.acol = acol; g.ln_eps = 1e-5f; }
+    const int n_tiles = ((s.M + 255) / 256) * (s.N / 256);
+    const int G = n_tiles < cus ? n_tiles : cus;
+    const double tf = 2.0 * s.M * s.N * s.K / 1e12;
+    double best[9] = {1e30, 1e30, 1e30, 1e30, 1e30, 1e30, 1e30, 1e30, 1e30};
+    for (int r = 0; r < ROUNDS; ++r)
+      for (int dbg = 0; dbg < 9; ++dbg) {
+        kfn k;
+        if (s.act == ACT_GELU_FAST) k = s.ep == 3 ? pick<ACT_GELU_FAST, 3>(dbg) : (s.ep == 1 ? pick<ACT_GELU_FAST, 1>(dbg) : pick<ACT_GELU_FAST, 0>(dbg));
+        else k = s.ep == 3 ? pick<ACT_NONE, 3>(dbg) : (s.ep == 1 ? pick<ACT_NONE, 1>(dbg) : pick<ACT_NONE, 0>(dbg));
+        for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(k, dim3(G), dim3(512), 0, 0, g, n_tiles);
+        CK(hipEventRecord(e0, 0));
+        for (int i = 0; i < IT; ++i) hipLaunchKernelGGL(k, dim3(G), dim3(512), 0, 0, g, n_tiles);
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        ms /= IT;
+        if (ms < best[dbg]) best[dbg] = ms;
+      }
+    const double rounds = (double)n_tiles / cus;
+    printf("%-10s M=%d N=%d K=%d tiles=%d (%.2f rounds)\n", s.name, s.M, s.N, s.K, n_tiles, rounds);
+    const char* nm[9] = {"full", "math,no-store", "no-epilogue", "store,no-math", "full-line stores", "nt stores",
+                         "L2-resident st", "half stores", "3x st in loop"};
+    for (int d = 0; d < 9; ++d)
+      printf("   %-14s %8.1f us  %7.1f TF/s  per-round %.2f us\n", nm[d], best[d] * 1e3, tf / (best[d] * 1e-3),
+             best[d] * 1e3 / __builtin_ceil(rounds));
+    fflush(stdout);
+  }
+  return 0;
+}
