@@ -44,7 +44,8 @@ from ssr_amd.model import SSEModel  # noqa: E402
 from ssr_amd.corpus import StepGather  # noqa: E402
 
 # Algorithmic FLOPs per clip: 2 x MACs of every GEMM/conv + QK^T, AV.
-FLOP_PER_CLIP = {"wavlm-base": 42.39e9, "wavlm-large": 109.6e9, "whisper-large-v2": 2272.67e9}
+FLOP_PER_CLIP = {"wavlm-base": 42.39e9, "wavlm-large": 109.6e9, "whisper-large-v2": 2272.67e9,
+                 "whisper-small": 344.16e9}   # whisper-small: conv 6.41 + 12 x 28.15 (attention 6.91) GF
 # MI355X dense MFMA peaks (MI355X_MICROARCH.md); fp16x3 runs three fp16 products per logical
 # multiply-add, so its model-level peak is the fp16 (= bf16) peak / 3 (its GEMM roofline counts the MFMA work)
 PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 157.3, "fp8": 5000.0, "fp16x3": 2500.0 / 3}
@@ -56,14 +57,16 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--model", default="wavlm-base", choices=["wavlm-base", "wavlm-large", "whisper-large-v2"],
-                    help="wavlm-large: the reference's default --model_name (REF/WavLM_embeddings.py:34)")
+    ap.add_argument("--model", default="wavlm-base",
+                    choices=["wavlm-base", "wavlm-large", "whisper-large-v2", "whisper-small"],
+                    help="wavlm-large: the reference's default --model_name (REF/WavLM_embeddings.py:34); "
+                         "whisper-small: the default of REF/whisper_embeddings_large.py:34")
     ap.add_argument("--batch", type=int, default=None,
                     help="clips per rank per step (default 256 WavLM / 64 Whisper bf16 / 128 Whisper fp8)")
     ap.add_argument("--seconds", type=float, default=None, help="clip length (default 3 s / 30 s)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8", "fp16x3", "fp16"],
                     help="fp8: Whisper only, MX-fp8 QKV / fc1 / fc2 GEMMs (BASELINE configs[4]); fp16x3: "
-                         "WavLM-base, split-fp16 GEMMs, fp32-class (<= 1e-4) embeddings; fp16: WavLM-base, the bf16 "
+                         "WavLM / Whisper, split-fp16 GEMMs, fp32-class (<= 1e-4) embeddings; fp16: WavLM, the bf16 "
                          "path with fp16 activations / operands (same MFMA rate, 8 more mantissa bits)")
     ap.add_argument("--cpu-sample", type=int, default=None, help="clips for the CPU baseline (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-launch event timing")
@@ -104,8 +107,8 @@ def cpu_model() -> str:
     return "unknown"
 
 
-CALIBRATION = "profiles/r2_cpu_baseline_calibration.json"
-CALIBRATION_WHISPER = "profiles/r3_cpu_baseline_calibration_whisper.json"
+CALIBRATION = "profiles/r4_cpu_baseline_calibration_wavlm.json"   # 16 clips x 7 alternating rounds
+CALIBRATION_WHISPER = "profiles/r4_cpu_baseline_calibration_whisper.json"   # encoder-only, 8 clips x 5 rounds
 
 
 def cpu_baseline(model_name: str, n: int, seconds: float):
@@ -137,13 +140,14 @@ def cpu_baseline(model_name: str, n: int, seconds: float):
                           f"fp32 ATen ops, torch.set_num_threads({thr})), {dt:.1f} s"}
     # Whisper: oracle/whisper_aten.py, the reference's extract_whisper_embeddings_fixed on the same ATen
     # ops (log-mel via torch.stft, HF WhisperEncoder's convs / addmm / SDPA / LayerNorm), batch-1,
-    # calibrated against the reference itself (oracle/calibrate_cpu_baseline.py --model whisper-large-v2,
-    # which times the reference WITH its 1-token decoder pass).  Timed here on the encoder part only:
-    # the GPU line measures encoder embeddings (BASELINE configs[2] / [4]).
+    # calibrated against the reference itself, like for like (oracle/calibrate_cpu_baseline.py --model
+    # whisper-large-v2: the reference's model with decoder_layers = 0, so its 1-token decoder pass is one
+    # embedding row; round 4).  Timed here on the encoder part only: the GPU line measures encoder
+    # embeddings (BASELINE configs[2] / [4]).
     from oracle.whisper_aten import WhisperAten
     thr = host_threads()
     torch.set_num_threads(thr)
-    spec = C.WHISPER_LARGE_V2
+    spec = C.WHISPER_SMALL if model_name == "whisper-small" else C.WHISPER_LARGE_V2
     o = WhisperAten(spec, synth.synth_whisper_state_dict(spec, seed=11))
     clips = synth.synth_clips(n + 1, int(16000 * seconds), seed=2024)
     idx = spec.default_layer_indices()
@@ -350,7 +354,8 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     wavlm = a.model.startswith("wavlm")
-    spec = {"wavlm-base": C.WAVLM_BASE, "wavlm-large": C.WAVLM_LARGE, "whisper-large-v2": C.WHISPER_LARGE_V2}[a.model]
+    spec = {"wavlm-base": C.WAVLM_BASE, "wavlm-large": C.WAVLM_LARGE, "whisper-large-v2": C.WHISPER_LARGE_V2,
+            "whisper-small": C.WHISPER_SMALL}[a.model]
     if a.dtype == "fp8" and wavlm:
         raise SystemExit("--dtype fp8 is the Whisper encoder mode (BASELINE configs[4])")
     B = a.batch or (256 if wavlm else (128 if a.dtype == "fp8" else 64))
