@@ -119,6 +119,36 @@ SSE_DEV f32x2 gelu_bf2(f32x2 x) {
   p = __builtin_elementwise_fma(p, s, f32x2{3.981720209e-01f, 3.981720209e-01f});
   return x * __builtin_elementwise_fma(xc, p, f32x2{0.5f, 0.5f});
 }
+// N independent pairs stage by stage (bit-identical to N calls of gelu_bf2 / gelu_fast2): a lone Horner
+// chain is latency-bound (a dependent packed fma every ~8 cycles plus hazard nops); N chains in lockstep
+// keep the VALU issuing (the persistent GEMM's epilogue runs 8 at a time).
+template <bool H16, int N>
+SSE_DEV void gelu_out2_n(f32x2 (&x)[N]) {
+  constexpr float C = H16 ? 4.5f : 4.0f;
+  constexpr int NC = H16 ? 9 : 7;
+  constexpr float cf[9] = {3.144668553e-11f, -3.420433270e-09f, 1.634204949e-07f, -4.547368462e-06f,
+                           8.266720397e-05f, -1.047152211e-03f, 9.627013467e-03f, -6.607707590e-02f,
+                           3.987890482e-01f};
+  constexpr float cb[7] = {2.368073737e-08f, -1.652635206e-06f, 4.923747110e-05f, -8.292031125e-04f,
+                           8.865549229e-03f, -6.484667212e-02f, 3.981720209e-01f};
+  f32x2 xc[N], s[N], p[N];
+  #pragma unroll
+  for (int n = 0; n < N; ++n) {
+    xc[n] = f32x2{__builtin_amdgcn_fmed3f(x[n].x, -C, C), __builtin_amdgcn_fmed3f(x[n].y, -C, C)};
+    s[n] = xc[n] * xc[n];
+    const float c0 = H16 ? cf[0] : cb[0];
+    p[n] = f32x2{c0, c0};
+  }
+  #pragma unroll
+  for (int k = 1; k < NC; ++k) {
+    const float ck = H16 ? cf[k] : cb[k < 7 ? k : 6];
+    #pragma unroll
+    for (int n = 0; n < N; ++n) p[n] = __builtin_elementwise_fma(p[n], s[n], f32x2{ck, ck});
+  }
+  #pragma unroll
+  for (int n = 0; n < N; ++n) x[n] = x[n] * __builtin_elementwise_fma(xc[n], p[n], f32x2{0.5f, 0.5f});
+}
+
 // the output's polynomial GELU: bf16 only -> gelu_bf2; fp16, fp32 or an fp32 copy (Cf) -> gelu_fast2
 template <bool H16> SSE_DEV f32x2 gelu_out2(f32x2 x) { return H16 ? gelu_fast2(x) : gelu_bf2(x); }
 SSE_DEV f32x2 gelu_out2(f32x2 x, bool bf_only) { return bf_only ? gelu_bf2(x) : gelu_fast2(x); }

@@ -36,9 +36,12 @@ int launch_layernorm(const TI* in, const float* w, const float* b, int rows, int
                      float* out_f, TO* out_t, hipStream_t s, float2* stats = nullptr);
 
 // split-fp16 (SSE_DTYPE_FP16X3) operands: tripled rows [hi | lo' | hi] (common.h x3_split4)
+// act: ACT_NONE or ACT_GELU (erf, fp32 input only: the "layer" conv frontend's LN + GELU)
 int launch_layernorm_x3(const void* in, bool in3, const float* w, const float* b, int rows, int H, float eps,
-                        float* out_f, f16* out3, hipStream_t s);
+                        float* out_f, f16* out3, hipStream_t s, int act = ACT_NONE);
 int launch_split3(const float* x, long long rows, int C, f16* y, hipStream_t s);
+int launch_conv0_ln_x3(const float* x, int B, int L, const float* norm, const float* w0, const float* b0, int C,
+                       int k0, int s0, int T0, const float* lnw, const float* lnb, float eps, f16* out3, hipStream_t s);
 int launch_conv0_gn_x3(const float* x, int B, int L, const float* norm, const float* w0, const float* b0, int C,
                        int k0, int s0, int T0, const float* gamma, const float* beta, float eps, double* mom,
                        float2* ss, f16* out3, hipStream_t s, const int* t0len);

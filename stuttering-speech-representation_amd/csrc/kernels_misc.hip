@@ -273,7 +273,16 @@ __global__ __launch_bounds__(256) void conv0_apply_kernel(const float* __restric
             o[p] = FAST ? gelu_out2<!__is_same(TO, bf16)>(z) : gelu_erf2(z);
           }
           const long long row = (long long)(t + 4 * f) * C;
-          if constexpr (sizeof(TO) == 2) {
+          if constexpr (OUT3) {   // split-fp16 path: tripled f16 rows of 3C
+            f16x4 h0, l0, h1, l1;
+            x3_split4(f32x4{o[0].x, o[0].y, o[1].x, o[1].y}, h0, l0);
+            x3_split4(f32x4{o[2].x, o[2].y, o[3].x, o[3].y}, h1, l1);
+            f16* o3 = (f16*)(void*)out + ((long long)b * T0 + t0 + t + 4 * f) * 3 * C + c;
+            const f16x8 h = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+            *(f16x8*)o3 = h;
+            *(f16x8*)(o3 + C) = f16x8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+            *(f16x8*)(o3 + 2 * C) = h;
+          } else if constexpr (sizeof(TO) == 2) {
             *(uint4*)(ob + row) = pack_h8<is_f16_v<TO>>(f32x4{o[0].x, o[0].y, o[1].x, o[1].y},
                                                          f32x4{o[2].x, o[2].y, o[3].x, o[3].y});
           } else {
@@ -464,6 +473,16 @@ int launch_conv0_gn_x3(const float* x, int B, int L, const float* norm, const fl
                      beta, eps, ss, t0len, (bf16x8*)nullptr);
   hipLaunchKernelGGL((conv0_apply_kernel<float, false, false, false, true>), dim3((T0 + C0_T - 1) / C0_T, B),
                      dim3(256), 0, s, x, L, norm, w0, b0, C, T0, ss, (float*)out3);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// split-fp16 path, "layer" frontend (WavLM-large): conv0 + LayerNorm(512) + erf-GELU in fp32, written as
+// tripled f16 rows (OUT3); -3: not covered
+int launch_conv0_ln_x3(const float* x, int B, int L, const float* norm, const float* w0, const float* b0, int C,
+                       int k0, int s0, int T0, const float* lnw, const float* lnb, float eps, f16* out3, hipStream_t s) {
+  if (k0 != K0 || s0 != 5 || C != 512) return -3;
+  hipLaunchKernelGGL((conv0_apply_kernel<float, true, false, true, true>), dim3((T0 + C0_T - 1) / C0_T, B), dim3(256),
+                     0, s, x, L, norm, w0, b0, C, T0, (const float2*)nullptr, (float*)out3, lnw, lnb, eps);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -814,9 +833,15 @@ __global__ __launch_bounds__(256) void layernorm_x3_rows_kernel(const float* __r
 // split-fp16 LayerNorm: input fp32 [rows][H] or tripled f16 [rows][3H] (in3), output fp32 (optional)
 // and tripled f16 [rows][3H]
 int launch_layernorm_x3(const void* in, bool in3, const float* w, const float* b, int rows, int H, float eps,
-                        float* out_f, f16* out3, hipStream_t s) {
+                        float* out_f, f16* out3, hipStream_t s, int act) {
   if (H % 4 || H > 2048 || !out3) return -3;
   constexpr int R = 4;
+  if (act != ACT_NONE) {   // LayerNorm + erf-GELU (the "layer" conv frontend)
+    if (in3 || act != ACT_GELU) return -3;
+    hipLaunchKernelGGL((layernorm_kernel<float, f16, false, true>), dim3((rows + 3) / 4), dim3(256), 0, s,
+                       (const float*)in, w, b, rows, H, eps, act, out_f, out3, (float2*)nullptr);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+  }
   if (!in3 && H == 768 && !sse_opt(OPT_LN_X3_V1))
     hipLaunchKernelGGL((layernorm_x3_rows_kernel<R, 3>), dim3((rows + 4 * R - 1) / (4 * R)), dim3(256), 0, s,
                        (const float*)in, w, b, rows, eps, out_f, out3);

@@ -486,7 +486,8 @@ int build_whisper(sse_model* m, Blob& bl, Arena& ar) {
     std::memcpy(qkv.data() + (size_t)2 * D * D, vw, (size_t)D * D * 4);
     for (int i = 0; i < D; ++i) qkvb[i] = qb[i] * scale;
     std::memcpy(qkvb.data() + 2 * D, vb, D * 4);                           // k_proj has no bias
-    L.qkv_w = ar.put_elem(qkv, BF);
+    const bool X3 = m->x3();   // split-fp16 encoder GEMMs (Arena::put_x3), the decoder and convs fp32
+    L.qkv_w = X3 ? ar.put_x3(qkv, 3 * D, 1, D) : ar.put_elem(qkv, BF);
     L.qkv_b = ar.put_f32(qkvb.data(), 3 * D);
     m->ldq = 3 * D;
     if (m->mx()) {
@@ -494,13 +495,16 @@ int build_whisper(sse_model* m, Blob& bl, Arena& ar) {
       L.f1_q = ar.put_mx(std::vector<float>(f1w, f1w + (size_t)F * D), F, D, &L.f1_s);
       L.f2_q = ar.put_mx(std::vector<float>(f2w, f2w + (size_t)D * F), D, F, &L.f2_s);
     }
-    L.o_w = ar.put_elem(std::vector<float>(ow, ow + (size_t)D * D), BF);
+    L.o_w = X3 ? ar.put_x3(std::vector<float>(ow, ow + (size_t)D * D), D, 1, D)
+               : ar.put_elem(std::vector<float>(ow, ow + (size_t)D * D), BF);
     L.o_b = ar.put_f32(ob, D);
     L.ln1_w = ar.put_f32(l1w, D);
     L.ln1_b = ar.put_f32(l1b, D);
-    L.f1_w = ar.put_elem(std::vector<float>(f1w, f1w + (size_t)F * D), BF);
+    L.f1_w = X3 ? ar.put_x3(std::vector<float>(f1w, f1w + (size_t)F * D), F, 1, D)
+                : ar.put_elem(std::vector<float>(f1w, f1w + (size_t)F * D), BF);
     L.f1_b = ar.put_f32(f1b, F);
-    L.f2_w = ar.put_elem(std::vector<float>(f2w, f2w + (size_t)D * F), BF);
+    L.f2_w = X3 ? ar.put_x3(std::vector<float>(f2w, f2w + (size_t)D * F), D, 1, F)
+                : ar.put_elem(std::vector<float>(f2w, f2w + (size_t)D * F), BF);
     L.f2_b = ar.put_f32(f2b, D);
     L.ln2_w = ar.put_f32(l2w, D);
     L.ln2_b = ar.put_f32(l2b, D);
@@ -680,11 +684,12 @@ WhisperWs whisper_plan(const sse_model* m, int B, Plan& p) {
   w.lm = p.add(logmel_workspace_bytes(B, c.n_mels));
   w.mel = p.add((size_t)B * T2 * c.n_mels * es);
   w.h1 = p.add((size_t)B * T2 * D * es);
+  const size_t ex = m->x3() ? 6 : es;   // GEMM operands: tripled f16 rows [hi | lo' | hi] on the fp16x3 path
   w.x = p.add(M * D * es);   // residual stream: bf16 on the bf16 / MX-fp8 paths, fp32 on the fp32 path
-  w.xb = p.add(M * D * es);
+  w.xb = p.add(M * D * ex);
   w.qkv = p.add(M * 3 * D * es);
-  w.ctx = p.add(M * D * es);
-  w.ff = p.add(M * (size_t)c.ffn * es);
+  w.ctx = p.add(M * D * ex);
+  w.ff = p.add(M * (size_t)c.ffn * ex);
   w.xf = p.add(M * D * 4);
   if (c.decoder_layers > 0) {
     w.dx = p.add((size_t)B * D * 4);
@@ -1064,21 +1069,47 @@ int wavlm_forward_x3(sse_model* m, const float* wave, int B, int L, const Sink& 
   const int C0 = c.conv_dim[0];
   const float* b0 = m->conv_b[0] ? m->ptr<float>(m->conv_b[0]) : nullptr;
   f16* bufs[2] = {(f16*)(ws + w.bufA), (f16*)(ws + w.bufB)};
-  RC(prof(m, s, "conv0_gn", 2.0 * B * (double)Ts[0] * C0 * c.conv_kernel[0], 0, [&] {
-    return launch_conv0_gn_x3(wave, B, L, norm, m->ptr<float>(m->conv_w[0]), b0, C0, c.conv_kernel[0],
-                              c.conv_stride[0], Ts[0], m->ptr<float>(m->conv_ln_w[0]), m->ptr<float>(m->conv_ln_b[0]),
-                              1e-5f, (double*)(ws + w.part), (float2*)(ws + w.ss), bufs[0], s, t0len); }));
-  for (int i = 1; i < c.n_conv; ++i) {
-    const int cin = c.conv_dim[i - 1], co = c.conv_dim[i], k = c.conv_kernel[i], st = c.conv_stride[i];
-    GemmArgs g{};
-    g.A = bufs[(i - 1) & 1]; g.B = m->ptr(m->conv_w[i]);
-    g.M = B * Ts[i]; g.N = co; g.K = k * 3 * cin;
-    g.rows_per_seg = Ts[i]; g.seg_stride = (long long)Ts[i - 1] * 3 * cin; g.lda = (long long)st * 3 * cin;
-    g.bias = m->conv_b[i] ? m->ptr<float>(m->conv_b[i]) : nullptr;
-    g.Ct = bufs[i & 1]; g.ct3 = 1; g.ldc = 3 * co; g.act = ACT_GELU;
-    RC(gemm3("gemm:conv", g, k * cin));
+  const f16* feat = nullptr;
+  if (c.feat_norm_layer) {
+    // "layer" frontend (WavLM-large, HF modeling_wavlm.py:696-720): conv -> LayerNorm over channels ->
+    // erf-GELU per layer.  conv0 + LN + GELU in one fp32 pass written tripled (bufA); each later conv is a
+    // split GEMM with fp32 output (into bufB) whose LayerNorm + GELU writes the next tripled operand back
+    // over its own (consumed) input in bufA
+    RC(prof(m, s, "conv0_ln", 2.0 * B * (double)Ts[0] * C0 * c.conv_kernel[0], 0, [&] {
+      return launch_conv0_ln_x3(wave, B, L, norm, m->ptr<float>(m->conv_w[0]), b0, C0, c.conv_kernel[0],
+                                c.conv_stride[0], Ts[0], m->ptr<float>(m->conv_ln_w[0]), m->ptr<float>(m->conv_ln_b[0]),
+                                1e-5f, bufs[0], s); }));
+    float* yf = (float*)bufs[1];
+    for (int i = 1; i < c.n_conv; ++i) {
+      const int cin = c.conv_dim[i - 1], co = c.conv_dim[i], k = c.conv_kernel[i], st = c.conv_stride[i];
+      GemmArgs g{};
+      g.A = bufs[0]; g.B = m->ptr(m->conv_w[i]);
+      g.M = B * Ts[i]; g.N = co; g.K = k * 3 * cin;
+      g.rows_per_seg = Ts[i]; g.seg_stride = (long long)Ts[i - 1] * 3 * cin; g.lda = (long long)st * 3 * cin;
+      g.bias = m->conv_b[i] ? m->ptr<float>(m->conv_b[i]) : nullptr;
+      g.Cf = yf; g.ldc = co; g.act = ACT_NONE;
+      RC(gemm3("gemm:conv", g, k * cin));
+      RC(launch_layernorm_x3(yf, false, m->ptr<float>(m->conv_ln_w[i]), m->ptr<float>(m->conv_ln_b[i]), B * Ts[i], co,
+                             1e-5f, nullptr, bufs[0], s, ACT_GELU));
+    }
+    feat = bufs[0];
+  } else {
+    RC(prof(m, s, "conv0_gn", 2.0 * B * (double)Ts[0] * C0 * c.conv_kernel[0], 0, [&] {
+      return launch_conv0_gn_x3(wave, B, L, norm, m->ptr<float>(m->conv_w[0]), b0, C0, c.conv_kernel[0],
+                                c.conv_stride[0], Ts[0], m->ptr<float>(m->conv_ln_w[0]), m->ptr<float>(m->conv_ln_b[0]),
+                                1e-5f, (double*)(ws + w.part), (float2*)(ws + w.ss), bufs[0], s, t0len); }));
+    for (int i = 1; i < c.n_conv; ++i) {
+      const int cin = c.conv_dim[i - 1], co = c.conv_dim[i], k = c.conv_kernel[i], st = c.conv_stride[i];
+      GemmArgs g{};
+      g.A = bufs[(i - 1) & 1]; g.B = m->ptr(m->conv_w[i]);
+      g.M = B * Ts[i]; g.N = co; g.K = k * 3 * cin;
+      g.rows_per_seg = Ts[i]; g.seg_stride = (long long)Ts[i - 1] * 3 * cin; g.lda = (long long)st * 3 * cin;
+      g.bias = m->conv_b[i] ? m->ptr<float>(m->conv_b[i]) : nullptr;
+      g.Ct = bufs[i & 1]; g.ct3 = 1; g.ldc = 3 * co; g.act = ACT_GELU;
+      RC(gemm3("gemm:conv", g, k * cin));
+    }
+    feat = bufs[(c.n_conv - 1) & 1];
   }
-  const f16* feat = bufs[(c.n_conv - 1) & 1];
   const int C = c.conv_dim[c.n_conv - 1];
   float* x = (float*)(ws + w.x);
   float* xt = (float*)(ws + w.xt);
@@ -1111,13 +1142,17 @@ int wavlm_forward_x3(sse_model* m, const float* wave, int B, int L, const Sink& 
     RC(prof(m, s, "gemm_conv:posconv", gflops(g, G), gbytes<float>(g, AMODE_CONV, G),
             [&] { return launch_gemm<float>(g, AMODE_CONV, G, s); }));
   }
-  RC(launch_layernorm_x3(x, false, m->ptr<float>(m->enc_ln_w), m->ptr<float>(m->enc_ln_b), M, H, eps, x, xb, s));
+  // post-LN (WavLM-base): the encoder LayerNorm before the layers; stable-LN (WavLM-large, HF
+  // modeling_wavlm.py:465-522): pre-LN layers and the encoder LayerNorm after the last one
+  const bool pre = c.stable_layer_norm;
+  if (!pre) RC(launch_layernorm_x3(x, false, m->ptr<float>(m->enc_ln_w), m->ptr<float>(m->enc_ln_b), M, H, eps, x, xb, s));
   RC(sink.emit(0, x));
   float* qkv = (float*)(ws + w.qkv);
   f16* ctx3 = (f16*)(ws + w.ctx3);
   f16* ff = (f16*)(ws + w.ff);
   for (int l = 0; l < c.layers; ++l) {
     const LayerW& Lw = m->layers[l];
+    if (pre) RC(launch_layernorm_x3(x, false, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, nullptr, xb, s));
     GemmArgs g{};
     g.A = xb; g.B = m->ptr(Lw.qkv_w); g.M = M; g.N = m->ldq; g.K = 3 * H;
     g.rows_per_seg = M; g.lda = 3 * H; g.bias = m->ptr<float>(Lw.qkv_b); g.Cf = qkv; g.ldc = m->ldq;
@@ -1136,7 +1171,10 @@ int wavlm_forward_x3(sse_model* m, const float* wave, int B, int L, const Sink& 
     g.A = ctx3; g.B = m->ptr(Lw.o_w); g.M = M; g.N = H; g.K = 3 * H; g.rows_per_seg = M; g.lda = 3 * H;
     g.bias = m->ptr<float>(Lw.o_b); g.resid = x; g.Cf = x; g.ldc = H;
     RC(gemm3("gemm:oproj", g, H));
-    RC(launch_layernorm_x3(x, false, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, x, xb, s));
+    if (pre)
+      RC(launch_layernorm_x3(x, false, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, H, eps, nullptr, xb, s));
+    else
+      RC(launch_layernorm_x3(x, false, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, x, xb, s));
     g = GemmArgs{};
     g.A = xb; g.B = m->ptr(Lw.f1_w); g.M = M; g.N = F; g.K = 3 * H; g.rows_per_seg = M; g.lda = 3 * H;
     g.bias = m->ptr<float>(Lw.f1_b); g.Ct = ff; g.ct3 = 1; g.ldc = 3 * F; g.act = ACT_GELU;
@@ -1145,8 +1183,16 @@ int wavlm_forward_x3(sse_model* m, const float* wave, int B, int L, const Sink& 
     g.A = ff; g.B = m->ptr(Lw.f2_w); g.M = M; g.N = H; g.K = 3 * F; g.rows_per_seg = M; g.lda = 3 * F;
     g.bias = m->ptr<float>(Lw.f2_b); g.resid = x; g.Cf = x; g.ldc = H;
     RC(gemm3("gemm:ffn2", g, F));
+    if (pre) {   // hidden_states[l + 1] = the residual stream (the last one: after the encoder LayerNorm)
+      if (l + 1 < c.layers) RC(sink.emit(l + 1, x));
+      continue;
+    }
     RC(launch_layernorm_x3(x, false, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, H, eps, x, xb, s));
     RC(sink.emit(l + 1, x));
+  }
+  if (pre) {
+    RC(launch_layernorm_x3(x, false, m->ptr<float>(m->enc_ln_w), m->ptr<float>(m->enc_ln_b), M, H, eps, x, xb, s));
+    RC(sink.emit(c.layers, x));
   }
   return 0;
 }
@@ -1331,6 +1377,91 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
   return 0;
 }
 
+// SSE_DTYPE_FP16X3 Whisper encoder: the fp32 path with the encoder layers' GEMMs in
+// split-fp16 form (as wavlm_forward_x3): pre-LN LayerNorms write the tripled operands, the attention core
+// (fp32 softmax, f16 matrix-core products of split operands) writes the out-projection's tripled operand,
+// fc1's epilogue the fc2 operand with erf-GELU; log-mel, conv1 / conv2 (exact-f32 MFMA, 0.7 % of the FLOPs),
+// the residual stream and the 1-token decoder stay fp32.
+int whisper_forward_x3(sse_model* m, const float* wave, int B, int L, const Sink& sink, char* ws, hipStream_t s,
+                       const float* mel_hf, const Sink* dsink, const int* lens) {
+  const sse_cfg& c = m->cfg;
+  Plan p;
+  const WhisperWs w = whisper_plan(m, B, p);
+  const int D = c.hidden, F = c.ffn, nh = c.heads, Tq = c.max_positions, T2 = 2 * Tq, nm = c.n_mels;
+  const int M = B * Tq;
+  const float eps = c.ln_eps;
+  void* zero = ws + w.zero;
+  if (hipMemsetAsync(zero, 0, 256, s) != hipSuccess) return SSE_ERR_HIP;
+  float* mel = (float*)(ws + w.mel);
+  if (mel_hf)
+    RC(launch_mel_to_cl<float>(mel_hf, B, nm, mel, s));
+  else
+    RC(prof(m, s, "logmel", B * 3000.0 * 5.0 * 200 * 7.64, (double)B * (480000.0 * 4 + 3000.0 * nm * 12.0),
+            [&] { return launch_logmel<float>(wave, B, L, nm, nullptr, mel, ws + w.lm, logmel_workspace_bytes(B, nm), s,
+                                              lens); }));
+  float* h1 = (float*)(ws + w.h1);
+  float* x = (float*)(ws + w.x);
+  f16* xb = (f16*)(ws + w.xb);
+  {
+    GemmArgs g{};   // conv1: k3 pad1, 80 -> D, GELU
+    g.A = mel; g.B = m->ptr(m->c1_w); g.M = B * T2; g.N = D; g.K = 3 * nm;
+    g.rows_per_seg = T2; g.T_in = T2; g.stride = 1; g.pad = 1; g.cin = nm; g.ld_in = nm;
+    g.bias = m->ptr<float>(m->c1_b); g.Cf = h1; g.ldc = D; g.act = ACT_GELU; g.zero = zero;
+    RC(prof(m, s, "gemm_conv:conv1", gflops(g), gbytes<float>(g, AMODE_CONV),
+            [&] { return launch_gemm<float>(g, AMODE_CONV, 1, s); }));
+    g = GemmArgs{};   // conv2: k3 s2 pad1, GELU, + embed_positions
+    g.A = h1; g.B = m->ptr(m->c2_w); g.M = M; g.N = D; g.K = 3 * D;
+    g.rows_per_seg = Tq; g.T_in = T2; g.stride = 2; g.pad = 1; g.cin = D; g.ld_in = D;
+    g.bias = m->ptr<float>(m->c2_b); g.resid = m->ptr<float>(m->positions); g.resid_rows = Tq;
+    g.Cf = x; g.ldc = D; g.act = ACT_GELU; g.zero = zero;
+    RC(prof(m, s, "gemm_conv:conv2", gflops(g), gbytes<float>(g, AMODE_CONV),
+            [&] { return launch_gemm<float>(g, AMODE_CONV, 1, s); }));
+  }
+  RC(sink.emit(0, x));
+  float* qkv = (float*)(ws + w.qkv);
+  f16* ctx3 = (f16*)(ws + w.ctx);
+  f16* ff = (f16*)(ws + w.ff);
+  auto gemm3 = [&](const char* tag, GemmArgs& g, int Klog) {   // logical K (the FLOP count), operands 3K
+    g.zero = zero;
+    g.f16 = 1;
+    g.alpha = m->alpha((size_t)((const char*)g.B - m->dmem));
+    return prof(m, s, tag, 2.0 * g.M * (double)g.N * Klog, gbytes<bf16>(g), [&] { return launch_gemm8_bf16(g, s); });
+  };
+  for (int l = 0; l < c.layers; ++l) {
+    const LayerW& Lw = m->layers[l];
+    RC(launch_layernorm_x3(x, false, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, D, eps, nullptr, xb, s));
+    GemmArgs g{};
+    g.A = xb; g.B = m->ptr(Lw.qkv_w); g.M = M; g.N = 3 * D; g.K = 3 * D; g.rows_per_seg = M; g.lda = 3 * D;
+    g.bias = m->ptr<float>(Lw.qkv_b); g.Cf = qkv; g.ldc = 3 * D;
+    RC(gemm3("gemm:qkv", g, D));
+    AttnArgs a{};
+    a.qkv = qkv; a.out = ctx3; a.out3 = 1; a.T = Tq; a.H = D; a.nh = nh; a.ldq = m->ldq; a.scale = 1.0f;
+    RC(prof(m, s, "attn", 4.0 * B * (double)Tq * Tq * D, (double)B * Tq * (3.0 * D * 4.0 + 6.0 * D),
+            [&] { return launch_attention<float>(a, B, s); }));
+    g = GemmArgs{};
+    g.A = ctx3; g.B = m->ptr(Lw.o_w); g.M = M; g.N = D; g.K = 3 * D; g.rows_per_seg = M; g.lda = 3 * D;
+    g.bias = m->ptr<float>(Lw.o_b); g.resid = x; g.Cf = x; g.ldc = D;
+    RC(gemm3("gemm:oproj", g, D));
+    RC(launch_layernorm_x3(x, false, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, D, eps, nullptr, xb, s));
+    g = GemmArgs{};
+    g.A = xb; g.B = m->ptr(Lw.f1_w); g.M = M; g.N = F; g.K = 3 * D; g.rows_per_seg = M; g.lda = 3 * D;
+    g.bias = m->ptr<float>(Lw.f1_b); g.Ct = ff; g.ct3 = 1; g.ldc = 3 * F; g.act = ACT_GELU;
+    RC(gemm3("gemm:ffn1", g, D));
+    g = GemmArgs{};
+    g.A = ff; g.B = m->ptr(Lw.f2_w); g.M = M; g.N = D; g.K = 3 * F; g.rows_per_seg = M; g.lda = 3 * F;
+    g.bias = m->ptr<float>(Lw.f2_b); g.resid = x; g.Cf = x; g.ldc = D;
+    RC(gemm3("gemm:ffn2", g, F));
+    if (l + 1 < c.layers) RC(sink.emit(l + 1, x));
+  }
+  // hidden_states[-1] is the post-LN last_hidden_state (HF/utils/output_capturing.py:268-279)
+  float* xf = (float*)(ws + w.xf);
+  RC((launch_layernorm<float, float>(x, m->ptr<float>(m->enc_ln_w), m->ptr<float>(m->enc_ln_b), M, D, eps, ACT_NONE,
+                                     xf, (float*)nullptr, s)));
+  RC(sink.emit(c.layers, xf));
+  if (dsink) RC(whisper_decoder<float>(m, xf, B, *dsink, ws, w, s));
+  return 0;
+}
+
 // WavLM embedding batches of at least SPLIT_MIN clips run as two half-batches on two streams (the
 // caller's and the model's aux stream): clips are independent, so each half is an ordinary forward
 // over its own rows, workspace and output slots, and the two halves' kernels share the CUs -- the last
@@ -1452,6 +1583,8 @@ int forward_one(sse_model* m, const float* d_in, int B, int L, const Sink& sink,
     rc = m->bf()    ? wavlm_forward<bf16>(m, d_in, B, L, sink, (char*)d_ws, s, lens)
          : m->h16() ? wavlm_forward<f16>(m, d_in, B, L, sink, (char*)d_ws, s, lens)
                     : wavlm_forward<float>(m, d_in, B, L, sink, (char*)d_ws, s, lens);
+  else if (m->x3())
+    rc = whisper_forward_x3(m, d_in, B, L, sink, (char*)d_ws, s, from_mel ? d_in : nullptr, dsink, lens);
   else
     rc = m->bf() ? whisper_forward<bf16>(m, d_in, B, L, sink, (char*)d_ws, s, from_mel ? d_in : nullptr, dsink, lens)
                  : whisper_forward<float>(m, d_in, B, L, sink, (char*)d_ws, s, from_mel ? d_in : nullptr, dsink, lens);
@@ -1537,10 +1670,10 @@ int sse_model_create(const sse_cfg* cfg, const float* host_weights, size_t nbyte
       (cfg->kind != SSE_KIND_WAVLM || cfg->hidden % 256 || cfg->ffn % 256 ||
        (cfg->hidden / cfg->pos_groups != 48 && cfg->hidden / cfg->pos_groups != 64)))
     return SSE_ERR_UNSUPPORTED;
-  // split-fp16: WavLM "group" frontend + post-LN encoder (WavLM-base); every GEMM N % 256 == 0
-  if (dtype == SSE_DTYPE_FP16X3 &&
-      (cfg->kind != SSE_KIND_WAVLM || cfg->feat_norm_layer || cfg->stable_layer_norm || cfg->hidden % 256 ||
-       cfg->ffn % 256 || cfg->conv_dim[0] != 512 || cfg->conv_bias))
+  // split-fp16: WavLM-base ("group" frontend, post-LN), WavLM-large ("layer" frontend, stable-LN) and the
+  // Whisper encoder; every split GEMM N % 256 == 0
+  if (dtype == SSE_DTYPE_FP16X3 && (cfg->hidden % 256 || cfg->ffn % 256 ||
+                                    (cfg->kind == SSE_KIND_WAVLM ? cfg->conv_dim[0] != 512 : cfg->kind != SSE_KIND_WHISPER)))
     return SSE_ERR_UNSUPPORTED;
   // MX-fp8 GEMMs: N % 256 and K % 128 for QKV (3D x D), fc1 (F x D), fc2 (D x F)
   if (dtype == SSE_DTYPE_FP8 && (cfg->kind != SSE_KIND_WHISPER || cfg->hidden % 256 || cfg->ffn % 256))

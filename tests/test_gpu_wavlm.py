@@ -122,9 +122,11 @@ def test_edge_lengths(m32, wavlm_sd):
         m32.embed(torch.zeros((1, 399), device="cuda:0"), [12])    # shorter than the receptive field (T = 0)
 
 
-@pytest.mark.parametrize("dtype,tol", [("fp32", FP32_TOL), ("bf16", BF16_TOL), ("fp16", 5e-3)])
+@pytest.mark.parametrize("dtype,tol", [("fp32", FP32_TOL), ("bf16", BF16_TOL), ("fp16", 5e-3), ("fp16x3", FP32_TOL)])
 def test_wavlm_large_matches_reference(dtype, tol):
-    """WavLM-large shape (layer-norm conv frontend, stable-LN encoder, do_normalize=True)."""
+    """WavLM-large shape (layer-norm conv frontend, stable-LN encoder, do_normalize=True), the
+    reference's default --model_name (REF/WavLM_embeddings.py:34).  fp16x3 (split-fp16 GEMMs) holds the
+    fp32 bar, 1e-4."""
     import os
     from conftest import GOLDEN
     from ssr_amd import config as C, synth

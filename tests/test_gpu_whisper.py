@@ -165,7 +165,7 @@ def test_whisper_large_v2_embed():
     clip = _clips(None, [3.0])[0]
     sd = synth.synth_whisper_state_dict(C.WHISPER_LARGE_V2, seed=11)
     idx = [int(i) for i in g["layer_indices"]]
-    for dtype, tol in (("fp32", 1e-4), ("bf16", 3e-2)):
+    for dtype, tol in (("fp32", 1e-4), ("bf16", 3e-2), ("fp16x3", 1e-4)):
         m = SSEModel(C.WHISPER_LARGE_V2, sd, device="cuda:0", dtype=dtype)
         got = m.embed(torch.from_numpy(clip).cuda(), idx).cpu().numpy()[0]
         rel = _rel(got, g["emb"][0])
@@ -224,12 +224,14 @@ def test_whisper_large_v2_bench_batch(dtype, B, tol, cos_min):
         assert rel <= tol and cos >= cos_min
 
 
-@pytest.mark.parametrize("dtype,tol,cos_min", [("fp32", 1e-4, 0.9999999), ("bf16", 3e-2, 0.999), ("fp8", 0.08, 0.995)])
+@pytest.mark.parametrize("dtype,tol,cos_min", [("fp32", 1e-4, 0.9999999), ("bf16", 3e-2, 0.999), ("fp8", 0.08, 0.995),
+                                                ("fp16x3", 1e-4, 0.9999999)])
 def test_whisper_small_matches_reference(dtype, tol, cos_min):
     """openai/whisper-small (768 / 12 layers / 12 heads / 3072), the reference's
     default Whisper (REF/whisper_embeddings_large.py:34), pinned by the reference's own
     extract_whisper_embeddings_fixed on a 3 s and a 12 s clip (encoder_layer_{12,11,10} and the
-    1-token decoder's decoder_layer_{12,11,10,0}).  fp8 = MX-fp8 encoder GEMMs (the decoder runs bf16)."""
+    1-token decoder's decoder_layer_{12,11,10,0}).  fp8 = MX-fp8 encoder GEMMs (the decoder runs bf16);
+    fp16x3 = split-fp16 encoder GEMMs (the decoder runs fp32) at the fp32 bar."""
     p = os.path.join(GOLDEN, "whisper_small.npz")
     if not os.path.exists(p):
         pytest.skip("whisper-small fixture not generated")

@@ -181,3 +181,19 @@ def test_whisper_aten_restatement_matches_reference(golden_manifest):
         d = o.extract(c, ei, di)
         assert _rel(np.stack([d[f"encoder_layer_{k}"] for k in ei]), g["emb"][i]).max() <= 1e-5
         assert _rel(np.stack([d[f"decoder_layer_{k}"] for k in di]), g["dec_emb"][i]).max() <= 1e-5
+
+
+def test_whisper_small_oracle_vs_reference(golden_manifest):
+    """openai/whisper-small shape (the reference's default Whisper, REF/whisper_embeddings_large.py:34):
+    encoder and 1-token decoder embeddings of the reference's own glue, one clip (the second clip is
+    covered by the GPU test), plus the fixture's input hashes."""
+    from oracle.whisper import WhisperOracle
+    from ssr_amd import config as C, synth
+    g = np.load(os.path.join(GOLDEN, "whisper_small.npz"))
+    man = golden_manifest["whisper_small"]
+    clips = [synth.synth_clips(1, int(16000 * d), seed=4321, first_clip=i)[0] for i, d in enumerate(man["durations_s"])]
+    assert [_sha(c) for c in clips] == man["clips_sha256"]
+    o = WhisperOracle(C.WHISPER_SMALL_DEC, synth.synth_whisper_state_dict(C.WHISPER_SMALL_DEC, seed=11))
+    enc, dec = o.embed_both(clips[0][None], [int(i) for i in g["layer_indices"]], [int(i) for i in g["decoder_indices"]])
+    assert _rel(enc[0], g["emb"][0]).max() <= ORACLE_TOL
+    assert _rel(dec[0], g["dec_emb"][0]).max() <= ORACLE_TOL
