@@ -149,6 +149,26 @@ SSE_DEV void gelu_out2_n(f32x2 (&x)[N]) {
   for (int n = 0; n < N; ++n) x[n] = x[n] * __builtin_elementwise_fma(xc[n], p[n], f32x2{0.5f, 0.5f});
 }
 
+// gelu_fp8out2 (below) over N independent pairs stage by stage (bit-identical to N calls)
+template <int N>
+SSE_DEV void gelu_fp8out2_n(f32x2 (&x)[N]) {
+  constexpr float cf[6] = {-3.503167250e-07f, 2.229058919e-05f, -5.630472442e-04f, 7.574830670e-03f,
+                           -6.208017841e-02f, 3.963519037e-01f};
+  f32x2 xc[N], s[N], p[N];
+  #pragma unroll
+  for (int n = 0; n < N; ++n) {
+    xc[n] = f32x2{__builtin_amdgcn_fmed3f(x[n].x, -3.5f, 3.5f), __builtin_amdgcn_fmed3f(x[n].y, -3.5f, 3.5f)};
+    s[n] = xc[n] * xc[n];
+    p[n] = f32x2{cf[0], cf[0]};
+  }
+  #pragma unroll
+  for (int k = 1; k < 6; ++k)
+    #pragma unroll
+    for (int n = 0; n < N; ++n) p[n] = __builtin_elementwise_fma(p[n], s[n], f32x2{cf[k], cf[k]});
+  #pragma unroll
+  for (int n = 0; n < N; ++n) x[n] = x[n] * __builtin_elementwise_fma(xc[n], p[n], f32x2{0.5f, 0.5f});
+}
+
 // the output's polynomial GELU: bf16 only -> gelu_bf2; fp16, fp32 or an fp32 copy (Cf) -> gelu_fast2
 template <bool H16> SSE_DEV f32x2 gelu_out2(f32x2 x) { return H16 ? gelu_fast2(x) : gelu_bf2(x); }
 SSE_DEV f32x2 gelu_out2(f32x2 x, bool bf_only) { return bf_only ? gelu_bf2(x) : gelu_fast2(x); }

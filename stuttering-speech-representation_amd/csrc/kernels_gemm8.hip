@@ -50,6 +50,7 @@ constexpr int G8_SMEM_MX = G8_OPS_MX > G8_EPI ? G8_OPS_MX : G8_EPI;
 
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // phase k = 4t + p (k >= -8) -> the (tile, half) whose LDS-DMA it issues
 SSE_DEV void g8_target(int k, int& tile, int& half) {
@@ -548,15 +549,6 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
 // retire in issue order) and the stores drain under the first K-tile's MFMAs.  From K-tile 1
 // on, waits target loads issued after the stores and the plain counts apply.
 // ======================================================================================
-// Deferred-store schedule of the persistent kernel (DEF): stores of the previous tile's 16 packed rows
-// issued at phase kk of the current tile, kk = 0..7 (K-tiles 0 and 1): 2 4 4 2 1 1 1 1.  Front-loaded
-// while the new tile's accumulators are still unwritten (quadrant p is first written in phase p), one per
-// phase once all 128 accumulators are live.
-constexpr int g8d_n(int kk) { return kk < 0 || kk > 7 ? 0 : (kk == 0 ? 2 : (kk <= 2 ? 4 : (kk == 3 ? 2 : 1))); }
-constexpr int g8d_first(int kk) { return kk <= 0 ? 0 : g8d_first(kk - 1) + g8d_n(kk - 1); }
-constexpr int g8d_recent(int kk) { return g8d_n(kk - 1) + g8d_n(kk - 2) + g8d_n(kk - 3); }
-static_assert(g8d_first(8) == 16, "every deferred store is scheduled");
-
 // tile of block b in round r (-1: idle), XCD-aware bijective remap within the round
 SSE_DEV int g8p_tile(int b, int r, int G, int n_tiles) {
   const int base = r * G;
@@ -609,6 +601,24 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
     }
   };
   auto finish_half = [&](int mi) {   // acc[mi] <- bias, activation, (LayerNorm'd) residual
+    if constexpr (Q8 && !RES) {   // MX-fp8 out (fc1): the row block's 8 pairs through one lockstep GELU
+      if (gelu_fast) {
+        #pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          f32x2 o2[8];
+          #pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const f32x4 o = acc[mi][u >> 1][i][u & 1] + bv[u >> 1][u & 1];
+            o2[2 * u] = f32x2{o[0], o[1]};
+            o2[2 * u + 1] = f32x2{o[2], o[3]};
+          }
+          gelu_fp8out2_n<8>(o2);
+          #pragma unroll
+          for (int u = 0; u < 4; ++u) acc[mi][u >> 1][i][u & 1] = f32x4{o2[2 * u].x, o2[2 * u].y, o2[2 * u + 1].x, o2[2 * u + 1].y};
+        }
+        return;
+      }
+    }
     #pragma unroll
     for (int i = 0; i < 4; ++i)
       #pragma unroll
@@ -731,15 +741,10 @@ constexpr int G8P_SMEM = G8_OPS + 2 * G8P_EP;
 //   o = act(acc + bias[n])                                        (otherwise: rstd = 1 and the acol term
 //                                                                  is not formed, bit-identical to a plain add)
 // DBG (timing probes only, tools/gemm8_probe.hip; the library launches DBG = 0): 1 = math without the
-// stores (results kept live by an empty asm), 3 = stores of the raw accumulators without the math,
-// 4 = stores in a full-line address pattern (wrong addresses: timing only), 5 = non-temporal stores,
-// 6 = every tile's stores into the same 128 KiB, 7 = half of the stores, 8 = math without the stores plus
-// one garbage 16-B store per lane in every steady main-loop phase (3x the tile's store count, spread),
-// 9 = deferred stores (DEF in gemm8p_kernel).
-// DBG = 9: deferred stores -- the packed 16-bit rows go to pk[mi][ni][i] (the next tile's main loop stores them).
+// stores (results kept live by an empty asm), 3 = stores of the raw accumulators without the math.
 template <int ACT, bool CT3, bool F16, bool has_bias, bool fold, int DBG = 0>
 SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, int n0, int wm, int wn, int q,
-                          int r16, const char* ep, uint4 (&pk)[2][2][4]) {
+                          int r16, const char* ep) {
   const float alpha = F16 ? g.alpha : 1.f;   // split-fp16: the weights' 2^s undone (exact)
   f32x4 bv[2][2], ac[2][2];
   #pragma unroll
@@ -799,7 +804,13 @@ SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, i
     }
   };
   // fp32 out: one 16-B store per (i, ni, j).  bf16 out: the two j blocks of a lane pair are exchanged
-  // with v_permlane16_swap so every lane holds 8 consecutive columns: one 16-B store per (i, ni).
+  // with v_permlane16_swap so every lane holds 8 consecutive columns: one 16-B store per (i, ni), through
+  // a buffer resource based at the tile's first row (no 64-bit address math, no exec-mask branch per
+  // store: rows >= M fall outside its num_records)
+  const __amdgpu_buffer_rsrc_t ct_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((bf16*)g.Ct + (long long)m0 * g.ldc), (short)0,
+      (int)min((long long)(g.M - m0) * g.ldc * 2, (long long)0x7FFFFFF0), 0x00020000);
+  const unsigned lane_off = (unsigned)(((wm * 64 + r16) * g.ldc + wn * 32 + (q & 1) * 16 + (q >> 1) * 8) * 2);
   auto store_half = [&](int mi) {
     #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -834,46 +845,22 @@ SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, i
           const auto s0 = __builtin_amdgcn_permlane16_swap(X.x, Y.x, false, false);
           const auto s1 = __builtin_amdgcn_permlane16_swap(X.y, Y.y, false, false);
           const long long c = n0 + ni * 128 + wn * 32 + (q & 1) * 16 + (q >> 1) * 8;
-          if constexpr (DBG == 9) {
-            static_assert(!CT3, "deferred stores: one plane");
-            pk[mi][ni][i] = make_uint4(s0[0], s1[0], s0[1], s1[1]);
-            continue;
-          }
-          if constexpr (DBG == 1 || DBG == 8) {
+          if constexpr (DBG == 1) {
             asm volatile("" ::"v"(s0[0]), "v"(s0[1]), "v"(s1[0]), "v"(s1[1]));
             continue;
           }
-          if constexpr (DBG == 4) {   // same data and count, full-line pattern: 8 rows x 128 B per store
-            const int r = m0 + mi * 128 + wm * 64 + i * 16 + ni * 8 + (threadIdx.x & 63) / 8;
-            if (r < g.M)
-              *(uint4*)((bf16*)g.Ct + (long long)r * g.ldc + n0 + wn * 64 + (threadIdx.x & 7) * 8) =
-                  make_uint4(s0[0], s1[0], s0[1], s1[1]);
-            continue;
-          }
-          if constexpr (DBG == 6) {   // every tile into the same 128 KiB (L2-resident)
-            const long long c6 = ni * 128 + wn * 32 + (q & 1) * 16 + (q >> 1) * 8;
-            const long long r6 = (long long)(mi * 128 + wm * 64 + i * 16 + r16) * 256;
-            *(uint4*)((bf16*)g.Ct + r6 + c6) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
-            continue;
-          }
-          if constexpr (DBG == 7) {   // half the stores (ni = 0 only)
-            if (ni == 0 && ok) *(uint4*)((bf16*)g.Ct + row + c) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
-            else asm volatile("" ::"v"(s0[0]), "v"(s0[1]), "v"(s1[0]), "v"(s1[1]));
-            continue;
-          }
-          if constexpr (DBG == 5) {   // non-temporal stores
-            if (ok) __builtin_nontemporal_store(i32x4{(int)s0[0], (int)s1[0], (int)s0[1], (int)s1[1]}, (i32x4*)((bf16*)g.Ct + row + c));
-            continue;
-          }
-          if (ok) {
-            const uint4 v = make_uint4(s0[0], s1[0], s0[1], s1[1]);
-            *(uint4*)((bf16*)g.Ct + row + c) = v;
-            if constexpr (CT3) *(uint4*)((bf16*)g.Ct + row + 2 * g.N + c) = v;
-          }
-          if constexpr (CT3) {   // lo' plane
+          // the tile's buffer resource: lane offset (one VGPR per half) + row-block offset in an SGPR + the
+          // column block as an immediate; rows >= M are dropped by the range check
+          const unsigned soff = (unsigned)(i * 16 * g.ldc * 2);
+          const unsigned voff = lane_off + (unsigned)(mi * 128 * g.ldc * 2) + (unsigned)(ni * 256);
+          const u32x4 v = {s0[0], s1[0], s0[1], s1[1]};
+          __builtin_amdgcn_raw_buffer_store_b128(v, ct_rsrc, voff, soff, 0);
+          if constexpr (CT3) {   // [hi | lo' | hi]: the second hi plane and the lo' plane
+            __builtin_amdgcn_raw_buffer_store_b128(v, ct_rsrc, voff + (unsigned)(4 * g.N), soff, 0);
             const auto t0 = __builtin_amdgcn_permlane16_swap(LX.x, LY.x, false, false);
             const auto t1 = __builtin_amdgcn_permlane16_swap(LX.y, LY.y, false, false);
-            if (ok) *(uint4*)((bf16*)g.Ct + row + g.N + c) = make_uint4(t0[0], t1[0], t0[1], t1[1]);
+            const u32x4 lv = {t0[0], t1[0], t0[1], t1[1]};
+            __builtin_amdgcn_raw_buffer_store_b128(lv, ct_rsrc, voff + (unsigned)(2 * g.N), soff, 0);
           }
         }
       }
@@ -883,16 +870,6 @@ SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, i
   store_half(0);
   finish_half(1);
   store_half(1);
-}
-
-// deferred store n (0..15) of a tile's packed rows: (mi, ni, i) = (n >> 3, (n >> 2) & 1, n & 3)
-template <int N>
-SSE_DEV void g8p_store_pk(const GemmArgs& g, const uint4 (&pk)[2][2][4], int m0, int n0, int wm, int wn, int q,
-                          int r16) {
-  constexpr int mi = N >> 3, ni = (N >> 2) & 1, i = N & 3;
-  const int m = m0 + mi * 128 + wm * 64 + i * 16 + r16;
-  if (m < g.M)
-    *(uint4*)((bf16*)g.Ct + (long long)m * g.ldc + n0 + ni * 128 + wn * 32 + (q & 1) * 16 + (q >> 1) * 8) = pk[mi][ni][i];
 }
 
 // ======================================================================================
@@ -1028,47 +1005,22 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   };
-  // Z: the tile's first K-tile -- the ks = 0 MFMAs take srcC = 0 (no accumulator reset)
-  auto mma_z = [&](f32x4 (&c)[4][2], const bf16x8 (&bf)[2][2], auto zc) {
-    constexpr bool Z = decltype(zc)::value;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-    #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-      #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          c[i][j] = g8_mfma<F16>(bf[j][ks], af[i][ks], (Z && ks == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : c[i][j]);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-  };
 
   int slot = 0;
   ep_issue(tile, 0);
   setup(tile);
   for (int k = -6; k < 0; ++k) issue(k);
   int S = 0;   // store instructions issued after the current tile's prologue
-  // DEF (deferred stores): a tile's packed rows (pk) are stored during the NEXT tile's first two K-tiles,
-  // after each phase's wait, so the waits of that tile's loads never include them (vector-memory ops
-  // retire in issue order: a store issued before a load delays every wait for that load).
-  constexpr bool DEF = DBG == 9;
-  uint4 pk[2][2][4];
-  bool pend = false;   // pk holds the previous tile's rows
-  int pm0 = 0, pn0 = 0;
   while (true) {
     const int m0 = (tile / n_tiles_n) * 256, n0 = (tile % n_tiles_n) * 256;
-    if constexpr (!DEF) {   // DEF: the first K-tile's MFMAs take srcC = 0 instead
+    #pragma unroll
+    for (int a = 0; a < 2; ++a)
       #pragma unroll
-      for (int a = 0; a < 2; ++a)
+      for (int c = 0; c < 2; ++c)
         #pragma unroll
-        for (int c = 0; c < 2; ++c)
+        for (int i = 0; i < 4; ++i)
           #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[a][c][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+          for (int j = 0; j < 2; ++j) acc[a][c][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     // the epilogue-parameter DMA precedes the prologue: retired by the same counted waits
     g8_vmcnt_dyn<false>(g8_count<false>(-1, nk) + S);
     g8_barrier();
@@ -1085,14 +1037,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
         if constexpr (FI) {
           g8_vmcnt_dyn<false>(g8_count<false>(kk, nk) + S);
         } else if constexpr (ST) {
-          if constexpr (DBG == 8) {   // probe: one 16-B store per lane per steady phase, after the wait
-            g8_vmcnt_dyn<true>(8 + min(3, kk - 4));
-            const int r8 = m0 + wave * 32 + (lane >> 1);
-            if (r8 < M)
-              *(bf16x8*)((bf16*)g.Ct + (long long)r8 * g.ldc + n0 + (lane & 1) * 8 + (kk & 15) * 16) = af[0][0];
-          } else {
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-          }
+          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         } else {
           g8_wait<false>(kk, nk);
         }
@@ -1118,54 +1063,8 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
       mma(acc[1][0], b0f);
       g8_barrier();
     };
-    // DEF: K-tiles 0..2 with compile-time phase numbers (the deferred stores index pk at compile time)
-    auto run_tile_def = [&](auto tc) {
-      constexpr int T = decltype(tc)::value;
-      const char* buf = smem + (T & 1) * G8_BUF;
-      auto issue_wait = [&](auto kc) {
-        constexpr int KK = decltype(kc)::value;
-        issue(KK);
-        int n = T == 0 ? g8_count<false>(KK, nk) + S : g8_count<false>(KK, nk);
-        if (pend) n += g8d_recent(KK);   // this wave's stores issued after the loads it waits for
-        g8_vmcnt_dyn<true>(n);
-        if (pend) {
-          g8_sfor<g8d_first(KK), g8d_first(KK) + g8d_n(KK)>([&](auto nc) {
-            g8p_store_pk<decltype(nc)::value>(g, pk, pm0, pn0, wm, wn, q, r16);
-          });
-        }
-      };
-      const std::integral_constant<bool, T == 0> z;
-      read_a(buf);
-      read_b(buf + 2 * G8_HALF, b0f);
-      issue_wait(std::integral_constant<int, 4 * T>{});
-      g8_barrier();
-      mma_z(acc[0][0], b0f, z);
-      g8_barrier();
-      read_b(buf + 3 * G8_HALF, b1f);
-      issue_wait(std::integral_constant<int, 4 * T + 1>{});
-      g8_barrier();
-      mma_z(acc[0][1], b1f, z);
-      g8_barrier();
-      read_a(buf + G8_HALF);
-      issue_wait(std::integral_constant<int, 4 * T + 2>{});
-      g8_barrier();
-      mma_z(acc[1][1], b1f, z);
-      g8_barrier();
-      issue_wait(std::integral_constant<int, 4 * T + 3>{});
-      g8_barrier();
-      mma_z(acc[1][0], b0f, z);
-      g8_barrier();
-    };
-    int t;
-    if constexpr (DEF) {   // nk >= 3 (launch_gemm8_bf16)
-      run_tile_def(std::integral_constant<int, 0>{});
-      run_tile_def(std::integral_constant<int, 1>{});
-      run_tile_def(std::integral_constant<int, 2>{});
-      t = 3;
-    } else {
-      run_tile(0, std::integral_constant<bool, false>{}, std::integral_constant<bool, true>{});
-      t = 1;
-    }
+    run_tile(0, std::integral_constant<bool, false>{}, std::integral_constant<bool, true>{});
+    int t = 1;
     for (; t + 2 < nk; ++t) run_tile(t, std::integral_constant<bool, true>{}, std::integral_constant<bool, false>{});
     for (; t < nk; ++t) run_tile(t, std::integral_constant<bool, false>{}, std::integral_constant<bool, false>{});
     if (wm == 0) g8_barrier();   // balance group 1's extra barrier: every wave's LDS reads are done
@@ -1185,21 +1084,11 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
           #pragma unroll
           for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(acc[a][c][i][0]), "v"(acc[a][c][i][1]));
     } else {
-      g8p_epilogue<ACT, CT3, F16, has_bias, fold, DBG>(g, acc, m0, n0, wm, wn, q, r16, smem + G8_OPS + slot * G8P_EP,
-                                                      pk);
-    }
-    if constexpr (DEF) {
-      if (next < 0) {   // the block's last tile: nothing to hide the stores behind
-        g8_sfor<0, 16>([&](auto nc) { g8p_store_pk<decltype(nc)::value>(g, pk, m0, n0, wm, wn, q, r16); });
-        break;
-      }
-      pend = true;
-      pm0 = m0;
-      pn0 = n0;
+      g8p_epilogue<ACT, CT3, F16, has_bias, fold, DBG>(g, acc, m0, n0, wm, wn, q, r16, smem + G8_OPS + slot * G8P_EP);
     }
     if (next < 0) break;
     slot ^= 1;
-    S = (DBG == 1 || DBG == 2 || DBG == 8 || DEF) ? 0 : (m0 + 256 <= M ? (DBG == 7 ? s_full / 2 : s_full) : 0);
+    S = (DBG == 1 || DBG == 2) ? 0 : (m0 + 256 <= M ? s_full : 0);
     tile = next;
   }
 }
