@@ -2072,15 +2072,249 @@ int launch_attention_full(const AttnArgs& a, int B, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+// Pipelined form of attention_full_kernel: block = (clip, hpb heads) with one wave per 16-query block
+// (NKB waves), looping over its heads with the NEXT head's K, V, Q and gate rows in flight (LDS-DMA into
+// the other half of a double-buffered LDS image) while the current head computes.  The short-T kernel
+// loads a head, waits for it and computes it: its blocks spend most of their residency waiting on loads
+// (r2 PMC: VALU ~32 %, MFMA ~10 % busy, the CU reading ~10 GB/s).  Per wave the arithmetic is the
+// short-T kernel's, instruction for instruction (same fragments, same softmax order), so the two are
+// bit-identical; the output goes out through a buffer resource covering the clip's T rows (padded
+// query rows are dropped by the range check: every wave issues exactly 4 stores per head, which the
+// counted vmcnt at the top of the next head relies on).
+// LDS: 2 x (K | V | Q images of TP x 128 B, gate rows TP x 16 B) + the relative-position bias rows of
+// the block's heads; NKB = 10: 2 x 63 KB + 7.5 KB (hpb 6), one block per CU.
+SSE_DEV void attn_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+typedef unsigned int u32x2a __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4a __attribute__((ext_vector_type(4)));
+
+template <bool BIAS, int NKB, bool RAG, bool H16 = false>
+__global__ __launch_bounds__(64 * NKB, 1) void attention_pipe_kernel(AttnArgs a, int hpb) {
+  constexpr int TP = NKB * 16;
+  constexpr int NW = NKB;                      // waves: one 16-query block each
+  constexpr int KS = TP * 128;                 // one head's K (V, Q) image
+  constexpr int NGP = (TP + 63) / 64;          // gate-row pieces (64 rows x 16 B)
+  constexpr int BUF = 3 * KS + NGP * 1024;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* rb = (float*)(smem + 2 * BUF);        // [hpb][2 * TP] bias rows, then [hpb] gate constants
+
+  const int h0 = blockIdx.x * hpb, b = blockIdx.y;
+  const int TS = a.T, T = a.tlen ? a.tlen[b] : a.T, H = a.H, H3 = a.ldq;
+  if (T > TP) return;   // a long clip of a mixed ragged batch: the flash kernel's
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  const bf16* qkv = (const bf16*)a.qkv + (long long)b * TS * H3;
+  const float LOG2E = 1.4426950408889634f;
+  const __amdgpu_buffer_rsrc_t orsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)((bf16*)a.out + (long long)b * TS * H), (short)0, T * H * 2, 0x00020000);
+  const int swk = (r16 >> 1) & 7;
+  const int koff0 = r16 * 128 + ((g ^ swk) << 4), koff1 = r16 * 128 + (((g + 4) ^ swk) << 4);
+  const int rowv = 4 * g + (r16 >> 2), swv = ((rowv >> 1) & 3) << 1;
+  int voffs[4];
+  #pragma unroll
+  for (int db = 0; db < 4; ++db) voffs[db] = rowv * 128 + (((2 * db + ((r16 & 3) >> 1)) ^ swv) << 4) + 8 * (r16 & 1);
+
+  // head hh's K / V / Q (8-row pieces, wave w: pieces w and w + NW) and gate rows into image `buf`.
+  // The DMA is inline asm: issued through the builtin, the compiler puts a vmcnt(0) in front of every
+  // ds_read_b64_tr_b16 while it is in flight (it cannot tell the V^T reads from the DMA's target image),
+  // which would drain the next head's loads.  Invisible to the compiler, the DMA only ever makes its own
+  // vmcnt waits stronger (the asm is volatile with a memory clobber: no LDS access crosses it).  The
+  // s_nop is the M0-write -> LDS-DMA wait state the hazard recognizer would otherwise have inserted.
+  const u32x4a crs = {(unsigned)(size_t)qkv, (unsigned)((size_t)qkv >> 32) & 0xffffu, (unsigned)(T * H3 * 2), 0x00020000u};
+  const unsigned sbase = (unsigned)(size_t)LPTR(smem);
+  auto dma = [&](unsigned lds, unsigned voff) {
+    asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(crs), "{m0}"(lds) : "memory");
+  };
+  auto issue = [&](int hh, int buf) {
+    const int h = h0 + hh;
+    const unsigned base = sbase + buf * BUF;
+    #pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int p = wave + NW * u;
+      const int row = 8 * p + (lane >> 3);
+      const unsigned rbase = (unsigned)(row * H3 * 2);
+      const unsigned kch = (unsigned)(((lane & 7) ^ ((row >> 1) & 7)) << 4);
+      const unsigned vch = (unsigned)(((lane & 7) ^ (((row >> 1) & 3) << 1)) << 4);
+      dma(base + p * 1024, rbase + kch + (unsigned)((H + h * AT_HD) * 2));
+      dma(base + KS + p * 1024, rbase + vch + (unsigned)((2 * H + h * AT_HD) * 2));
+      dma(base + 2 * KS + p * 1024, rbase + kch + (unsigned)(h * AT_HD * 2));
+    }
+    if (BIAS && wave < NGP) dma(base + 3 * KS + wave * 1024, (unsigned)((64 * wave + lane) * H3 * 2 + (3 * H + 8 * h) * 2));
+  };
+  issue(0, 0);
+  if (BIAS) {
+    for (int i = tid; i < hpb * 2 * TP; i += 64 * NW) {
+      const int hh = i / (2 * TP), j = i - hh * 2 * TP;
+      float v = 0.f;
+      if (j < 2 * TP - 1) {
+        int d = j - (TP - 1);
+        d = d < -a.maxd ? -a.maxd : (d > a.maxd ? a.maxd : d);
+        v = a.relb[(long long)(h0 + hh) * (2 * a.maxd + 1) + a.maxd + d];
+      }
+      rb[i] = v;
+    }
+    // the gate constants too (a per-head load in the loop would be a vector load, and its wait a
+    // vmcnt(0) that drains the next head's DMA)
+    if (tid < hpb) rb[hpb * 2 * TP + tid] = a.gconst[h0 + tid];
+  }
+  const int qb = wave, qi = qb * 16 + r16;
+  const float sl2 = a.scale * LOG2E;
+  for (int hh = 0; hh < hpb; ++hh) {
+    const int h = h0 + hh;
+    // this wave's pieces of head hh have landed (only the 4 stores of head hh - 1 may be younger)
+    if (hh == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    attn_barrier();   // ...every wave's have, and every wave is done with image (hh + 1) & 1
+    if (hh + 1 < hpb) issue(hh + 1, (hh + 1) & 1);
+    const char* base = smem + (hh & 1) * BUF;
+    const char* Ks = base;
+    const char* Vs = base + KS;
+    const char* Qs = base + 2 * KS + qb * 2048;
+    bf16x8 qf[2];
+    qf[0] = *(const bf16x8*)(Qs + koff0);
+    qf[1] = *(const bf16x8*)(Qs + koff1);
+    f32x4 s[NKB];
+    #pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      #pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 kf = *(const bf16x8*)(Ks + kb * 2048 + (ks ? koff1 : koff0));
+        acc = mfma_h<H16>(kf, qf[ks], acc);
+      }
+      s[kb] = acc;
+    }
+    float gq2 = 0.f;
+    const float* rbh = rb + hh * 2 * TP;
+    if (BIAS) gq2 = wavlm_gate_v<H16>(*(const bf16x8*)(base + 3 * KS + qi * 16), rb[hpb * 2 * TP + hh]) * LOG2E;
+    #pragma unroll
+    for (int kb = 0; kb < NKB; ++kb)
+      #pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const int key = kb * 16 + 4 * g + 2 * hf;
+        f32x2 v = f32x2{s[kb][2 * hf], s[kb][2 * hf + 1]} * sl2;
+        if (BIAS) {
+          const int d = key - qi + (TP - 1);
+          v = __builtin_elementwise_fma(f32x2{gq2, gq2}, f32x2{rbh[d], rbh[d + 1]}, v);
+        }
+        if (RAG || kb >= NKB - 2) v = f32x2{key < T ? v.x : -INFINITY, key + 1 < T ? v.y : -INFINITY};
+        s[kb][2 * hf] = v.x;
+        s[kb][2 * hf + 1] = v.y;
+      }
+    float mx = fmaxf(s[0][0], s[0][1]);
+    #pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) mx = fmaxf(fmaxf(mx, fmaxf(s[kb][0], s[kb][1])), fmaxf(s[kb][2], s[kb][3]));
+    {
+      const auto t16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = fmaxf(__uint_as_float(t16[0]), __uint_as_float(t16[1]));
+      const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = fmaxf(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
+    }
+    f32x2 l2 = {0.f, 0.f};
+    const f32x2 mm = {-mx, -mx};
+    #pragma unroll
+    for (int kb = 0; kb < NKB; ++kb)
+      #pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const f32x2 d = f32x2{s[kb][2 * hf], s[kb][2 * hf + 1]} + mm;
+        const f32x2 p = {__builtin_amdgcn_exp2f(d.x), __builtin_amdgcn_exp2f(d.y)};
+        l2 += p;
+        s[kb][2 * hf] = p.x;
+        s[kb][2 * hf + 1] = p.y;
+      }
+    float l = l2.x + l2.y;
+    {
+      const auto t16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(l), __float_as_uint(l), false, false);
+      l = __uint_as_float(t16[0]) + __uint_as_float(t16[1]);
+      const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(l), __float_as_uint(l), false, false);
+      l = __uint_as_float(t32[0]) + __uint_as_float(t32[1]);
+    }
+    f32x4 o[4];
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    #pragma unroll
+    for (int ks = 0; ks < NKB / 2; ++ks) {
+      bf16x8 pf;
+      #pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pf[r] = hbits<H16>(s[2 * ks][r]);
+        pf[4 + r] = hbits<H16>(s[2 * ks + 1][r]);
+      }
+      #pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const char* va = Vs + ks * 4096 + voffs[db];
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)va);
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(va + 2048));
+        const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[db] = mfma_h<H16>(vf, pf, o[db]);
+      }
+    }
+    const float inv = 1.0f / l;
+    #pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const uint2 p = pack_h4<H16>(o[db] * inv);
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2a{p.x, p.y}, orsrc, (unsigned)((qi * H + h * AT_HD + db * 16 + 4 * g) * 2), 0, 0);
+    }
+  }
+}
+
+template <bool BIAS, int NKB, bool RAG, bool H16>
+int launch_attention_pipe(const AttnArgs& a, int B, hipStream_t s) {
+  constexpr int TP = NKB * 16;
+  constexpr int BUF = 3 * TP * 128 + ((TP + 63) / 64) * 1024;
+  constexpr int NT = 64 * NKB;
+  static int per_cu[64][13] = {{0}}, cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || a.nh > 12 * 64) return -2;
+  if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -2;
+  // heads per block: each block pays one exposed head load (its prologue), so the cost of a choice is
+  // block rounds x (heads per block + 1)
+  int hpb = 1;
+  double best = 1e30;
+  for (int c = 1; c <= a.nh && c <= 12; ++c) {
+    if (a.nh % c) continue;
+    const size_t lds = 2 * (size_t)BUF + (BIAS ? (size_t)c * (2 * TP + 1) * 4 : 0);
+    if (lds > 160 * 1024) continue;
+    int& pc = per_cu[dev][c];
+    if (!pc) {
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, attention_pipe_kernel<BIAS, NKB, RAG, H16>, NT, lds) != hipSuccess)
+        return -2;
+      if (pc < 1) pc = -1;
+    }
+    if (pc < 1) continue;
+    const long long slots = (long long)cus[dev] * pc;
+    const long long nb = (long long)(a.nh / c) * B;
+    const long long rounds = (nb + slots - 1) / slots;
+    const double cost = (double)rounds * (c + 1);
+    if (cost < best) best = cost, hpb = c;
+  }
+  if (best >= 1e30) return -3;
+  const size_t lds = 2 * (size_t)BUF + (BIAS ? (size_t)hpb * (2 * TP + 1) * 4 : 0);
+  hipLaunchKernelGGL((attention_pipe_kernel<BIAS, NKB, RAG, H16>), dim3(a.nh / hpb, B), dim3(NT), lds, s, a, hpb);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+template <bool BIAS, int NKB, bool RAG, bool H16>
+int launch_attention_short(const AttnArgs& a, int B, hipStream_t s) {
+  return sse_opt(OPT_ATTN_PIPE) ? launch_attention_pipe<BIAS, NKB, RAG, H16>(a, B, s)
+                                : launch_attention_full<BIAS, NKB, RAG, H16>(a, B, s);
+}
+
 template <bool BIAS, bool RAG, bool H16>
 int dispatch_full(const AttnArgs& a, int B, hipStream_t s) {
   const int nkb = ((a.T + 31) / 32) * 2;
   switch (nkb) {
-    case 2: return launch_attention_full<BIAS, 2, RAG, H16>(a, B, s);
-    case 4: return launch_attention_full<BIAS, 4, RAG, H16>(a, B, s);
-    case 6: return launch_attention_full<BIAS, 6, RAG, H16>(a, B, s);
-    case 8: return launch_attention_full<BIAS, 8, RAG, H16>(a, B, s);
-    case 10: return launch_attention_full<BIAS, 10, RAG, H16>(a, B, s);
+    case 2: return launch_attention_short<BIAS, 2, RAG, H16>(a, B, s);
+    case 4: return launch_attention_short<BIAS, 4, RAG, H16>(a, B, s);
+    case 6: return launch_attention_short<BIAS, 6, RAG, H16>(a, B, s);
+    case 8: return launch_attention_short<BIAS, 8, RAG, H16>(a, B, s);
+    case 10: return launch_attention_short<BIAS, 10, RAG, H16>(a, B, s);
     default: return -3;
   }
 }
@@ -2106,8 +2340,8 @@ int launch_attention(const AttnArgs& a, int B, hipStream_t s) {
       // ragged batch with clips on both sides of 160 frames: each clip runs the kernel it would run
       // alone (the short-T kernel at 10 key blocks skips the long clips, the flash kernel the short
       // ones), so every clip's result is bit-identical to its solo call
-      const int rc = a.relb ? launch_attention_full<true, 10, true, H>(a, B, s)
-                            : launch_attention_full<false, 10, true, H>(a, B, s);
+      const int rc = a.relb ? launch_attention_short<true, 10, true, H>(a, B, s)
+                            : launch_attention_short<false, 10, true, H>(a, B, s);
       if (rc) return rc;
       af.min_t = 160;
     }
