@@ -2179,17 +2179,19 @@ __global__ __launch_bounds__(64 * NKB, 1) void attention_pipe_kernel(AttnArgs a,
     bf16x8 qf[2];
     qf[0] = *(const bf16x8*)(Qs + koff0);
     qf[1] = *(const bf16x8*)(Qs + koff1);
-    f32x4 s[NKB];
+    // all K fragments first, then the 2 x NKB MFMAs as NKB independent chains (the per-kb read ->
+    // wait -> dependent MFMA pair the compiler schedules otherwise is latency-bound at 2-3 waves/SIMD)
+    bf16x8 kf[NKB][2];
     #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
-      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-      #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 kf = *(const bf16x8*)(Ks + kb * 2048 + (ks ? koff1 : koff0));
-        acc = mfma_h<H16>(kf, qf[ks], acc);
-      }
-      s[kb] = acc;
+      kf[kb][0] = *(const bf16x8*)(Ks + kb * 2048 + koff0);
+      kf[kb][1] = *(const bf16x8*)(Ks + kb * 2048 + koff1);
     }
+    f32x4 s[NKB];
+    #pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) s[kb] = mfma_h<H16>(kf[kb][0], qf[0], f32x4{0.f, 0.f, 0.f, 0.f});
+    #pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) s[kb] = mfma_h<H16>(kf[kb][1], qf[1], s[kb]);
     float gq2 = 0.f;
     const float* rbh = rb + hh * 2 * TP;
     if (BIAS) gq2 = wavlm_gate_v<H16>(*(const bf16x8*)(base + 3 * KS + qi * 16), rb[hpb * 2 * TP + hh]) * LOG2E;
