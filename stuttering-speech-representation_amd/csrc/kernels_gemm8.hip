@@ -807,9 +807,11 @@ SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, i
   // with v_permlane16_swap so every lane holds 8 consecutive columns: one 16-B store per (i, ni), through
   // a buffer resource based at the tile's first row (no 64-bit address math, no exec-mask branch per
   // store: rows >= M fall outside its num_records)
+  // (based at the tile's first element (m0, n0): num_records ends at row M's column n0, so every column
+  // of rows < M is in range -- n0 + 256 (+ 2N, CT3) <= ldc -- and every row >= M is out)
   const __amdgpu_buffer_rsrc_t ct_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)((bf16*)g.Ct + (long long)m0 * g.ldc), (short)0,
-      (int)min((long long)(g.M - m0) * g.ldc * 2, (long long)0x7FFFFFF0), 0x00020000);
+      (void*)((bf16*)g.Ct + (long long)m0 * g.ldc + n0), (short)0,
+      (int)min((long long)(g.M - m0) * g.ldc * 2 - (long long)n0 * 2, (long long)0x7FFFFFF0), 0x00020000);
   const unsigned lane_off = (unsigned)(((wm * 64 + r16) * g.ldc + wn * 32 + (q & 1) * 16 + (q >> 1) * 8) * 2);
   auto store_half = [&](int mi) {
     #pragma unroll

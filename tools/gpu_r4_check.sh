@@ -5,7 +5,11 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 TAG=$1; N=$2; shift 2
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1
+if [ -x tools/_build/attn_probe ]; then
+  timeout -k 10 120 tools/_build/attn_probe > gpurun_out/${TAG}_attn_probe.txt 2>&1 || { echo "attn probe failed"; tail -5 gpurun_out/${TAG}_attn_probe.txt; exit 1; }
+  cat gpurun_out/${TAG}_attn_probe.txt | grep -v "^  mismatch" 
+fi
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/${TAG}_tests.log 2>&1
 rc=$?
 tail -3 gpurun_out/${TAG}_tests.log
 [ $rc -eq 0 ] || { grep -E "FAILED|Error|error" gpurun_out/${TAG}_tests.log | head -20; exit $rc; }
