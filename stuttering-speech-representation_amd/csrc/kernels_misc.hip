@@ -2093,7 +2093,9 @@ SSE_DEV void attn_barrier() {
 typedef unsigned int u32x2a __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4a __attribute__((ext_vector_type(4)));
 
-template <bool BIAS, int NKB, bool RAG, bool H16 = false>
+// DBG (tools/attn_probe.hip timing only): 1 = loads and waits, no compute / stores; 2 = compute on the
+// first head's image, no further loads
+template <bool BIAS, int NKB, bool RAG, bool H16 = false, int DBG = 0>
 __global__ __launch_bounds__(64 * NKB, 1) void attention_pipe_kernel(AttnArgs a, int hpb) {
   constexpr int TP = NKB * 16;
   constexpr int NW = NKB;                      // waves: one 16-query block each
@@ -2168,11 +2170,15 @@ __global__ __launch_bounds__(64 * NKB, 1) void attention_pipe_kernel(AttnArgs a,
   for (int hh = 0; hh < hpb; ++hh) {
     const int h = h0 + hh;
     // this wave's pieces of head hh have landed (only the 4 stores of head hh - 1 may be younger)
-    if (hh == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    if (hh == 0 || DBG == 2) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     attn_barrier();   // ...every wave's have, and every wave is done with image (hh + 1) & 1
-    if (hh + 1 < hpb) issue(hh + 1, (hh + 1) & 1);
-    const char* base = smem + (hh & 1) * BUF;
+    if (DBG != 2 && hh + 1 < hpb) issue(hh + 1, (hh + 1) & 1);
+    if constexpr (DBG == 1) {
+      for (int db = 0; db < 4; ++db) __builtin_amdgcn_raw_buffer_store_b64(u32x2a{0u, 0u}, orsrc, 0x7FFFFFF0u, 0, 0);
+      continue;
+    }
+    const char* base = smem + (DBG == 2 ? 0 : (hh & 1)) * BUF;
     const char* Ks = base;
     const char* Vs = base + KS;
     const char* Qs = base + 2 * KS + qb * 2048;
@@ -2266,7 +2272,7 @@ __global__ __launch_bounds__(64 * NKB, 1) void attention_pipe_kernel(AttnArgs a,
   }
 }
 
-template <bool BIAS, int NKB, bool RAG, bool H16>
+template <bool BIAS, int NKB, bool RAG, bool H16, int DBG = 0>
 int launch_attention_pipe(const AttnArgs& a, int B, hipStream_t s) {
   constexpr int TP = NKB * 16;
   constexpr int BUF = 3 * TP * 128 + ((TP + 63) / 64) * 1024;
@@ -2285,7 +2291,7 @@ int launch_attention_pipe(const AttnArgs& a, int B, hipStream_t s) {
     if (lds > 160 * 1024) continue;
     int& pc = per_cu[dev][c];
     if (!pc) {
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, attention_pipe_kernel<BIAS, NKB, RAG, H16>, NT, lds) != hipSuccess)
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, attention_pipe_kernel<BIAS, NKB, RAG, H16, DBG>, NT, lds) != hipSuccess)
         return -2;
       if (pc < 1) pc = -1;
     }
@@ -2298,7 +2304,7 @@ int launch_attention_pipe(const AttnArgs& a, int B, hipStream_t s) {
   }
   if (best >= 1e30) return -3;
   const size_t lds = 2 * (size_t)BUF + (BIAS ? (size_t)hpb * (2 * TP + 1) * 4 : 0);
-  hipLaunchKernelGGL((attention_pipe_kernel<BIAS, NKB, RAG, H16>), dim3(a.nh / hpb, B), dim3(NT), lds, s, a, hpb);
+  hipLaunchKernelGGL((attention_pipe_kernel<BIAS, NKB, RAG, H16, DBG>), dim3(a.nh / hpb, B), dim3(NT), lds, s, a, hpb);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -81,6 +81,29 @@ static int run(int B, int T, bool h16, bool ragged, int reps) {
     CK(hipEventElapsedTime(&ms[k], e0, e1));
     ms[k] /= reps;
   }
+  if (!h16 && !ragged && T == 149 && B >= 128) {   // where a head's time goes: loads only / compute only
+    AttnArgs a{};
+    a.qkv = dq, a.out = dout[1], a.T = T, a.H = H, a.nh = nh, a.ldq = ldq, a.scale = 0.125f;
+    a.gconst = dg, a.relb = dr, a.maxd = maxd;
+    float md[2];
+    for (int d = 0; d < 2; ++d) {
+      auto go = [&] { return d == 0 ? launch_attention_pipe<true, 10, false, false, 1>(a, B, 0)
+                                    : launch_attention_pipe<true, 10, false, false, 2>(a, B, 0); };
+      (void)go();
+      CK(hipDeviceSynchronize());
+      CK(hipEventRecord(e0, 0));
+      for (int r = 0; r < reps; ++r) (void)go();
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&md[d], e0, e1));
+      md[d] /= reps;
+    }
+    std::printf("  pipe B=%d: loads+waits only %.2f us, compute only %.2f us\n", B, 1e3 * md[0], 1e3 * md[1]);
+    CK(hipMemset(dout[1], 0, ob));
+    g_pipe = 1;
+    (void)launch_attention<bf16>(a, B, 0);
+    CK(hipDeviceSynchronize());
+  }
   std::vector<uint16_t> o0(ob / 2), o1(ob / 2);
   CK(hipMemcpy(o0.data(), dout[0], ob, hipMemcpyDeviceToHost));
   CK(hipMemcpy(o1.data(), dout[1], ob, hipMemcpyDeviceToHost));
