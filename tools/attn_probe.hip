@@ -40,13 +40,14 @@ static int run(int B, int T, bool h16, bool ragged, int reps) {
   for (auto& x : hr) x = rnd();
   std::vector<int> hl(B);
   for (int b = 0; b < B; ++b) hl[b] = ragged ? (b % 5 == 0 ? T : 1 + (int)((T - 1) * (0.5f + 0.5f * rnd()))) : T;
-  void *dq, *dout[2];
+  void *dq, *dout[3];
   float *dg, *dr;
   int* dl;
   const size_t ob = (size_t)B * T * H * 2;
   CK(hipMalloc(&dq, hq.size() * 2));
   CK(hipMalloc(&dout[0], ob));
   CK(hipMalloc(&dout[1], ob));
+  CK(hipMalloc(&dout[2], ob));
   CK(hipMalloc(&dg, nh * 4));
   CK(hipMalloc(&dr, hr.size() * 4));
   CK(hipMalloc(&dl, B * 4));
@@ -54,11 +55,11 @@ static int run(int B, int T, bool h16, bool ragged, int reps) {
   CK(hipMemcpy(dg, hg.data(), nh * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(dr, hr.data(), hr.size() * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(dl, hl.data(), B * 4, hipMemcpyHostToDevice));
-  float ms[2] = {0, 0};
+  float ms[3] = {0, 0, 0};
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < 3; ++k) {
     CK(hipMemset(dout[k], 0, ob));
     AttnArgs a{};
     a.qkv = dq;
@@ -102,34 +103,38 @@ static int run(int B, int T, bool h16, bool ragged, int reps) {
     CK(hipMemset(dout[1], 0, ob));
     g_pipe = 1;
     (void)launch_attention<bf16>(a, B, 0);
-    CK(hipDeviceSynchronize());
+    CK(hipDeviceSynchronize());   // (dout[1] restored for the comparison)
   }
   std::vector<uint16_t> o0(ob / 2), o1(ob / 2);
   CK(hipMemcpy(o0.data(), dout[0], ob, hipMemcpyDeviceToHost));
-  CK(hipMemcpy(o1.data(), dout[1], ob, hipMemcpyDeviceToHost));
-  long long bad = 0;
-  int shown = 0;
-  for (int b = 0; b < B; ++b)
-    for (int t = 0; t < hl[b]; ++t)
-      for (int c = 0; c < H; ++c) {
-        const size_t i = ((size_t)b * T + t) * H + c;
-        if (o0[i] != o1[i]) {
-          if (shown < 12) {
-            std::printf("  mismatch clip %d row %d head %d col %d: %04x vs %04x\n", b, t, c / 64, c % 64, o0[i], o1[i]);
-            ++shown;
+  long long bad[3] = {0, 0, 0};
+  for (int k = 1; k < 3; ++k) {
+    CK(hipMemcpy(o1.data(), dout[k], ob, hipMemcpyDeviceToHost));
+    int shown = 0;
+    for (int b = 0; b < B; ++b)
+      for (int t = 0; t < hl[b]; ++t)
+        for (int c = 0; c < H; ++c) {
+          const size_t i = ((size_t)b * T + t) * H + c;
+          if (o0[i] != o1[i]) {
+            if (shown < 8) {
+              std::printf("  mismatch (pipe %d) clip %d row %d head %d col %d: %04x vs %04x\n", k, b, t, c / 64, c % 64, o0[i],
+                          o1[i]);
+              ++shown;
+            }
+            ++bad[k];
           }
-          ++bad;
         }
-      }
-  std::printf("B=%d T=%d %s%s: full %.2f us, pipe %.2f us, mismatches %lld\n", B, T, h16 ? "fp16" : "bf16",
-              ragged ? " ragged" : "", 1e3 * ms[0], 1e3 * ms[1], bad);
+  }
+  std::printf("B=%d T=%d %s%s: full %.2f us, pipe %.2f us, pipe3 %.2f us, mismatches %lld / %lld\n", B, T,
+              h16 ? "fp16" : "bf16", ragged ? " ragged" : "", 1e3 * ms[0], 1e3 * ms[1], 1e3 * ms[2], bad[1], bad[2]);
   CK(hipFree(dq));
   CK(hipFree(dout[0]));
   CK(hipFree(dout[1]));
+  CK(hipFree(dout[2]));
   CK(hipFree(dg));
   CK(hipFree(dr));
   CK(hipFree(dl));
-  return bad ? 1 : 0;
+  return bad[1] || bad[2] ? 1 : 0;
 }
 
 int main() {
@@ -141,6 +146,7 @@ int main() {
   fails += run(256, 149, false, false, 20);
   fails += run(128, 149, true, false, 20);
   fails += run(48, 149, false, true, 5);
+  fails += run(256, 149, true, true, 10);
   std::printf("%s\n", fails ? "DIFFER" : "all identical");
   return 0;
 }
