@@ -9,6 +9,10 @@ if [ -x tools/_build/attn_probe ]; then
   timeout -k 10 120 tools/_build/attn_probe > gpurun_out/${TAG}_attn_probe.txt 2>&1 || { echo "attn probe failed"; tail -5 gpurun_out/${TAG}_attn_probe.txt; exit 1; }
   cat gpurun_out/${TAG}_attn_probe.txt | grep -v "^  mismatch" 
 fi
+if [ -x tools/_build/gemm8mx_probe ]; then
+  timeout -k 10 120 tools/_build/gemm8mx_probe > gpurun_out/${TAG}_mx_probe.txt 2>&1 || { echo "mx probe failed"; tail -5 gpurun_out/${TAG}_mx_probe.txt; exit 1; }
+  cat gpurun_out/${TAG}_mx_probe.txt
+fi
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/${TAG}_tests.log 2>&1
 rc=$?
 tail -3 gpurun_out/${TAG}_tests.log
