@@ -807,15 +807,21 @@ SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, i
   // with v_permlane16_swap so every lane holds 8 consecutive columns: one 16-B store per (i, ni), through
   // a buffer resource based at the tile's first row (no 64-bit address math, no exec-mask branch per
   // store: rows >= M fall outside its num_records)
-  // (based at the tile's first element (m0, n0): num_records ends at row M's column n0, so every column
-  // of rows < M is in range -- n0 + 256 (+ 2N, CT3) <= ldc -- and every row >= M is out)
-  const __amdgpu_buffer_rsrc_t ct_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)((bf16*)g.Ct + (long long)m0 * g.ldc + n0), (short)0,
-      (int)min((long long)(g.M - m0) * g.ldc * 2 - (long long)n0 * 2, (long long)0x7FFFFFF0), 0x00020000);
+  // One resource per 16-row block i, based at element (m0 + 16 i, n0): its num_records ends at row M's
+  // column n0, so every column of rows < M is in range (n0 + 256 (+ 2N, CT3) <= ldc) and every row >= M out.
+  // (The row block cannot ride in the SGPR offset of one tile-wide resource: the range check sees only the
+  // VGPR offset + immediate, so rows >= M of a partial tile would be written.)
+  auto ct_rsrc_of = [&](int i) {
+    const long long rows = (long long)g.M - m0 - 16 * i;
+    const long long nrec = rows > 0 ? rows * g.ldc * 2 - (long long)n0 * 2 : 0;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((bf16*)g.Ct + (long long)(m0 + 16 * i) * g.ldc + n0), (short)0,
+                                             (int)min(nrec, (long long)0x7FFFFFF0), 0x00020000);
+  };
   const unsigned lane_off = (unsigned)(((wm * 64 + r16) * g.ldc + wn * 32 + (q & 1) * 16 + (q >> 1) * 8) * 2);
   auto store_half = [&](int mi) {
     #pragma unroll
     for (int i = 0; i < 4; ++i) {
+      const __amdgpu_buffer_rsrc_t ct_rsrc = ct_rsrc_of(i);
       const int m = m0 + mi * 128 + wm * 64 + i * 16 + r16;
       const bool ok = m < g.M;
       const long long row = (long long)(ok ? m : 0) * g.ldc;
@@ -851,9 +857,9 @@ SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, i
             asm volatile("" ::"v"(s0[0]), "v"(s0[1]), "v"(s1[0]), "v"(s1[1]));
             continue;
           }
-          // the tile's buffer resource: lane offset (one VGPR per half) + row-block offset in an SGPR + the
-          // column block as an immediate; rows >= M are dropped by the range check
-          const unsigned soff = (unsigned)(i * 16 * g.ldc * 2);
+          // the row block's buffer resource: lane offset (one VGPR per half) + the column block as an
+          // immediate; rows >= M are dropped by the range check
+          const unsigned soff = 0u;
           const unsigned voff = lane_off + (unsigned)(mi * 128 * g.ldc * 2) + (unsigned)(ni * 256);
           const u32x4 v = {s0[0], s1[0], s0[1], s1[1]};
           __builtin_amdgcn_raw_buffer_store_b128(v, ct_rsrc, voff, soff, 0);
