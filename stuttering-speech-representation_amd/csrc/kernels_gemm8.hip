@@ -245,6 +245,29 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
     }
   };
 
+  // the steady loop's issue (t + 2 < nk): phase p's (tile, half) known at compile time and no range checks.
+  // Branch-free on purpose: with issue()'s checks the K-tile body is several basic blocks, sched_barrier
+  // does not hold across them, and the MX build had its phase 0-2 MFMAs sunk to the end of the K-tile
+  // (the ping-pong gone: 8 0 0 0 MFMAs per phase in the ISA)
+  auto issue_steady = [&](int t, auto p_c) {
+    constexpr int P = decltype(p_c)::value;
+    constexpr int half = P == 0 ? 3 : (P == 1 ? 1 : (P == 2 ? 0 : 2));
+    const int tile = P < 2 ? t + 1 : t + 2;
+    char* dst = smem + (tile & 1) * G8_BUF + half * G8_HALF;
+    const unsigned soff = (unsigned)tile * 128u;
+    if constexpr (MX && half == 0)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(s_rsrc, LPTR(smem + G8_OPS + (tile & 3) * G8_SC + wave * 256), 4, s_voff,
+                                               (unsigned)tile * 1024u, 0, 0);
+    if constexpr (half < 2) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, LPTR(dst + wave * 1024), 16, a_voff[half][0], soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, LPTR(dst + (wave + 8) * 1024), 16, a_voff[half][1], soff, 0, 0);
+    } else {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, LPTR(dst + wave * 1024), 16, b_voff[half - 2][0], soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, LPTR(dst + (wave + 8) * 1024), 16, b_voff[half - 2][1], soff, 0,
+                                               0);
+    }
+  };
+
   f32x4 acc[2][2][4][2];
   #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -332,18 +355,22 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
 
   // steady K-tiles (t + 2 < nk): every phase issues a half and waits vmcnt(8) with no
   // scalar bookkeeping; the last two K-tiles take the counted tail path.
-  auto run_tile = [&](int t, auto steady) {
-    constexpr bool ST = decltype(steady)::value;
+  // MODE 1: steady K-tile (t + 2 < nk), branch-free (issue_steady, a uniform counted wait); 0: the last two
+  // K-tiles (range-checked issues and computed waits; there the compiler still sinks the MX MFMAs of phases
+  // 1-3 to the K-tile's end -- a compile-time tail kept them in place but spilled the 256-VGPR MX kernel)
+  auto run_tile = [&](int t, auto mode_c) {
+    constexpr int MODE = decltype(mode_c)::value;
     const char* buf = smem + (t & 1) * G8_BUF;
     const int k = 4 * t;
-    auto issue_wait = [&](int kk) {
-      if constexpr (ST) {
-        issue(kk);
+    auto issue_wait = [&](auto p_c) {
+      constexpr int P = decltype(p_c)::value;
+      if constexpr (MODE == 1) {
+        issue_steady(t, p_c);
         if constexpr (MX) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       } else {
-        issue(kk);
-        g8_wait<MX>(kk, nk);
+        issue(k + P);
+        g8_wait<MX>(k + P, nk);
       }
     };
     const std::integral_constant<int, 0> ni0;
@@ -353,32 +380,32 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
     read_b(buf + 2 * G8_HALF, b0f, b0x);
     read_sa(t, 0);
     read_sb(t);
-    issue_wait(k);
+    issue_wait(std::integral_constant<int, 0>{});
     g8_barrier();
     mma(acc[0][0], b0f, b0x, ni0);
     g8_barrier();
     // phase 1: (mi 0, ni 1) reads B cols 128-255
     read_b(buf + 3 * G8_HALF, b1f, b1x);
-    issue_wait(k + 1);
+    issue_wait(std::integral_constant<int, 1>{});
     g8_barrier();
     mma(acc[0][1], b1f, b1x, ni1);
     g8_barrier();
     // phase 2: (mi 1, ni 1) reads A rows 128-255
     read_a(buf + G8_HALF);
     read_sa(t, 1);
-    issue_wait(k + 2);
+    issue_wait(std::integral_constant<int, 2>{});
     g8_barrier();
     mma(acc[1][1], b1f, b1x, ni1);
     g8_barrier();
     // phase 3: (mi 1, ni 0) no reads
-    issue_wait(k + 3);
+    issue_wait(std::integral_constant<int, 3>{});
     g8_barrier();
     mma(acc[1][0], b0f, b0x, ni0);
     g8_barrier();
   };
   int t = 0;
-  for (; t + 2 < nk; ++t) run_tile(t, std::integral_constant<bool, true>{});
-  for (; t < nk; ++t) run_tile(t, std::integral_constant<bool, false>{});
+  for (; t + 2 < nk; ++t) run_tile(t, std::integral_constant<int, 1>{});
+  for (; t < nk; ++t) run_tile(t, std::integral_constant<int, 0>{});
   if (wm == 0) g8_barrier();   // balance group 1's extra barrier
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if constexpr (DBG == 1) {
