@@ -1349,6 +1349,20 @@ SSE_DEV float wavlm_gate_v(const bf16x8& r, float c) {
   const float ga = 1.f / (1.f + expf(-ra)), gb = 1.f / (1.f + expf(-rb));
   return ga * (gb * c - 1.0f) + 2.0f;
 }
+// wavlm_gate_v for the 16 rows of a wave whose 4 lane groups hold the same row (attn_head_body): each lane
+// pair of groups (0, 1) / (2, 3) evaluates one of the two sigmoids and swaps it with its partner
+// (v_permlane16_swap: result 0 = the even group's value, 1 = the odd group's), one exp + one divide per
+// lane instead of two; bit-identical to wavlm_gate_v
+template <bool H16 = false>
+SSE_DEV float wavlm_gate_pair(const bf16x8& r, float c, int g) {
+  const float ra = hval<H16>(r[0]) + hval<H16>(r[1]) + hval<H16>(r[2]) + hval<H16>(r[3]);
+  const float rb = hval<H16>(r[4]) + hval<H16>(r[5]) + hval<H16>(r[6]) + hval<H16>(r[7]);
+  const float x = (g & 1) ? rb : ra;
+  const float sg = 1.f / (1.f + expf(-x));
+  const auto t = __builtin_amdgcn_permlane16_swap(__float_as_uint(sg), __float_as_uint(sg), false, false);
+  const float ga = __uint_as_float(t[0]), gb = __uint_as_float(t[1]);
+  return ga * (gb * c - 1.0f) + 2.0f;
+}
 
 // X3 (split-fp16 path, TE = float, a.out3): fp32 q/k/v from the QKV GEMM, split while loaded / staged
 // (x3_split4) into hi and lo' 2^-11 planes, and both products on the f16 matrix cores with the bf16
@@ -2082,7 +2096,7 @@ int launch_attention_full(const AttnArgs& a, int B, hipStream_t s) {
 // query rows are dropped by the range check: every wave issues exactly 4 stores per head, which the
 // counted vmcnt at the top of the next head relies on).
 // LDS: 2 x (K | V | Q images of TP x 128 B, gate rows TP x 16 B) + the relative-position bias rows of
-// the block's heads; NKB = 10: 2 x 63 KB + 7.5 KB (hpb 6), one block per CU.
+// the block's heads (pairs, 2.5 KB per head); NKB = 10: 2 x 63 KB + 15 KB (hpb 6), one block per CU.
 SSE_DEV void attn_barrier() {
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("" ::: "memory");
@@ -2091,6 +2105,7 @@ SSE_DEV void attn_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 typedef unsigned int u32x2a __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) const float2 lds_f2;
 typedef unsigned int u32x4a __attribute__((ext_vector_type(4)));
 
 // One head of one 16-query block (one wave): S = K Q^T from the LDS images (K fragments first, then the
@@ -2099,7 +2114,7 @@ typedef unsigned int u32x4a __attribute__((ext_vector_type(4)));
 // Shared by attention_pipe_kernel and attention_pipe3_kernel, instruction for instruction the per-query-
 // block body of attention_full_kernel (bit-identical results).
 template <bool BIAS, int NKB, bool RAG, bool H16>
-SSE_DEV void attn_head_body(const char* Ks, const char* Vs, const char* grow, const bf16x8 (&qf)[2], const float* rbh,
+SSE_DEV void attn_head_body(const char* Ks, const char* Vs, const char* grow, const bf16x8 (&qf)[2], const float2* rbp,
                             float gcon, int T, int qi, int g, int koff0, int koff1, const int (&voffs)[4], float sl2,
                             __amdgpu_buffer_rsrc_t orsrc, unsigned obase) {
   constexpr int TP = NKB * 16;
@@ -2118,7 +2133,12 @@ SSE_DEV void attn_head_body(const char* Ks, const char* Vs, const char* grow, co
   #pragma unroll
   for (int kb = 0; kb < NKB; ++kb) s[kb] = mfma_h<H16>(kf[kb][1], qf[1], s[kb]);
   float gq2 = 0.f;
-  if (BIAS) gq2 = wavlm_gate_v<H16>(*(const bf16x8*)grow, gcon) * LOG2E;
+  if (BIAS) gq2 = wavlm_gate_pair<H16>(*(const bf16x8*)grow, gcon, g) * LOG2E;
+  // this lane's bias pairs start at d0 = 4 g - qi + TP - 1 (d = d0 + 16 kb + 2 hf): its LDS address in a
+  // register the compiler cannot fold (the table sits past 64 KB, beyond a ds_read's 16-bit offset, and a
+  // folded constant base costs a v_add per read), the key-block offsets as immediates
+  unsigned rl = (unsigned)(size_t)LPTR(rbp + (4 * g - qi + (TP - 1)));
+  asm volatile("" : "+v"(rl));
   #pragma unroll
   for (int kb = 0; kb < NKB; ++kb)
     #pragma unroll
@@ -2127,7 +2147,8 @@ SSE_DEV void attn_head_body(const char* Ks, const char* Vs, const char* grow, co
       f32x2 v = f32x2{s[kb][2 * hf], s[kb][2 * hf + 1]} * sl2;
       if (BIAS) {
         const int d = key - qi + (TP - 1);
-        v = __builtin_elementwise_fma(f32x2{gq2, gq2}, f32x2{rbh[d], rbh[d + 1]}, v);
+        const float2 rr = *(const lds_f2*)(size_t)(rl + (unsigned)((kb * 16 + 2 * hf) * 8));   // (bias[d], bias[d + 1])
+        v = __builtin_elementwise_fma(f32x2{gq2, gq2}, f32x2{rr.x, rr.y}, v);
       }
       if (RAG || kb >= NKB - 2) v = f32x2{key < T ? v.x : -INFINITY, key + 1 < T ? v.y : -INFINITY};
       s[kb][2 * hf] = v.x;
@@ -2199,7 +2220,8 @@ __global__ __launch_bounds__(64 * NKB, 1) void attention_pipe_kernel(AttnArgs a,
   constexpr int NGP = (TP + 63) / 64;          // gate-row pieces (64 rows x 16 B)
   constexpr int BUF = 3 * KS + NGP * 1024;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* rb = (float*)(smem + 2 * BUF);        // [hpb][2 * TP] bias rows, then [hpb] gate constants
+  float2* rb2 = (float2*)(smem + 2 * BUF);     // [hpb][2 * TP] bias pairs, then [hpb] gate constants
+  float* gcs = (float*)(rb2 + hpb * 2 * TP);
 
   const int h0 = blockIdx.x * hpb, b = blockIdx.y;
   const int TS = a.T, T = a.tlen ? a.tlen[b] : a.T, H = a.H, H3 = a.ldq;
@@ -2247,19 +2269,25 @@ __global__ __launch_bounds__(64 * NKB, 1) void attention_pipe_kernel(AttnArgs a,
   };
   issue(0, 0);
   if (BIAS) {
+    // pairs (bias[j], bias[j + 1]) per head, j < 2 TP (bias[j] = 0 for j >= 2 TP - 1)
     for (int i = tid; i < hpb * 2 * TP; i += 64 * NW) {
       const int hh = i / (2 * TP), j = i - hh * 2 * TP;
-      float v = 0.f;
-      if (j < 2 * TP - 1) {
-        int d = j - (TP - 1);
-        d = d < -a.maxd ? -a.maxd : (d > a.maxd ? a.maxd : d);
-        v = a.relb[(long long)(h0 + hh) * (2 * a.maxd + 1) + a.maxd + d];
+      const float* rh = a.relb + (long long)(h0 + hh) * (2 * a.maxd + 1) + a.maxd;
+      float v[2];
+      #pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        v[e] = 0.f;
+        if (j + e < 2 * TP - 1) {
+          int d = j + e - (TP - 1);
+          d = d < -a.maxd ? -a.maxd : (d > a.maxd ? a.maxd : d);
+          v[e] = rh[d];
+        }
       }
-      rb[i] = v;
+      rb2[i] = make_float2(v[0], v[1]);
     }
     // the gate constants too (a per-head load in the loop would be a vector load, and its wait a
     // vmcnt(0) that drains the next head's DMA)
-    if (tid < hpb) rb[hpb * 2 * TP + tid] = a.gconst[h0 + tid];
+    if (tid < hpb) gcs[tid] = a.gconst[h0 + tid];
   }
   const int qb = wave, qi = qb * 16 + r16;
   const float sl2 = a.scale * LOG2E;
@@ -2281,7 +2309,7 @@ __global__ __launch_bounds__(64 * NKB, 1) void attention_pipe_kernel(AttnArgs a,
     bf16x8 qf[2];
     qf[0] = *(const bf16x8*)(Qs + koff0);
     qf[1] = *(const bf16x8*)(Qs + koff1);
-    attn_head_body<BIAS, NKB, RAG, H16>(Ks, Vs, base + 3 * KS + qi * 16, qf, rb + hh * 2 * TP, BIAS ? rb[hpb * 2 * TP + hh] : 0.f, T,
+    attn_head_body<BIAS, NKB, RAG, H16>(Ks, Vs, base + 3 * KS + qi * 16, qf, rb2 + hh * 2 * TP, BIAS ? gcs[hh] : 0.f, T,
                                         qi, g, koff0, koff1, voffs, sl2, orsrc, (unsigned)((qi * H + h * AT_HD) * 2));
   }
 }
@@ -2301,7 +2329,8 @@ __global__ __launch_bounds__(64 * NKB, 1) void attention_pipe3_kernel(AttnArgs a
   constexpr int SLOT = 2 * KS + NGP * 1024;   // K | V | gate rows
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Qimg = smem + 3 * SLOT;                // [TP][128 B]
-  float* rb = (float*)(Qimg + KS);             // [hpb][2 * TP] bias rows, then [hpb] gate constants
+  float2* rb2 = (float2*)(Qimg + KS);          // [hpb][2 * TP] bias pairs, then [hpb] gate constants
+  float* gcs = (float*)(rb2 + hpb * 2 * TP);
 
   const int h0 = blockIdx.x * hpb, b = blockIdx.y;
   const int TS = a.T, T = a.tlen ? a.tlen[b] : a.T, H = a.H, H3 = a.ldq;
@@ -2355,17 +2384,23 @@ __global__ __launch_bounds__(64 * NKB, 1) void attention_pipe3_kernel(AttnArgs a
   issue(0);
   if (1 < hpb) issue(1);
   if (BIAS) {
+    // pairs (bias[j], bias[j + 1]) per head, j < 2 TP (bias[j] = 0 for j >= 2 TP - 1)
     for (int i = tid; i < hpb * 2 * TP; i += 64 * NW) {
       const int hh = i / (2 * TP), j = i - hh * 2 * TP;
-      float v = 0.f;
-      if (j < 2 * TP - 1) {
-        int d = j - (TP - 1);
-        d = d < -a.maxd ? -a.maxd : (d > a.maxd ? a.maxd : d);
-        v = a.relb[(long long)(h0 + hh) * (2 * a.maxd + 1) + a.maxd + d];
+      const float* rh = a.relb + (long long)(h0 + hh) * (2 * a.maxd + 1) + a.maxd;
+      float v[2];
+      #pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        v[e] = 0.f;
+        if (j + e < 2 * TP - 1) {
+          int d = j + e - (TP - 1);
+          d = d < -a.maxd ? -a.maxd : (d > a.maxd ? a.maxd : d);
+          v[e] = rh[d];
+        }
       }
-      rb[i] = v;
+      rb2[i] = make_float2(v[0], v[1]);
     }
-    if (tid < hpb) rb[hpb * 2 * TP + tid] = a.gconst[h0 + tid];
+    if (tid < hpb) gcs[tid] = a.gconst[h0 + tid];
   }
   const float sl2 = a.scale * LOG2E;
   for (int hh = 0; hh < hpb; ++hh) {
@@ -2390,8 +2425,8 @@ __global__ __launch_bounds__(64 * NKB, 1) void attention_pipe3_kernel(AttnArgs a
     }
     if (hh + 2 < hpb) issue(hh + 2);
     const char* base = smem + (hh % 3) * SLOT;
-    attn_head_body<BIAS, NKB, RAG, H16>(base, base + KS, base + 2 * KS + qi * 16, qf, rb + hh * 2 * TP,
-                                        BIAS ? rb[hpb * 2 * TP + hh] : 0.f, T, qi, g, koff0, koff1, voffs, sl2, orsrc,
+    attn_head_body<BIAS, NKB, RAG, H16>(base, base + KS, base + 2 * KS + qi * 16, qf, rb2 + hh * 2 * TP,
+                                        BIAS ? gcs[hh] : 0.f, T, qi, g, koff0, koff1, voffs, sl2, orsrc,
                                         (unsigned)((qi * H + h * AT_HD) * 2));
   }
 }
@@ -2413,7 +2448,7 @@ int launch_attention_pipe(const AttnArgs& a, int B, hipStream_t s) {
   double best = 1e30;
   for (int c = 1; c <= a.nh && c <= 12; ++c) {
     if (a.nh % c) continue;
-    const size_t lds = (size_t)IMG + (BIAS ? (size_t)c * (2 * TP + 1) * 4 : 0);
+    const size_t lds = (size_t)IMG + (BIAS ? (size_t)c * (2 * TP * 8 + 4) : 0);
     if (lds > 160 * 1024) continue;
     int& pc = per_cu[dev][c];
     if (!pc) {
@@ -2429,7 +2464,7 @@ int launch_attention_pipe(const AttnArgs& a, int B, hipStream_t s) {
     if (cost < best) best = cost, hpb = c;
   }
   if (best >= 1e30) return -3;
-  const size_t lds = (size_t)IMG + (BIAS ? (size_t)hpb * (2 * TP + 1) * 4 : 0);
+  const size_t lds = (size_t)IMG + (BIAS ? (size_t)hpb * (2 * TP * 8 + 4) : 0);
   hipLaunchKernelGGL(kern, dim3(a.nh / hpb, B), dim3(NT), lds, s, a, hpb);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
