@@ -2105,7 +2105,7 @@ SSE_DEV void attn_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 typedef unsigned int u32x2a __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) const float2 lds_f2;
+typedef __attribute__((address_space(3))) const f32x2 lds_f32x2;
 typedef unsigned int u32x4a __attribute__((ext_vector_type(4)));
 
 // One head of one 16-query block (one wave): S = K Q^T from the LDS images (K fragments first, then the
@@ -2147,8 +2147,8 @@ SSE_DEV void attn_head_body(const char* Ks, const char* Vs, const char* grow, co
       f32x2 v = f32x2{s[kb][2 * hf], s[kb][2 * hf + 1]} * sl2;
       if (BIAS) {
         const int d = key - qi + (TP - 1);
-        const float2 rr = *(const lds_f2*)(size_t)(rl + (unsigned)((kb * 16 + 2 * hf) * 8));   // (bias[d], bias[d + 1])
-        v = __builtin_elementwise_fma(f32x2{gq2, gq2}, f32x2{rr.x, rr.y}, v);
+        const f32x2 rr = *(const lds_f32x2*)(size_t)(rl + (unsigned)((kb * 16 + 2 * hf) * 8));   // (bias[d], bias[d + 1])
+        v = __builtin_elementwise_fma(f32x2{gq2, gq2}, rr, v);
       }
       if (RAG || kb >= NKB - 2) v = f32x2{key < T ? v.x : -INFINITY, key + 1 < T ? v.y : -INFINITY};
       s[kb][2 * hf] = v.x;
