@@ -8,9 +8,9 @@ Tolerances (written here, stated in DESIGN.md §4):
 * MX GEMM: error <= 1e-4 of max|C| against the fp64 product of the dequantised operands (measured
   1.6-2.9e-5: v_mfma_scale_f32_16x16x128_f8f6f4 does not round like an fp32 fma chain over its 128
   products; the bf16 kernels' bar is 1e-5);
-* fp8 encoder embeddings vs the fp32 oracle / the reference's fixture: rel-L2 <= 0.12 and cosine
-  >= 0.99 (e4m3 keeps 3 mantissa bits: ~2^-5 relative error per operand element; the bf16 path's
-  bar is 3e-2).
+* fp8 encoder embeddings vs the fp32 oracle / the reference's fixture: rel-L2 <= 0.08 and cosine
+  >= 0.995 (e4m3 keeps 3 mantissa bits: ~2^-5 relative error per operand element; the bf16 path's
+  bar is 3e-2; round 4 tightened from 0.12 / 0.99 against the observed <= 0.067).
 """
 import os
 
@@ -153,7 +153,7 @@ def test_whisper_fp8_encoder_vs_oracle():
         print(dtype, "rel-L2", _rel(got, ref).max(), "cos", _cos(got, ref).min())
         del m
     assert np.isfinite(res["fp8"]).all()
-    assert _rel(res["fp8"], ref).max() <= 0.12 and _cos(res["fp8"], ref).min() >= 0.99
+    assert _rel(res["fp8"], ref).max() <= 0.08 and _cos(res["fp8"], ref).min() >= 0.995
     # hidden_states[0] (conv front end, bf16 in both) is identical in the two builds
     assert np.array_equal(res["fp8"][:, 3], res["bf16"][:, 3])
     # batch independence: clip 1 alone == clip 1 in the batch
@@ -177,4 +177,4 @@ def test_whisper_large_v2_fp8_vs_reference_fixture():
     got = m.embed(torch.from_numpy(clip).cuda(), idx).cpu().numpy()[0]
     rel, cos = _rel(got, g["emb"][0]).max(), _cos(got, g["emb"][0]).min()
     print("fp8 whisper-large-v2 rel-L2", rel, "cos", cos)
-    assert rel <= 0.12 and cos >= 0.99
+    assert rel <= 0.08 and cos >= 0.995

@@ -10,7 +10,7 @@ Bars (stated here and in DESIGN.md "Parity bars"):
                  cosine 0.9746 on these inputs (profiles/r2_emulate_outlier.json; 7.8e-3 on the
                  benign weights, where the bar stays 3e-2).  The unnormalised conv feature encoder
                  dominates; inputs like these need fp16x3 (observed 2.1e-5);
-  bf16 (Whisper) rel-L2 <= 3e-2, cosine >= 0.999;  MX-fp8 rel-L2 <= 0.12, cosine >= 0.99."""
+  bf16 (Whisper) rel-L2 <= 3e-2, cosine >= 0.999;  MX-fp8 rel-L2 <= 0.08, cosine >= 0.995."""
 import os
 
 import numpy as np
@@ -48,7 +48,7 @@ def test_wavlm_outlier_weights(golden, dtype, tol, cos):
     assert _rel(got, ref).max() <= tol and _cos(got, ref).min() >= cos
 
 
-@pytest.mark.parametrize("dtype,tol,cos", [("fp32", 1e-4, 0.99999), ("bf16", 3e-2, 0.999), ("fp8", 0.12, 0.99)])
+@pytest.mark.parametrize("dtype,tol,cos", [("fp32", 1e-4, 0.99999), ("bf16", 3e-2, 0.999), ("fp8", 0.08, 0.995)])
 def test_whisper_outlier_weights(golden, dtype, tol, cos):
     from ssr_amd import config as C, synth
     from ssr_amd.model import SSEModel

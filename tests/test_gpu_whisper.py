@@ -187,7 +187,7 @@ def test_whisper_large_v2_embed():
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("dtype,B,tol,cos_min", [("bf16", 64, 3e-2, 0.999), ("fp8", 128, 0.12, 0.99)])
+@pytest.mark.parametrize("dtype,B,tol,cos_min", [("bf16", 64, 3e-2, 0.999), ("fp8", 128, 0.08, 0.995)])
 def test_whisper_large_v2_bench_batch(dtype, B, tol, cos_min):
     """The bench shapes themselves (BASELINE configs[2]: bf16 B = 64 x 30 s; configs[4]: fp8
     B = 128 x 30 s): M = B*1500 = 96k / 192k GEMM rows, the flash-attention grid at B*20 heads.
