@@ -2309,7 +2309,12 @@ __global__ __launch_bounds__(64 * NKB, 1) void attention_pipe_kernel(AttnArgs a,
     bf16x8 qf[2];
     qf[0] = *(const bf16x8*)(Qs + koff0);
     qf[1] = *(const bf16x8*)(Qs + koff1);
-    attn_head_body<BIAS, NKB, RAG, H16>(Ks, Vs, base + 3 * KS + qi * 16, qf, rb2 + hh * 2 * TP, BIAS ? gcs[hh] : 0.f, T,
+    // the clip's length re-read per head (opaque): hoisted out of the head loop, the ragged build's 40 key
+    // masks occupied 80 SGPRs across the loop (spills into VGPR lanes, and a miscompare vs the one-head
+    // kernel on ragged batches)
+    int Th = T;
+    if constexpr (RAG) asm volatile("" : "+s"(Th));
+    attn_head_body<BIAS, NKB, RAG, H16>(Ks, Vs, base + 3 * KS + qi * 16, qf, rb2 + hh * 2 * TP, BIAS ? gcs[hh] : 0.f, Th,
                                         qi, g, koff0, koff1, voffs, sl2, orsrc, (unsigned)((qi * H + h * AT_HD) * 2));
   }
 }
@@ -2425,8 +2430,10 @@ __global__ __launch_bounds__(64 * NKB, 1) void attention_pipe3_kernel(AttnArgs a
     }
     if (hh + 2 < hpb) issue(hh + 2);
     const char* base = smem + (hh % 3) * SLOT;
+    int Th = T;   // opaque per head (see attention_pipe_kernel)
+    if constexpr (RAG) asm volatile("" : "+s"(Th));
     attn_head_body<BIAS, NKB, RAG, H16>(base, base + KS, base + 2 * KS + qi * 16, qf, rb2 + hh * 2 * TP,
-                                        BIAS ? gcs[hh] : 0.f, T, qi, g, koff0, koff1, voffs, sl2, orsrc,
+                                        BIAS ? gcs[hh] : 0.f, Th, qi, g, koff0, koff1, voffs, sl2, orsrc,
                                         (unsigned)((qi * H + h * AT_HD) * 2));
   }
 }
