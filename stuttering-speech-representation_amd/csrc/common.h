@@ -273,7 +273,7 @@ enum {
   OPT_ATTN_X3_F32,      // 1: the split-fp16 path's attention on the exact-f32 MFMA (A/B, tests)
   OPT_LN_ROWS_V1,       // 1: 16-bit LayerNorm rows over 512 columns on the one-row-per-wave kernel (A/B, tests)
   OPT_POSCONV_2CL,      // 1: the 16-bit positional conv at 2 clips per block for every shape (A/B, tests)
-  OPT_ATTN_PIPE,        // 1 / 2: short-T attention on the head-pipelined / three-deep kernel (A/B, bit-identity test)
+  OPT_ATTN_SHORT,       // short-T attention: 0 head-pipelined (default), 1 one head at a time, 2 three-deep (A/B, tests)
   OPT_COUNT
 };
 int sse_opt(int id);

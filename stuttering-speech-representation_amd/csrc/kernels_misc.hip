@@ -2319,7 +2319,7 @@ __global__ __launch_bounds__(64 * NKB, 1) void attention_pipe_kernel(AttnArgs a,
   }
 }
 
-// Three-deep form (option attn_pipe = 2): K / V / gate-row images in a 3-slot LDS ring (heads hh + 1 and
+// Three-deep form (option attn_short = 2): K / V / gate-row images in a 3-slot LDS ring (heads hh + 1 and
 // hh + 2 in flight while hh computes: ~2 x 43 KB of loads per CU in flight instead of 63 KB every other
 // head).  Q has one image: each wave stages only its own 16 rows (two 8-row pieces), reads its fragments
 // into registers right after the barrier and then re-issues its rows for the next head -- no other wave
@@ -2478,9 +2478,9 @@ int launch_attention_pipe(const AttnArgs& a, int B, hipStream_t s) {
 
 template <bool BIAS, int NKB, bool RAG, bool H16>
 int launch_attention_short(const AttnArgs& a, int B, hipStream_t s) {
-  const int o = sse_opt(OPT_ATTN_PIPE);
+  const int o = sse_opt(OPT_ATTN_SHORT);   // 0 (default): pipelined; 1: one head at a time; 2: three-deep ring
   if (o == 2) return launch_attention_pipe<BIAS, NKB, RAG, H16, 0, true>(a, B, s);
-  return o ? launch_attention_pipe<BIAS, NKB, RAG, H16>(a, B, s) : launch_attention_full<BIAS, NKB, RAG, H16>(a, B, s);
+  return o == 1 ? launch_attention_full<BIAS, NKB, RAG, H16>(a, B, s) : launch_attention_pipe<BIAS, NKB, RAG, H16>(a, B, s);
 }
 
 template <bool BIAS, bool RAG, bool H16>

@@ -35,7 +35,7 @@ static int g_opt[OPT_COUNT] = {0};
 static const char* const g_opt_name[OPT_COUNT] = {"gemm_cfg", "gemm_nonpersist", "gelu_exact", "conv0_valu",
                                                    "posconv_gemm", "no_lnfold", "gemm_mx_staged", "no_split",
                                                    "logmel_v1", "split_parts", "ln_x3_v1", "attn_x3_f32", "ln_rows_v1", "posconv_2cl",
-                                                   "attn_pipe"};
+                                                   "attn_short"};
 int sse_opt(int id) { return __atomic_load_n(&g_opt[id], __ATOMIC_RELAXED); }
 
 namespace {

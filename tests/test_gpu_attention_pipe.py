@@ -1,5 +1,6 @@
 """The head-pipelined short-T attention kernel (attention_pipe_kernel, kernels_misc.hip; option
-attn_pipe) against the one-head-at-a-time kernel it replaces (attention_full_kernel): per wave the
+attn_short = 0, the default; 2: the three-deep variant) against the one-head-at-a-time kernel it replaced
+(attention_full_kernel, attn_short = 1): per wave the
 same fragments, the same softmax order and the same MFMA chain, so the embeddings must agree bit for
 bit -- at batch sizes that select 1, 3, 6 and 12 heads per block (the double-buffered head loop; mode 2:
 the three-deep ring, at most 6 heads per block),
@@ -25,13 +26,14 @@ def _batch(lens, seed):
 
 def _both(m, w, idx, mode, **kw):
     from ssr_amd import _lib
-    a = m.embed(w, idx, **kw)
-    with _lib.option("attn_pipe", mode):
+    with _lib.option("attn_short", 1):
+        a = m.embed(w, idx, **kw)
+    with _lib.option("attn_short", mode):
         b = m.embed(w, idx, **kw)
     return a, b
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [0, 2])
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])
 @pytest.mark.parametrize("n_clips,samples", [(6, 48000), (48, 48000), (128, 48000), (256, 48000), (5, 16000),
                                              (40, 16000)])
@@ -49,7 +51,7 @@ def test_attention_pipe_bit_identical(wavlm_sd, mode, dtype, n_clips, samples):
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [0, 2])
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])
 def test_attention_pipe_ragged(wavlm_sd, mode, dtype):
     from ssr_amd import config as C
@@ -61,7 +63,7 @@ def test_attention_pipe_ragged(wavlm_sd, mode, dtype):
         assert torch.equal(a, b), lens
         # and each clip still equals its solo call on the pipelined kernel
         from ssr_amd import _lib
-        with _lib.option("attn_pipe", mode):
+        with _lib.option("attn_short", mode):
             for i in (0, 2):
                 one = m.embed(torch.from_numpy(clips[i]).cuda()[None], [12, 6, 0])
                 assert torch.equal(b[i:i + 1], one), (lens, i)

@@ -1,4 +1,4 @@
-// Short-T attention probe: attention_full_kernel vs attention_pipe_kernel (option attn_pipe) on the same
+// Short-T attention probe: attention_full_kernel vs attention_pipe_kernel / _pipe3_kernel (option attn_short) on the same
 // random WavLM-base-shaped q|k|v|gate rows -- bitwise comparison (first mismatches by clip / row / head /
 // column) and event timing of each at the bench's batch sizes.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -mllvm -amdgpu-mfma-vgpr-form \
@@ -12,7 +12,8 @@
 #include <vector>
 
 static int g_pipe = 0;
-int sse_opt(int id) { return id == OPT_ATTN_PIPE ? g_pipe : 0; }
+// g_pipe: 0 full, 1 pipelined, 2 three-deep -> option attn_short 1, 0, 2
+int sse_opt(int id) { return id == OPT_ATTN_SHORT ? (g_pipe == 0 ? 1 : (g_pipe == 1 ? 0 : 2)) : 0; }
 
 #define CK(x)                                                                      \
   do {                                                                             \
