@@ -1670,6 +1670,7 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
 // next tile's global loads are issued into registers before the current tile's MFMAs and
 // written to the other LDS buffer after them — one barrier per tile.
 constexpr int F2_QPW = 32, F2_Q = 128, F2_K = 64;
+constexpr float F2_TH = 8.0f;   // no-bias flash kernel: running-max slack (log2 units) before an O / l rescale
 // V is staged row-major ([key][64 dims], 160-B rows) and read transposed by ds_read_b64_tr_b16:
 // the 8 key rows x 32 B one half-wave touches land on 8 disjoint 8-bank ranges at a 40-dword stride
 constexpr int VR_STRIDE = 160;
@@ -1790,8 +1791,63 @@ __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
     // with the raw v_exp_f32; pairs of scores in packed fp32 (v_pk_mul / v_pk_add); the cross-lane
     // max over the 4 key groups by v_permlane16/32_swap; key masking only in the ragged last tile
     bf16x8 pf[2][2];
+    if constexpr (!BIAS) {
+      // Whisper (no bias): the row max over the RAW scores (scale > 0 commutes with max), the running max
+      // in the scaled log2 domain moved only when a row's max grows past it by more than F2_TH (p then
+      // stays <= 2^F2_TH, exact in the bf16 P and the fp32 sums), and p = 2^fma(s, scale log2 e, -m):
+      // one packed fma per score pair where the scaled form took a multiply and a subtract, and the O / l
+      // rescale only on a real jump
+      #pragma unroll
+      for (int qq = 0; qq < 2; ++qq) {
+        f32x2 s2[8];
+        #pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+          #pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            f32x2 v = f32x2{sc[qq][kb][2 * hh], sc[qq][kb][2 * hh + 1]};
+            if (last) {
+              const int key = kbase + kb * 16 + 4 * g + 2 * hh;
+              v = f32x2{key < T ? v.x : -INFINITY, key + 1 < T ? v.y : -INFINITY};
+            }
+            s2[kb * 2 + hh] = v;
+          }
+        float tmax;
+        {
+          tmax = fmaxf(fmaxf(s2[0].x, s2[0].y), s2[1].x);
+          tmax = fmaxf(fmaxf(tmax, s2[1].y), s2[2].x);
+          #pragma unroll
+          for (int e = 2; e < 8; ++e) tmax = e == 2 ? fmaxf(tmax, s2[2].y) : fmaxf(fmaxf(tmax, s2[e].x), s2[e].y);
+          const auto t16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
+          tmax = fmaxf(__uint_as_float(t16[0]), __uint_as_float(t16[1]));
+          const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
+          tmax = fmaxf(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
+        }
+        const float tm = tmax * sl2;
+        // finite floor: a row with every key so far masked keeps fma(-inf, ., -m) = -inf, never NaN
+        const float m_use = fmaxf(tm > m_run[qq] + F2_TH ? tm : m_run[qq], -1e30f);
+        if (__any(m_use > m_run[qq])) {
+          const float alpha = __builtin_amdgcn_exp2f(m_run[qq] - m_use);
+          l_run[qq] *= f32x2{alpha, alpha};
+          #pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const f32x2 lo = f32x2{o[qq][i][0], o[qq][i][1]} * alpha, hi = f32x2{o[qq][i][2], o[qq][i][3]} * alpha;
+            o[qq][i] = f32x4{lo.x, lo.y, hi.x, hi.y};
+          }
+        }
+        m_run[qq] = m_use;
+        const f32x2 sl = {sl2, sl2}, nm = {-m_use, -m_use};
+        #pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const f32x2 d = __builtin_elementwise_fma(s2[e], sl, nm);
+          const f32x2 pv = {__builtin_amdgcn_exp2f(d.x), __builtin_amdgcn_exp2f(d.y)};
+          l_run[qq] += pv;
+          pf[qq][e >> 2][(e & 3) * 2] = hbits<H16>(pv.x);
+          pf[qq][e >> 2][(e & 3) * 2 + 1] = hbits<H16>(pv.y);
+        }
+      }
+    }
     #pragma unroll
-    for (int qq = 0; qq < 2; ++qq) {
+    for (int qq = 0; qq < (BIAS ? 2 : 0); ++qq) {
       const float gq2 = BIAS ? gate[wave * F2_QPW + qq * 16 + r16] * LOG2E : 0.f;
       f32x2 v2[8];
       #pragma unroll
