@@ -43,7 +43,7 @@ static kfn pick(int dbg) {
   }
 }
 
-struct Shape { const char* name; int M, N, K, act, ep; };
+struct Shape { const char* name; int M, N, K, act, ep; int rps = 0; long long seg = 0, lda = 0; };   // rps > 0: conv addressing
 
 int main() {
   int cus = 256;
@@ -52,7 +52,12 @@ int main() {
       {"qkv", 38144, 2560, 768, ACT_NONE, 1},        {"qkv_fold", 38144, 2560, 768, ACT_NONE, 3},
       {"ffn1", 38144, 3072, 768, ACT_GELU_FAST, 1},  {"ffn1_fold", 38144, 3072, 768, ACT_GELU_FAST, 3},
       {"conv1", 1228544, 512, 1536, ACT_GELU_FAST, 0}, {"k1536", 38144, 2560, 1536, ACT_NONE, 1},
-      {"k3072", 38144, 2560, 3072, ACT_NONE, 1},     {"sq4096", 4096, 4096, 4096, ACT_NONE, 0},
+      {"k3072", 38144, 2560, 3072, ACT_NONE, 1},
+      // conv1 as the library runs it (overlapping k = 3, s = 2 windows over conv0's 256 x 9599 x 512 output:
+      // 2.5 GB of A) and the same GEMM with every row tile reading one L2-resident 256-row window -- the
+      // bound on what a conv0 -> conv1 fusion could save on conv1's side (its A never leaving the chip)
+      {"conv1_real", 1228544, 512, 1536, ACT_GELU_FAST, 0, 4799, 9599LL * 512, 1024},
+      {"conv1_l2", 1228544, 512, 1536, ACT_GELU_FAST, 0, 256, 0, 1024},     {"sq4096", 4096, 4096, 4096, ACT_NONE, 0},
   };
   const long long maxA = 1228544LL * 1536, maxB = 4096LL * 4096, maxC = 1228544LL * 512;
   bf16 *a, *b, *c;
@@ -77,6 +82,7 @@ int main() {
   for (const Shape& s : shapes) {
     GemmArgs g{};
     g.A = a; g.B = b; g.M = s.M; g.N = s.N; g.K = s.K; g.rows_per_seg = s.M; g.lda = s.K;
+    if (s.rps) { g.rows_per_seg = s.rps; g.seg_stride = s.seg; g.lda = s.lda; }
     g.bias = (s.ep & 1) ? bias : nullptr; g.Ct = c; g.ldc = s.N; g.act = s.act; g.zero = zero;
     if (s.ep & 2) { g.apart = apart; g.apart_nt = 3; g.acol = acol; g.ln_eps = 1e-5f; }
     const int n_tiles = ((s.M + 255) / 256) * (s.N / 256);
