@@ -74,7 +74,8 @@ def parse():
                     help="clips streamed from pinned host memory each step (double-buffered H2D on a side stream)")
     ap.add_argument("--logmel", action="store_true",
                     help="the Whisper log-mel front end alone (sse_logmel, K9): B x 30 s clips -> [B, 80, 3000], "
-                         "reported against the HBM roofline (1.92 MB in + 0.96 MB out per clip)")
+                         "reported against the HBM roofline (1.92 MB in + 0.96 MB out per clip) with the STFT "
+                         "kernel's PMC-measured VALU issue / wait fractions (roofline.valu)")
     ap.add_argument("--lib", default=None, help="load this build of libsse.so instead of the in-tree one (A/B)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="sse_set_option A/B kernel switch (repeatable)")
@@ -109,6 +110,8 @@ def cpu_model() -> str:
 
 CALIBRATION = "profiles/r4_cpu_baseline_calibration_wavlm.json"   # 16 clips x 7 alternating rounds
 CALIBRATION_WHISPER = "profiles/r4_cpu_baseline_calibration_whisper.json"   # encoder-only, 8 clips x 5 rounds
+LOGMEL_PMC = "profiles/r4_pmc_sq_logmel_b128.json"            # SQ counters of the log-mel kernels, B = 128
+LOGMEL_TRAFFIC = "profiles/r4_pmc_traffic_logmel_b128.json"    # FETCH / WRITE_SIZE of the same
 
 
 def cpu_baseline(model_name: str, n: int, seconds: float):
@@ -251,14 +254,41 @@ def logmel_run(a, dev):
     # clamp: real traffic = by + 2 x 0.96 MB per clip)
     by = B * (L * 4.0 + 80 * 3000 * 4.0)
     gbs = by / (ms * 1e-3) / 1e9
+    # what actually bounds the STFT kernel: its SQ counters (tools/pmc_kernel.sh, committed file) give the
+    # VALU issue fraction (wave-64 VALU instructions x 2 cycles over 1024 SIMDs x the kernel's cycles per
+    # XCD) and the share of wave cycles spent waiting (s_waitcnt / barriers); HBM traffic from the PMC
+    # traffic file when present
+    valu = None
+    try:
+        with open(os.path.join(ROOT, LOGMEL_PMC)) as fh:
+            pm = json.load(fh)
+        k = next(k for k in pm if "lm_stft_mel" in k)
+        c = {n: v["mean"] for n, v in pm[k].items()}
+        cyc = c["GRBM_GUI_ACTIVE"] / 8.0
+        valu = {"kernel": k.split("(")[0], "valu_insts_per_call": c["SQ_INSTS_VALU"],
+                "valu_issue_frac": round(c["SQ_INSTS_VALU"] * 2.0 / (1024 * cyc), 3),
+                "lds_insts_per_call": c["SQ_INSTS_LDS"],
+                "wait_frac_of_wave_cycles": round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 3),
+                "lds_bank_conflict_cycles": c["SQ_LDS_BANK_CONFLICT"], "source": LOGMEL_PMC,
+                "reading": "neither HBM- nor VALU-bound: latency (LDS round trips between the FFT stages' "
+                           "wave barriers) -- the issue fraction is the headroom a deeper schedule could use"}
+    except (OSError, StopIteration, KeyError, ValueError):
+        pass
+    traffic = None
+    try:
+        with open(os.path.join(ROOT, LOGMEL_TRAFFIC)) as fh:
+            tj = json.load(fh)
+        traffic = sum(v["hbm_bytes_per_launch"] for k, v in tj["kernels"].items() if "lm_" in k)
+    except (OSError, KeyError, ValueError):
+        pass
     res = {"metric": "clips/sec (30 s) Whisper log-mel front end", "value": round(B * a.steps / el, 1), "unit": "clips/s",
            "n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1e3 * el / a.steps, 3),
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
            "data": "synthetic 16 kHz clips (splitmix64 Gaussian+tones)",
            "config": {"workload": f"log-mel of {B} x 30 s clips -> [{B}, 80, 3000] fp32 (sse_logmel)", "global_batch": B},
            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None, "alg_bytes_per_call": by,
-                        "mean_call_ms": round(ms, 4),
+                        "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "alg_bytes_per_call": by,
+                        "mean_call_ms": round(ms, 4), "valu": valu,
                         "note": "fused STFT (LDS FFT) + |X|^2 + mel + log10 per 20-frame block, then the per-clip "
                                 "max clamp; the spectrum never leaves LDS"},
            "finite": bool(torch.isfinite(out).all().item())}
