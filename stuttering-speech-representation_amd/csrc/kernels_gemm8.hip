@@ -51,6 +51,7 @@ constexpr int G8_SMEM_MX = G8_OPS_MX > G8_EPI ? G8_OPS_MX : G8_EPI;
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 // phase k = 4t + p (k >= -8) -> the (tile, half) whose LDS-DMA it issues
 SSE_DEV void g8_target(int k, int& tile, int& half) {
@@ -677,6 +678,19 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
   // (rows q, q^1 of 16 lanes) are exchanged with v_permlane16_swap so every lane holds 8
   // consecutive columns, n = n0 + ni*128 + wn*32 + (q&1)*16 + (q>>1)*8: one 16-B store per
   // (i, ni) instead of two 8-B stores (the per-CU store path is bound by instruction count).
+  // Ct stores go through one buffer resource per 16-row block, based at (row m0 + mi*128 + 16 i, column n0),
+  // num_records ending at row M (the range check sees the VGPR offset only, so the row block rides in the
+  // base, not in the SGPR offset); es = Ct element bytes (2 bf16, 1 MX-fp8)
+  auto ct_rsrc_of = [&](int mi, int i, int es) {
+    const long long r0 = (long long)m0 + mi * 128 + i * 16;
+    const long long rows = (long long)g.M - r0;
+    const long long nrec = rows > 0 ? (rows * g.ldc - n0) * es : 0;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((unsigned char*)g.Ct + (r0 * g.ldc + n0) * es), (short)0,
+                                             (int)min(nrec, (long long)0x7FFFFFF0), 0x00020000);
+  };
+  const unsigned lane_col = (unsigned)(wn * 32 + (q & 1) * 16 + (q >> 1) * 8);
+  const unsigned lane_off2 = (unsigned)(((wm * 64 + r16) * g.ldc + lane_col) * 2);
+  const unsigned lane_off1 = (unsigned)((wm * 64 + r16) * g.ldc + lane_col);
   auto store_half = [&](int mi) {
     #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -697,10 +711,9 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
           const uint2 X = __builtin_bit_cast(uint2, x0), Y = __builtin_bit_cast(uint2, x1);
           const auto s0 = __builtin_amdgcn_permlane16_swap(X.x, Y.x, false, false);
           const auto s1 = __builtin_amdgcn_permlane16_swap(X.y, Y.y, false, false);
-          if (ok) {
-            const uint4 v = make_uint4(s0[0], s1[0], s0[1], s1[1]);
-            *(uint4*)((bf16*)g.Ct + row + n0 + ni * 128 + wn * 32 + (q & 1) * 16 + (q >> 1) * 8) = v;
-          }
+          // the row block's buffer resource (rows >= M out of range): no 64-bit address math, no branch
+          const u32x4 v = {s0[0], s1[0], s0[1], s1[1]};
+          __builtin_amdgcn_raw_buffer_store_b128(v, ct_rsrc_of(mi, i, 2), lane_off2 + (unsigned)(ni * 256), 0u, 0);
         }
       }
     }
@@ -723,8 +736,12 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
         const f32x4 o0 = acc[mi][ni][i][0], o1 = acc[mi][ni][i][1];
         float a = fmaxf(fmaxf(fmaxf(fabsf(o0[0]), fabsf(o0[1])), fmaxf(fabsf(o0[2]), fabsf(o0[3]))),
                         fmaxf(fmaxf(fabsf(o1[0]), fabsf(o1[1])), fmaxf(fabsf(o1[2]), fabsf(o1[3]))));
-        a = fmaxf(a, __shfl_xor(a, 16, 64));
-        a = fmaxf(a, __shfl_xor(a, 32, 64));
+        {   // the row's four q lanes: max over q ^ 1 then q ^ 2 by lane-group swaps (VALU, no LDS round trip)
+          const auto t16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(a), false, false);
+          a = fmaxf(__uint_as_float(t16[0]), __uint_as_float(t16[1]));
+          const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(a), false, false);
+          a = fmaxf(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
+        }
         const int e = mx_scale_exp(a);
         const float inv = mx_inv_scale(e);
         int x0 = __builtin_amdgcn_cvt_pk_fp8_f32(o0[0] * inv, o0[1] * inv, 0, false);
@@ -732,7 +749,7 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
         int x1 = __builtin_amdgcn_cvt_pk_fp8_f32(o1[0] * inv, o1[1] * inv, 0, false);
         x1 = __builtin_amdgcn_cvt_pk_fp8_f32(o1[2] * inv, o1[3] * inv, x1, true);
         const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)x0, (unsigned)x1, false, false);
-        if (ok) *(uint2*)(C8 + row + n0 + ni * 128 + wn * 32 + (q & 1) * 16 + (q >> 1) * 8) = make_uint2(sw[0], sw[1]);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{sw[0], sw[1]}, ct_rsrc_of(mi, i, 1), lane_off1 + (unsigned)(ni * 128), 0u, 0);
         scw[mi][ni] |= (unsigned)e << (8 * i);
       }
     }
