@@ -257,6 +257,12 @@ const char* sse_version(void);
  *   "posconv_gemm"      1 = grouped GEMM for the bf16 positional conv
  *   "no_lnfold"         1 = materialise the post-LN LayerNorm outputs (bf16 WavLM-base)
  *   "gemm_mx_staged"    1 = LDS-staged epilogue for every MX-fp8 GEMM
+ *   "no_split"          1 = WavLM batches run as one stream (no two-stream half-batch split)
+ *   "logmel_v1"         1 = the one-frame-per-wave log-mel kernel
+ *   "split_parts"       3 / 4 = WavLM batches split into that many streams (default 2)
+ *   "ln_x3_v1", "attn_x3_f32", "ln_rows_v1", "posconv_2cl"   earlier kernels kept for A/B and bit-identity tests
+ *   "attn_short"        short-T (<= 160 frames) attention: 0 = head-pipelined (production), 1 = one head
+ *                       at a time, 2 = three-deep ring (all three bit-identical)
  * sse_set_option returns the previous value (>= 0) or SSE_ERR_INVALID for an unknown name. */
 int sse_set_option(const char* name, int value);
 int sse_get_option(const char* name);
