@@ -265,7 +265,7 @@ def logmel_run(a, dev):
         k = next(k for k in pm if "lm_stft_mel" in k)
         c = {n: v["mean"] for n, v in pm[k].items()}
         cyc = c["GRBM_GUI_ACTIVE"] / 8.0
-        valu = {"kernel": k.split("(")[0], "valu_insts_per_call": c["SQ_INSTS_VALU"],
+        valu = {"kernel": k.replace("(anonymous namespace)::", "").split("(")[0], "valu_insts_per_call": c["SQ_INSTS_VALU"],
                 "valu_issue_frac": round(c["SQ_INSTS_VALU"] * 2.0 / (1024 * cyc), 3),
                 "lds_insts_per_call": c["SQ_INSTS_LDS"],
                 "wait_frac_of_wave_cycles": round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 3),
