@@ -228,6 +228,14 @@ template <bool H16> SSE_DEV f32x4 mfma_h(const bf16x8& a, const bf16x8& b, const
   else
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+// 32x32x16 MFMA on bf16 or fp16 operands held in bf16x8 containers
+template <bool H16> SSE_DEV f32x16 mfma32_h(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  if constexpr (H16)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
 // 8 fp32 -> 16 B of bf16 / fp16
 template <bool H16> SSE_DEV uint4 pack_h8(const f32x4& a, const f32x4& b) {
   const uint2 x = pack_h4<H16>(a), y = pack_h4<H16>(b);
@@ -274,6 +282,7 @@ enum {
   OPT_LN_ROWS_V1,       // 1: 16-bit LayerNorm rows over 512 columns on the one-row-per-wave kernel (A/B, tests)
   OPT_POSCONV_2CL,      // 1: the 16-bit positional conv at 2 clips per block for every shape (A/B, tests)
   OPT_ATTN_SHORT,       // short-T attention: 0 head-pipelined (default), 1 one head at a time, 2 three-deep (A/B, tests)
+  OPT_ATTN_LONG,        // no-bias (Whisper) flash attention: 0 32x32 swapped form (default), 1 the 16x16 flash2 kernel
   OPT_COUNT
 };
 int sse_opt(int id);

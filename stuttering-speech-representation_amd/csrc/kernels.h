@@ -80,6 +80,8 @@ struct AttnArgs {
   const int* tlen;       // ragged batch: frames of each clip [B] (T is then the per-clip row stride)
   int min_t;             // flash kernel: clips of at most min_t frames are skipped (ragged batches whose
                          // short clips run on the short-T kernel, exactly as when run alone)
+  int q_log2;            // q carries scale * log2(e) (Whisper bf16 / fp8 encoder): scale = ln 2, and the
+                         // flash3 kernel (which requires it) takes the scores as log2-domain logits
   int out3;              // fp32 kernel: write the output tripled for a split-fp16 GEMM ([hi | lo' | hi],
                          // rows of 3H fp16, x3_split4) instead of fp32 (SSE_DTYPE_FP16X3)
 };

@@ -1927,6 +1927,219 @@ __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
   }
 }
 
+// Whisper flash attention (no bias), round 4: the 32x32x16 MFMA on the swapped product S^T = K Q^T, so a
+// lane holds 16 scores of ONE query (its column) for each 32-key block and the row max / sum need a single
+// v_permlane32_swap (the two half-waves hold the other 16 keys of the same queries), and half as many
+// MFMA instructions as the 16x16x32 form (each holds the SIMD's vector issue for 8 cycles).  The K rows of a
+// 32-key block enter the MFMA permuted (MFMA row r <- key pi(r)) so that the C layout leaves each lane's 16
+// probabilities as exactly the two 8-key B operands of the P.V MFMAs (O^T = V^T P^T): no lane shuffles.
+// Block = 4 waves x 32 queries, 64-key tiles double-buffered in LDS (register staging, flash2's layout and
+// swizzles); the running max moves only past an 8 (log2) slack (flash2's no-bias path), and the row max
+// itself is taken only on tiles whose row sums show a probability past that slack; the subtraction of
+// the running max is a fifth k-step of the S^T MFMA (scores arrive in log2 units: q_log2).  Per tile the
+// vector issue, not the MFMA pipe, is the bound, so the loop is written for VALU count:
+// K / V / Q arrive by buffer loads from a resource covering the clip's T rows (keys past T read as
+// zeros: no predication, no 64-bit address math), the max (when taken) is v_maximum3 on the raw MFMA
+// outputs, and the softmax arithmetic is scalar f32.
+template <bool H16 = false>
+__global__ __launch_bounds__(256, 3) void attention_flash3_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int qc, h, b;
+  attn_block_xcd(qc, h, b);
+  const int TS = a.T, T = a.tlen ? a.tlen[b] : a.T, H = a.H, LQ = a.ldq;
+  if (T <= a.min_t) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = lane & 31, hw = lane >> 5, g16 = lane >> 4, r16 = lane & 15;
+  const int nkt = (T + F2_K - 1) / F2_K;
+  // the clip's T valid rows (the host bounds T * ldq * 2 bytes below 2^31)
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)((const bf16*)a.qkv + (long long)b * TS * LQ), (short)0,
+                                                    T * LQ * 2, 0x00020000);
+  const int qi = qc * F2_Q + wave * 32 + j;   // this lane's query
+  bf16x8 qf[4];
+  {
+    const int qo = (qi * LQ + h * AT_HD + 8 * hw) * 2;
+    #pragma unroll
+    for (int ds = 0; ds < 4; ++ds)
+      qf[ds] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, qo + 32 * ds, 0, 0));
+  }
+  // staging roles (flash2): K and V rows, 2 chunks of 16 B per thread each
+  const int kr0 = tid >> 3, kch = tid & 7;
+  const int kvo = (kr0 * LQ + h * AT_HD + kch * 8 + H) * 2;
+  bf16x8 kreg[2], vreg[2];
+  auto load_tile = [&](int kt) {
+    #pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int o = kvo + (kt * F2_K + 32 * u) * LQ * 2;
+      kreg[u] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
+      vreg[u] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, o + 2 * H, 0, 0));
+    }
+  };
+  auto store_tile = [&](int buf) {
+    char* Ks = smem + buf * F2_BUF;
+    char* Vs = Ks + F2_KS;
+    #pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int kr = kr0 + 32 * u;
+      *(bf16x8*)(Ks + kr * 128 + ((kch ^ ((kr >> 1) & 7)) * 16)) = kreg[u];
+      *(bf16x8*)(Vs + kr * VR_STRIDE + kch * 16) = vreg[u];
+    }
+  };
+  // K row read by this lane for the S^T MFMA of key block kb: key 32 kb + pi(j), pi = the C-layout
+  // permutation (chunk c = j / 4: 16 (c / 4) + 8 (c % 2) + 4 ((c / 2) % 2) + j % 4); 16 B at d = 16 ds + 8 hw
+  const int cq = j >> 2;
+  const int pik = 16 * (cq >> 2) + 8 * (cq & 1) + 4 * ((cq >> 1) & 1) + (j & 3);
+  int koff[2][4];
+  #pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+    const int kr = 32 * kb + pik;
+    #pragma unroll
+    for (int ds = 0; ds < 4; ++ds) koff[kb][ds] = kr * 128 + (((2 * ds + hw) ^ ((kr >> 1) & 7)) * 16);
+  }
+  // V^T operand of the P.V MFMA (dims 32 db + j, keys 32 kb + 16 hh + 8 hw + 0..7): two transpose reads,
+  // this 16-lane group's 4 x 16 block at keys +0..3 / +4..7, lane 4q + p -> row q, dims 4p .. 4p + 3
+  const int voff0 = (8 * hw + (r16 >> 2)) * VR_STRIDE + (16 * (g16 & 1) + 4 * (r16 & 3)) * 2;
+  f32x16 o[2];
+  #pragma unroll
+  for (int e = 0; e < 16; ++e) o[0][e] = o[1][e] = 0.f;
+  // Scores arrive in log2 units (the host folded scale * log2 e into Q: AttnArgs::q_log2), and from the
+  // second tile on the running max is subtracted by the matrix core: a fifth k-step of the S^T MFMA with
+  // A (key side) = 1 at k = 0 and B (query side) = -m at k = 0 adds -m to every score of the query's
+  // column, so p = 2^(MFMA output) with no VALU op between.  m is kept a 16-bit (bf16 / fp16) value so
+  // that it enters the operand exactly.
+  const bf16 h_one = hbits<H16>(1.0f), h_zero = hbits<H16>(0.0f);
+  bf16x8 aext, bext;
+  #pragma unroll
+  for (int e = 0; e < 8; ++e) aext[e] = bext[e] = h_zero;
+  if (hw == 0) aext[0] = h_one;
+  float m_run, l_run = 0.f;
+  const float lmax = 32.f * (1 << (int)F2_TH);
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  // kt == 0 (FIRST): plain S^T, the exact row max sets m; later tiles: see exp_tile below
+  auto tile_step = [&](int kt, auto cur_c, auto first_c, auto last_c) {
+    constexpr bool first = decltype(first_c)::value, last = decltype(last_c)::value;
+    const int cur = cur_c;
+    if (kt + 1 < nkt) load_tile(kt + 1);
+    const char* Ks = smem + cur * F2_BUF;
+    const char* Vs = Ks + F2_KS;
+    const int kbase = kt * F2_K;
+    f32x16 st[2];
+    #pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      #pragma unroll
+      for (int e = 0; e < 16; ++e) st[kb][e] = 0.f;
+      if (!first) st[kb] = mfma32_h<H16>(aext, bext, st[kb]);
+      #pragma unroll
+      for (int ds = 0; ds < 4; ++ds) st[kb] = mfma32_h<H16>(*(const bf16x8*)(Ks + koff[kb][ds]), qf[ds], st[kb]);
+    }
+    // element e of key block kb is key 32 kb + 16 (e / 8) + 8 hw + e % 8, masked past T on the ragged tile
+    if (last) {
+      #pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+        #pragma unroll
+        for (int e = 0; e < 16; ++e)
+          if (kbase + 32 * kb + 16 * (e >> 3) + 8 * hw + (e & 7) >= T) st[kb][e] = -INFINITY;
+    }
+    // the row max over both half-waves (IEEE-754 2019 maximum: v_maximum3_f32 takes MFMA outputs as they
+    // are, where fmaxf's maxnum first canonicalises each operand)
+    auto row_max = [&]() {
+      float ta = __builtin_elementwise_maximum(st[0][0], st[0][1]), tb = __builtin_elementwise_maximum(st[1][0], st[1][1]);
+      #pragma unroll
+      for (int e = 2; e < 16; e += 2) {
+        ta = __builtin_elementwise_maximum(__builtin_elementwise_maximum(ta, st[0][e]), st[0][e + 1]);
+        tb = __builtin_elementwise_maximum(__builtin_elementwise_maximum(tb, st[1][e]), st[1][e + 1]);
+      }
+      const float t = __builtin_elementwise_maximum(ta, tb);
+      const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(t), __float_as_uint(t), false, false);
+      return __builtin_elementwise_maximum(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
+    };
+    bf16x8 pf[2][2];
+    float lt;   // one chain: two would be paired into v_pk_add_f32, slower beside MFMAs than two v_add
+    auto exp_tile = [&](float sub) {
+      lt = 0.f;
+      #pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+        #pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const float p = __builtin_amdgcn_exp2f(st[kb][e] - sub);   // sub = 0 folds away
+          lt += p;
+          pf[kb][e >> 3][e & 7] = hbits<H16>(p);
+        }
+    };
+    if (first) {
+      // key 0 is valid (T >= 1), so the max is finite; m rounded to the operand type
+      m_run = hval<H16>(hbits<H16>(row_max()));
+      bext[0] = hw == 0 ? hbits<H16>(-m_run) : h_zero;
+      exp_tile(m_run);
+    } else {
+      // p = 2^(s - m) against the running max as it stands, with no max taken over this tile: the lane's
+      // row sum shows whether any p passed the slack (sum > 32 * 2^F2_TH).  Only then (any lane of the
+      // wave) the tile's exact row max moves m by flash2's rule, O and l are rescaled and the tile is
+      // exponentiated again.  p <= 2^13 where flash2 bounds it by 2^8: the same fp32 O / l headroom and
+      // bf16 relative precision.
+      exp_tile(0.f);
+      if (__any(!(lt <= lmax))) {
+        const float tmax = row_max();   // relative to m_run
+        const float m_new = tmax > F2_TH ? hval<H16>(hbits<H16>(m_run + tmax)) : m_run;
+        const float delta = m_new - m_run;
+        const float alpha = __builtin_amdgcn_exp2f(-delta);
+        l_run *= alpha;
+        #pragma unroll
+        for (int db = 0; db < 2; ++db)
+          #pragma unroll
+          for (int e = 0; e < 16; ++e) o[db][e] *= alpha;
+        m_run = m_new;
+        bext[0] = hw == 0 ? hbits<H16>(-m_run) : h_zero;
+        exp_tile(delta);
+      }
+    }
+    l_run += lt;
+    #pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+      #pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+        #pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          const char* va = Vs + (32 * kb + 16 * hh) * VR_STRIDE + 32 * db * 2 + voff0;
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)va);
+          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(va + 4 * VR_STRIDE));
+          const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          o[db] = mfma32_h<H16>(vf, pf[kb][hh], o[db]);
+        }
+    if (kt + 1 < nkt) store_tile(cur ^ 1);
+    __syncthreads();
+  };
+  using F = std::integral_constant<bool, false>;
+  using L = std::integral_constant<bool, true>;
+  const int nsteady = nkt - ((T % F2_K) != 0 ? 1 : 0);
+  if (nsteady == 0) {
+    tile_step(0, 0, L{}, L{});
+  } else {
+    tile_step(0, 0, L{}, F{});
+    for (int kt = 1; kt < nsteady; ++kt) tile_step(kt, kt & 1, F{}, F{});
+    if (nsteady < nkt) tile_step(nsteady, nsteady & 1, F{}, L{});
+  }
+  // row sum: this lane's keys + the partner half-wave's
+  {
+    const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_run), __float_as_uint(l_run), false, false);
+    l_run = __uint_as_float(t32[0]) + __uint_as_float(t32[1]);
+  }
+  if (qi < T) {
+    const float inv = 1.0f / l_run;
+    bf16* orow = (bf16*)a.out + ((long long)b * TS + qi) * H + h * AT_HD;
+    // o[db] element e: dim 32 db + 8 (e / 4) + 4 hw + e % 4 -> 4 consecutive dims per (db, e / 4)
+    #pragma unroll
+    for (int db = 0; db < 2; ++db)
+      #pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const f32x4 x = {o[db][4 * c] * inv, o[db][4 * c + 1] * inv, o[db][4 * c + 2] * inv, o[db][4 * c + 3] * inv};
+        *(uint2*)(orow + 32 * db + 8 * c + 4 * hw) = pack_h4<H16>(x);
+      }
+  }
+}
+
 // Short-sequence bf16 attention (T <= 160, WavLM 3 s clips: T = 149): block = (clip, hpb heads),
 // one wave per 16-query block, the whole padded key row (NKB x 16 keys) of one head in LDS.
 // K and V go HBM -> LDS by LDS-DMA (buffer_load ... lds, 16 B per lane, XOR-swizzled 16-B chunks
@@ -2584,8 +2797,10 @@ int launch_attention(const AttnArgs& a, int B, hipStream_t s) {
     dim3 g2((a.T + F2_Q - 1) / F2_Q, a.nh, B);
     if (a.relb)
       hipLaunchKernelGGL((attention_flash2_kernel<true, H>), g2, dim3(256), lds2, s, af);
-    else
+    else if (!a.q_log2 || sse_opt(OPT_ATTN_LONG) == 1 || (long long)a.T * a.ldq * 2 >= (1LL << 31))   // flash3: 32-bit offsets
       hipLaunchKernelGGL((attention_flash2_kernel<false, H>), g2, dim3(256), lds2, s, af);
+    else
+      hipLaunchKernelGGL((attention_flash3_kernel<H>), g2, dim3(256), lds2, s, af);
     return hipGetLastError() == hipSuccess ? 0 : -2;
   }
   if constexpr (!is_f16_v<T>) {   // fp32 (and the bf16 grid's unused tail)

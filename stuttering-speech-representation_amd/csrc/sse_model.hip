@@ -35,7 +35,7 @@ static int g_opt[OPT_COUNT] = {0};
 static const char* const g_opt_name[OPT_COUNT] = {"gemm_cfg", "gemm_nonpersist", "gelu_exact", "conv0_valu",
                                                    "posconv_gemm", "no_lnfold", "gemm_mx_staged", "no_split",
                                                    "logmel_v1", "split_parts", "ln_x3_v1", "attn_x3_f32", "ln_rows_v1", "posconv_2cl",
-                                                   "attn_short"};
+                                                   "attn_short", "attn_long"};
 int sse_opt(int id) { return __atomic_load_n(&g_opt[id], __ATOMIC_RELAXED); }
 
 namespace {
@@ -472,6 +472,9 @@ int build_whisper(sse_model* m, Blob& bl, Arena& ar) {
     m->positions = ar.put_f32(pos, (size_t)c.max_positions * D);
   }
   const float scale = 0.125f;   // head_dim ** -0.5 for head_dim 64: exact power of two
+  // bf16 / fp8 encoder: q also carries log2(e) (still one rounding of sWq to the operand type), so the
+  // flash kernel's scores are log2-domain logits (AttnArgs::q_log2, scale ln 2 for any other consumer)
+  const float qscale = m->bf() ? scale * 1.4426950408889634f : scale;
   for (int l = 0; l < c.layers; ++l) {
     const float *qw = bl.take((size_t)D * D), *qb = bl.take(D), *kw = bl.take((size_t)D * D);
     const float *vw = bl.take((size_t)D * D), *vb = bl.take(D), *ow = bl.take((size_t)D * D), *ob = bl.take(D);
@@ -482,10 +485,10 @@ int build_whisper(sse_model* m, Blob& bl, Arena& ar) {
     if (!qw) continue;
     LayerW L{};
     std::vector<float> qkv((size_t)3 * D * D), qkvb((size_t)3 * D, 0.f);
-    for (size_t i = 0; i < (size_t)D * D; ++i) qkv[i] = qw[i] * scale;   // (xWq + bq) * s == x(sWq) + s bq, s = 2^-3
+    for (size_t i = 0; i < (size_t)D * D; ++i) qkv[i] = qw[i] * qscale;   // (xWq + bq) * s == x(sWq) + s bq
     std::memcpy(qkv.data() + (size_t)D * D, kw, (size_t)D * D * 4);
     std::memcpy(qkv.data() + (size_t)2 * D * D, vw, (size_t)D * D * 4);
-    for (int i = 0; i < D; ++i) qkvb[i] = qb[i] * scale;
+    for (int i = 0; i < D; ++i) qkvb[i] = qb[i] * qscale;
     std::memcpy(qkvb.data() + 2 * D, vb, D * 4);                           // k_proj has no bias
     const bool X3 = m->x3();   // split-fp16 encoder GEMMs (Arena::put_x3), the decoder and convs fp32
     L.qkv_w = X3 ? ar.put_x3(qkv, 3 * D, 1, D) : ar.put_elem(qkv, BF);
@@ -1343,7 +1346,9 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
     }
     GemmArgs g{};
     AttnArgs a{};
-    a.qkv = qkv; a.out = ctx; a.T = Tq; a.H = D; a.nh = nh; a.ldq = m->ldq; a.scale = 1.0f;
+    a.qkv = qkv; a.out = ctx; a.T = Tq; a.H = D; a.nh = nh; a.ldq = m->ldq;
+    a.q_log2 = m->bf();
+    a.scale = a.q_log2 ? 0.6931471805599453f : 1.0f;
     RC(prof(m, s, "attn", 4.0 * B * (double)Tq * Tq * D, (double)B * Tq * 4.0 * D * sizeof(T),
             [&] { return launch_attention<T>(a, B, s); }));
     g = GemmArgs{};

@@ -253,3 +253,36 @@ def test_whisper_small_matches_reference(dtype, tol, cos_min):
         cos = ((got * ref).sum(-1) / (np.linalg.norm(got, axis=-1) * np.linalg.norm(ref, axis=-1))).min()
         print(dtype, "whisper-small", name, "rel-L2", rel, "cos", cos)
         assert rel <= tol and cos >= cos_min, (name, rel, cos)
+
+
+@pytest.mark.parametrize("dtype,tol", [("bf16", 3e-2), ("fp8", 0.08)])
+def test_whisper_flash3_matches_flash2(dtype, tol):
+    """The 32x32 swapped-product flash kernel (attention_flash3_kernel, attn_long = 0, the default for
+    the no-bias Whisper encoder; bf16 operands for the bf16 and MX-fp8 paths) against the 16x16 kernel it
+    replaced (attn_long = 1): the same bf16 probabilities and the same running-max rule, fp32 sums in another order -- so close, not bit-equal.
+    Whisper-small on the reference fixture's clips (T = 1500 keys: 23 full 64-key tiles and the ragged
+    28-key tail) and a batch of 9 (grid rows beyond one block), both at the reference bar."""
+    p = os.path.join(GOLDEN, "whisper_small.npz")
+    if not os.path.exists(p):
+        pytest.skip("whisper-small fixture not generated")
+    from ssr_amd import _lib, config as C, synth
+    from ssr_amd.model import SSEModel
+    g = np.load(p)
+    m = SSEModel(C.WHISPER_SMALL_DEC, synth.synth_whisper_state_dict(C.WHISPER_SMALL_DEC, seed=11), device="cuda:0",
+                 dtype=dtype)
+    idx = [int(i) for i in g["layer_indices"]]
+    w = torch.from_numpy(synth.synth_clips(9, 480000, seed=17)).cuda()
+    for q, c in enumerate(_clips(None, [3.0, 12.0])):
+        w[q] = 0.0
+        w[q, :c.shape[0]] = torch.from_numpy(c)
+    a = m.whisper_embed(w, idx, [])[0]
+    with _lib.option("attn_long", 1):
+        b = m.whisper_embed(w, idx, [])[0]
+    assert torch.isfinite(a).all()
+    d = _rel(a.cpu().numpy(), b.cpu().numpy()).max()
+    print(dtype, "flash3 vs flash2 rel-L2", d)
+    assert d <= 5e-3
+    for q in range(2):
+        rel = _rel(a[q].cpu().numpy(), g["emb"][q]).max()
+        print(dtype, "flash3 whisper-small rel-L2", q, rel)
+        assert rel <= tol
