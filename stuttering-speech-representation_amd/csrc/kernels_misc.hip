@@ -2412,39 +2412,47 @@ SSE_DEV void attn_head_body(const char* Ks, const char* Vs, const char* grow, co
   for (int kb = 0; kb < NKB; ++kb)
     #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
+      // scalar f32 (packed f32 VALU issues slower than two scalar ops beside MFMAs; same values)
       const int key = kb * 16 + 4 * g + 2 * hf;
-      f32x2 v = f32x2{s[kb][2 * hf], s[kb][2 * hf + 1]} * sl2;
+      float vx = s[kb][2 * hf] * sl2, vy = s[kb][2 * hf + 1] * sl2;
       if (BIAS) {
-        const int d = key - qi + (TP - 1);
         const f32x2 rr = *(const lds_f32x2*)(size_t)(rl + (unsigned)((kb * 16 + 2 * hf) * 8));   // (bias[d], bias[d + 1])
-        v = __builtin_elementwise_fma(f32x2{gq2, gq2}, rr, v);
+        vx = __builtin_fmaf(gq2, rr.x, vx);
+        vy = __builtin_fmaf(gq2, rr.y, vy);
       }
-      if (RAG || kb >= NKB - 2) v = f32x2{key < T ? v.x : -INFINITY, key + 1 < T ? v.y : -INFINITY};
-      s[kb][2 * hf] = v.x;
-      s[kb][2 * hf + 1] = v.y;
+      if (RAG || kb >= NKB - 2) {
+        vx = key < T ? vx : -INFINITY;
+        vy = key + 1 < T ? vy : -INFINITY;
+      }
+      s[kb][2 * hf] = vx;
+      s[kb][2 * hf + 1] = vy;
     }
-  float mx = fmaxf(s[0][0], s[0][1]);
+  // row max: IEEE-754 2019 maximum (v_maximum3_f32) -- the same value as fmaxf on these finite / -inf
+  // scores, without maxnum's canonicalising v_max in front of every operand
+  float mx = __builtin_elementwise_maximum(s[0][0], s[0][1]);
   #pragma unroll
-  for (int kb = 0; kb < NKB; ++kb) mx = fmaxf(fmaxf(mx, fmaxf(s[kb][0], s[kb][1])), fmaxf(s[kb][2], s[kb][3]));
+  for (int kb = 0; kb < NKB; ++kb) {
+    mx = __builtin_elementwise_maximum(__builtin_elementwise_maximum(mx, s[kb][0]), s[kb][1]);
+    mx = __builtin_elementwise_maximum(__builtin_elementwise_maximum(mx, s[kb][2]), s[kb][3]);
+  }
   {
     const auto t16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-    mx = fmaxf(__uint_as_float(t16[0]), __uint_as_float(t16[1]));
+    mx = __builtin_elementwise_maximum(__uint_as_float(t16[0]), __uint_as_float(t16[1]));
     const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-    mx = fmaxf(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
+    mx = __builtin_elementwise_maximum(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
   }
-  f32x2 l2 = {0.f, 0.f};
-  const f32x2 mm = {-mx, -mx};
+  float lx = 0.f, ly = 0.f;   // the even / odd keys' sums (the order of the packed form this replaced)
   #pragma unroll
   for (int kb = 0; kb < NKB; ++kb)
     #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
-      const f32x2 d = f32x2{s[kb][2 * hf], s[kb][2 * hf + 1]} + mm;
-      const f32x2 p = {__builtin_amdgcn_exp2f(d.x), __builtin_amdgcn_exp2f(d.y)};
-      l2 += p;
-      s[kb][2 * hf] = p.x;
-      s[kb][2 * hf + 1] = p.y;
+      const float px = __builtin_amdgcn_exp2f(s[kb][2 * hf] - mx), py = __builtin_amdgcn_exp2f(s[kb][2 * hf + 1] - mx);
+      lx += px;
+      ly += py;
+      s[kb][2 * hf] = px;
+      s[kb][2 * hf + 1] = py;
     }
-  float l = l2.x + l2.y;
+  float l = lx + ly;
   {
     const auto t16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(l), __float_as_uint(l), false, false);
     l = __uint_as_float(t16[0]) + __uint_as_float(t16[1]);
