@@ -263,8 +263,9 @@ const char* sse_version(void);
  *   "ln_x3_v1", "attn_x3_f32", "ln_rows_v1", "posconv_2cl"   earlier kernels kept for A/B and bit-identity tests
  *   "attn_short"        short-T (<= 160 frames) attention: 0 = head-pipelined (production), 1 = one head
  *                       at a time, 2 = three-deep ring (all three bit-identical)
- *   "attn_long"         Whisper bf16 / fp8 encoder attention: 0 = the 32x32 swapped-product kernel
- *                       (production), 1 = the 16x16 flash kernel (same bar, not bit-identical)
+ *   "attn_long"         Whisper bf16 / fp8 encoder attention: 0 = the 32x32 swapped-product kernel with two
+ *                       32-query blocks per wave (production), 2 = the same with one (identical outputs),
+ *                       1 = the 16x16 flash kernel (same bar, not bit-identical)
  * sse_set_option returns the previous value (>= 0) or SSE_ERR_INVALID for an unknown name. */
 int sse_set_option(const char* name, int value);
 int sse_get_option(const char* name);

@@ -282,7 +282,8 @@ enum {
   OPT_LN_ROWS_V1,       // 1: 16-bit LayerNorm rows over 512 columns on the one-row-per-wave kernel (A/B, tests)
   OPT_POSCONV_2CL,      // 1: the 16-bit positional conv at 2 clips per block for every shape (A/B, tests)
   OPT_ATTN_SHORT,       // short-T attention: 0 head-pipelined (default), 1 one head at a time, 2 three-deep (A/B, tests)
-  OPT_ATTN_LONG,        // no-bias (Whisper) flash attention: 0 32x32 swapped form (default), 1 the 16x16 flash2 kernel
+  OPT_ATTN_LONG,        // no-bias (Whisper) flash attention: 0 32x32 swapped form, 2 query blocks per wave (default);
+                        // 2 the same with one; 1 the 16x16 flash2 kernel
   OPT_COUNT
 };
 int sse_opt(int id);

@@ -1941,8 +1941,10 @@ __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
 // K / V / Q arrive by buffer loads from a resource covering the clip's T rows (keys past T read as
 // zeros: no predication, no 64-bit address math), the max (when taken) is v_maximum3 on the raw MFMA
 // outputs, and the softmax arithmetic is scalar f32.
-template <bool H16 = false>
-__global__ __launch_bounds__(256, 3) void attention_flash3_kernel(AttnArgs a) {
+// QB query blocks of 32 per wave (QB = 2: 64 queries, 256 per block, 2 waves / SIMD): every K fragment and
+// V^T fragment read from LDS feeds QB MFMAs, halving the LDS instructions per query.
+template <bool H16 = false, int QB = 1>
+__global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attention_flash3_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int qc, h, b;
   attn_block_xcd(qc, h, b);
@@ -1955,13 +1957,14 @@ __global__ __launch_bounds__(256, 3) void attention_flash3_kernel(AttnArgs a) {
   // the clip's T valid rows (the host bounds T * ldq * 2 bytes below 2^31)
   const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)((const bf16*)a.qkv + (long long)b * TS * LQ), (short)0,
                                                     T * LQ * 2, 0x00020000);
-  const int qi = qc * F2_Q + wave * 32 + j;   // this lane's query
-  bf16x8 qf[4];
-  {
-    const int qo = (qi * LQ + h * AT_HD + 8 * hw) * 2;
+  const int q0 = qc * (F2_Q * QB) + wave * (32 * QB) + j;   // this lane's query in block qb: q0 + 32 qb
+  bf16x8 qf[QB][4];
+  #pragma unroll
+  for (int qb = 0; qb < QB; ++qb) {
+    const int qo = ((q0 + 32 * qb) * LQ + h * AT_HD + 8 * hw) * 2;
     #pragma unroll
     for (int ds = 0; ds < 4; ++ds)
-      qf[ds] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, qo + 32 * ds, 0, 0));
+      qf[qb][ds] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, qo + 32 * ds, 0, 0));
   }
   // staging roles (flash2): K and V rows, 2 chunks of 16 B per thread each
   const int kr0 = tid >> 3, kch = tid & 7;
@@ -1999,20 +2002,28 @@ __global__ __launch_bounds__(256, 3) void attention_flash3_kernel(AttnArgs a) {
   // V^T operand of the P.V MFMA (dims 32 db + j, keys 32 kb + 16 hh + 8 hw + 0..7): two transpose reads,
   // this 16-lane group's 4 x 16 block at keys +0..3 / +4..7, lane 4q + p -> row q, dims 4p .. 4p + 3
   const int voff0 = (8 * hw + (r16 >> 2)) * VR_STRIDE + (16 * (g16 & 1) + 4 * (r16 & 3)) * 2;
-  f32x16 o[2];
+  f32x16 o[QB][2];
   #pragma unroll
-  for (int e = 0; e < 16; ++e) o[0][e] = o[1][e] = 0.f;
+  for (int qb = 0; qb < QB; ++qb)
+    #pragma unroll
+    for (int e = 0; e < 16; ++e) o[qb][0][e] = o[qb][1][e] = 0.f;
   // Scores arrive in log2 units (the host folded scale * log2 e into Q: AttnArgs::q_log2), and from the
   // second tile on the running max is subtracted by the matrix core: a fifth k-step of the S^T MFMA with
   // A (key side) = 1 at k = 0 and B (query side) = -m at k = 0 adds -m to every score of the query's
   // column, so p = 2^(MFMA output) with no VALU op between.  m is kept a 16-bit (bf16 / fp16) value so
   // that it enters the operand exactly.
   const bf16 h_one = hbits<H16>(1.0f), h_zero = hbits<H16>(0.0f);
-  bf16x8 aext, bext;
+  bf16x8 aext, bext[QB];
   #pragma unroll
-  for (int e = 0; e < 8; ++e) aext[e] = bext[e] = h_zero;
+  for (int e = 0; e < 8; ++e) aext[e] = h_zero;
+  #pragma unroll
+  for (int qb = 0; qb < QB; ++qb)
+    #pragma unroll
+    for (int e = 0; e < 8; ++e) bext[qb][e] = h_zero;
   if (hw == 0) aext[0] = h_one;
-  float m_run, l_run = 0.f;
+  float m_run[QB], l_run[QB];
+  #pragma unroll
+  for (int qb = 0; qb < QB; ++qb) l_run[qb] = 0.f;
   const float lmax = 32.f * (1 << (int)F2_TH);
   load_tile(0);
   store_tile(0);
@@ -2025,77 +2036,89 @@ __global__ __launch_bounds__(256, 3) void attention_flash3_kernel(AttnArgs a) {
     const char* Ks = smem + cur * F2_BUF;
     const char* Vs = Ks + F2_KS;
     const int kbase = kt * F2_K;
-    f32x16 st[2];
+    f32x16 st[QB][2];
     #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
+      bf16x8 kf[4];
       #pragma unroll
-      for (int e = 0; e < 16; ++e) st[kb][e] = 0.f;
-      if (!first) st[kb] = mfma32_h<H16>(aext, bext, st[kb]);
+      for (int ds = 0; ds < 4; ++ds) kf[ds] = *(const bf16x8*)(Ks + koff[kb][ds]);
       #pragma unroll
-      for (int ds = 0; ds < 4; ++ds) st[kb] = mfma32_h<H16>(*(const bf16x8*)(Ks + koff[kb][ds]), qf[ds], st[kb]);
+      for (int qb = 0; qb < QB; ++qb) {
+        #pragma unroll
+        for (int e = 0; e < 16; ++e) st[qb][kb][e] = 0.f;
+        if (!first) st[qb][kb] = mfma32_h<H16>(aext, bext[qb], st[qb][kb]);
+        #pragma unroll
+        for (int ds = 0; ds < 4; ++ds) st[qb][kb] = mfma32_h<H16>(kf[ds], qf[qb][ds], st[qb][kb]);
+      }
     }
     // element e of key block kb is key 32 kb + 16 (e / 8) + 8 hw + e % 8, masked past T on the ragged tile
     if (last) {
       #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+      for (int qb = 0; qb < QB; ++qb)
         #pragma unroll
-        for (int e = 0; e < 16; ++e)
-          if (kbase + 32 * kb + 16 * (e >> 3) + 8 * hw + (e & 7) >= T) st[kb][e] = -INFINITY;
-    }
-    // the row max over both half-waves (IEEE-754 2019 maximum: v_maximum3_f32 takes MFMA outputs as they
-    // are, where fmaxf's maxnum first canonicalises each operand)
-    auto row_max = [&]() {
-      float ta = __builtin_elementwise_maximum(st[0][0], st[0][1]), tb = __builtin_elementwise_maximum(st[1][0], st[1][1]);
-      #pragma unroll
-      for (int e = 2; e < 16; e += 2) {
-        ta = __builtin_elementwise_maximum(__builtin_elementwise_maximum(ta, st[0][e]), st[0][e + 1]);
-        tb = __builtin_elementwise_maximum(__builtin_elementwise_maximum(tb, st[1][e]), st[1][e + 1]);
-      }
-      const float t = __builtin_elementwise_maximum(ta, tb);
-      const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(t), __float_as_uint(t), false, false);
-      return __builtin_elementwise_maximum(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
-    };
-    bf16x8 pf[2][2];
-    float lt;   // one chain: two would be paired into v_pk_add_f32, slower beside MFMAs than two v_add
-    auto exp_tile = [&](float sub) {
-      lt = 0.f;
-      #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-        #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const float p = __builtin_amdgcn_exp2f(st[kb][e] - sub);   // sub = 0 folds away
-          lt += p;
-          pf[kb][e >> 3][e & 7] = hbits<H16>(p);
-        }
-    };
-    if (first) {
-      // key 0 is valid (T >= 1), so the max is finite; m rounded to the operand type
-      m_run = hval<H16>(hbits<H16>(row_max()));
-      bext[0] = hw == 0 ? hbits<H16>(-m_run) : h_zero;
-      exp_tile(m_run);
-    } else {
-      // p = 2^(s - m) against the running max as it stands, with no max taken over this tile: the lane's
-      // row sum shows whether any p passed the slack (sum > 32 * 2^F2_TH).  Only then (any lane of the
-      // wave) the tile's exact row max moves m by flash2's rule, O and l are rescaled and the tile is
-      // exponentiated again.  p <= 2^13 where flash2 bounds it by 2^8: the same fp32 O / l headroom and
-      // bf16 relative precision.
-      exp_tile(0.f);
-      if (__any(!(lt <= lmax))) {
-        const float tmax = row_max();   // relative to m_run
-        const float m_new = tmax > F2_TH ? hval<H16>(hbits<H16>(m_run + tmax)) : m_run;
-        const float delta = m_new - m_run;
-        const float alpha = __builtin_amdgcn_exp2f(-delta);
-        l_run *= alpha;
-        #pragma unroll
-        for (int db = 0; db < 2; ++db)
+        for (int kb = 0; kb < 2; ++kb)
           #pragma unroll
-          for (int e = 0; e < 16; ++e) o[db][e] *= alpha;
-        m_run = m_new;
-        bext[0] = hw == 0 ? hbits<H16>(-m_run) : h_zero;
-        exp_tile(delta);
-      }
+          for (int e = 0; e < 16; ++e)
+            if (kbase + 32 * kb + 16 * (e >> 3) + 8 * hw + (e & 7) >= T) st[qb][kb][e] = -INFINITY;
     }
-    l_run += lt;
+    bf16x8 pf[QB][2][2];
+    #pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+      // the row max over both half-waves (IEEE-754 2019 maximum: v_maximum3_f32 takes MFMA outputs as
+      // they are, where fmaxf's maxnum first canonicalises each operand)
+      auto row_max = [&]() {
+        float ta = __builtin_elementwise_maximum(st[qb][0][0], st[qb][0][1]);
+        float tb = __builtin_elementwise_maximum(st[qb][1][0], st[qb][1][1]);
+        #pragma unroll
+        for (int e = 2; e < 16; e += 2) {
+          ta = __builtin_elementwise_maximum(__builtin_elementwise_maximum(ta, st[qb][0][e]), st[qb][0][e + 1]);
+          tb = __builtin_elementwise_maximum(__builtin_elementwise_maximum(tb, st[qb][1][e]), st[qb][1][e + 1]);
+        }
+        const float t = __builtin_elementwise_maximum(ta, tb);
+        const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(t), __float_as_uint(t), false, false);
+        return __builtin_elementwise_maximum(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
+      };
+      float lt;   // one chain: two would be paired into v_pk_add_f32, slower beside MFMAs than two v_add
+      auto exp_tile = [&](float sub) {
+        lt = 0.f;
+        #pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+          #pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const float p = __builtin_amdgcn_exp2f(st[qb][kb][e] - sub);   // sub = 0 folds away
+            lt += p;
+            pf[qb][kb][e >> 3][e & 7] = hbits<H16>(p);
+          }
+      };
+      if (first) {
+        // key 0 is valid (T >= 1), so the max is finite; m rounded to the operand type
+        m_run[qb] = hval<H16>(hbits<H16>(row_max()));
+        bext[qb][0] = hw == 0 ? hbits<H16>(-m_run[qb]) : h_zero;
+        exp_tile(m_run[qb]);
+      } else {
+        // p = 2^(s - m) against the running max as it stands, with no max taken over this tile: the
+        // lane's row sum shows whether any p passed the slack (sum > 32 * 2^F2_TH).  Only then (any lane
+        // of the wave) the tile's exact row max moves m by flash2's rule, O and l are rescaled and the
+        // tile is exponentiated again.  p <= 2^13 where flash2 bounds it by 2^8: the same fp32 O / l
+        // headroom and bf16 relative precision.
+        exp_tile(0.f);
+        if (__any(!(lt <= lmax))) {
+          const float tmax = row_max();   // relative to m_run
+          const float m_new = tmax > F2_TH ? hval<H16>(hbits<H16>(m_run[qb] + tmax)) : m_run[qb];
+          const float delta = m_new - m_run[qb];
+          const float alpha = __builtin_amdgcn_exp2f(-delta);
+          l_run[qb] *= alpha;
+          #pragma unroll
+          for (int db = 0; db < 2; ++db)
+            #pragma unroll
+            for (int e = 0; e < 16; ++e) o[qb][db][e] *= alpha;
+          m_run[qb] = m_new;
+          bext[qb][0] = hw == 0 ? hbits<H16>(-m_run[qb]) : h_zero;
+          exp_tile(delta);
+        }
+      }
+      l_run[qb] += lt;
+    }
     #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
       #pragma unroll
@@ -2106,7 +2129,8 @@ __global__ __launch_bounds__(256, 3) void attention_flash3_kernel(AttnArgs a) {
           const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)va);
           const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(va + 4 * VR_STRIDE));
           const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          o[db] = mfma32_h<H16>(vf, pf[kb][hh], o[db]);
+          #pragma unroll
+          for (int qb = 0; qb < QB; ++qb) o[qb][db] = mfma32_h<H16>(vf, pf[qb][kb][hh], o[qb][db]);
         }
     if (kt + 1 < nkt) store_tile(cur ^ 1);
     __syncthreads();
@@ -2121,22 +2145,26 @@ __global__ __launch_bounds__(256, 3) void attention_flash3_kernel(AttnArgs a) {
     for (int kt = 1; kt < nsteady; ++kt) tile_step(kt, kt & 1, F{}, F{});
     if (nsteady < nkt) tile_step(nsteady, nsteady & 1, F{}, L{});
   }
-  // row sum: this lane's keys + the partner half-wave's
-  {
-    const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_run), __float_as_uint(l_run), false, false);
-    l_run = __uint_as_float(t32[0]) + __uint_as_float(t32[1]);
-  }
-  if (qi < T) {
-    const float inv = 1.0f / l_run;
-    bf16* orow = (bf16*)a.out + ((long long)b * TS + qi) * H + h * AT_HD;
-    // o[db] element e: dim 32 db + 8 (e / 4) + 4 hw + e % 4 -> 4 consecutive dims per (db, e / 4)
-    #pragma unroll
-    for (int db = 0; db < 2; ++db)
+  #pragma unroll
+  for (int qb = 0; qb < QB; ++qb) {
+    // row sum: this lane's keys + the partner half-wave's
+    float l = l_run[qb];
+    const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(l), __float_as_uint(l), false, false);
+    l = __uint_as_float(t32[0]) + __uint_as_float(t32[1]);
+    const int qi = q0 + 32 * qb;
+    if (qi < T) {
+      const float inv = 1.0f / l;
+      bf16* orow = (bf16*)a.out + ((long long)b * TS + qi) * H + h * AT_HD;
+      // o[db] element e: dim 32 db + 8 (e / 4) + 4 hw + e % 4 -> 4 consecutive dims per (db, e / 4)
       #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const f32x4 x = {o[db][4 * c] * inv, o[db][4 * c + 1] * inv, o[db][4 * c + 2] * inv, o[db][4 * c + 3] * inv};
-        *(uint2*)(orow + 32 * db + 8 * c + 4 * hw) = pack_h4<H16>(x);
-      }
+      for (int db = 0; db < 2; ++db)
+        #pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const f32x4 x = {o[qb][db][4 * c] * inv, o[qb][db][4 * c + 1] * inv, o[qb][db][4 * c + 2] * inv,
+                           o[qb][db][4 * c + 3] * inv};
+          *(uint2*)(orow + 32 * db + 8 * c + 4 * hw) = pack_h4<H16>(x);
+        }
+    }
   }
 }
 
@@ -2808,7 +2836,11 @@ int launch_attention(const AttnArgs& a, int B, hipStream_t s) {
     else if (!a.q_log2 || sse_opt(OPT_ATTN_LONG) == 1 || (long long)a.T * a.ldq * 2 >= (1LL << 31))   // flash3: 32-bit offsets
       hipLaunchKernelGGL((attention_flash2_kernel<false, H>), g2, dim3(256), lds2, s, af);
     else
-      hipLaunchKernelGGL((attention_flash3_kernel<H>), g2, dim3(256), lds2, s, af);
+      if (sse_opt(OPT_ATTN_LONG) == 2)
+        hipLaunchKernelGGL((attention_flash3_kernel<H, 1>), g2, dim3(256), lds2, s, af);
+      else
+        hipLaunchKernelGGL((attention_flash3_kernel<H, 2>), dim3((a.T + 2 * F2_Q - 1) / (2 * F2_Q), a.nh, B), dim3(256),
+                           lds2, s, af);
     return hipGetLastError() == hipSuccess ? 0 : -2;
   }
   if constexpr (!is_f16_v<T>) {   // fp32 (and the bf16 grid's unused tail)
