@@ -215,6 +215,14 @@ int sse_profile_stop(sse_model* m);
 int sse_gemm(int dtype, const void* d_a, const void* d_b, const float* d_bias, const float* d_resid, float* d_cf,
              void* d_ct, int M, int N, int K, int act, const void* d_zero, void* stream);
 
+/* The Whisper (no-bias) flash attention of the bf16 / fp8 encoder (test hook): d_out bf16 [B*T][H] =
+ * softmax(scale * q k^T) v per head (nh heads of 64), q | k | v the bf16 rows of d_qkv [B*T][ldq]
+ * (q at column 0, k at H, v at 2H).  q_log2 = 1: q already carries scale' * log2(e) and scale is ln 2
+ * (the encoder's layout; the 32x32 kernel, option attn_long picks the variant); q_log2 = 0: any scale,
+ * the 16x16 kernel.  REF/whisper_embeddings_large.py:250 -> HF WhisperAttention (SDPA). */
+int sse_attention(const void* d_qkv, void* d_out, int B, int T, int H, int nh, int ldq, float scale, int q_log2,
+                  void* stream);
+
 /* The folded-LayerNorm GEMM of the bf16 post-LN path (test hook): d_ct bf16 [M][N] =
  * act(rstd_m * (A B^T)[m][n] + bias[n] - rstd_m mean_m acol[n]), (mean_m, rstd_m) combined from the
  * per-256-column partials d_apart [M][3] (float2 (mean, M2)) with eps; K = 768 (three column tiles),

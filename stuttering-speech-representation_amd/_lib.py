@@ -32,7 +32,8 @@ EXPORTED = ("sse_weight_floats", "sse_model_create", "sse_model_destroy", "sse_o
             "sse_whisper_decoder_hidden_states", "sse_mono", "sse_resample_length", "sse_resample_workspace_bytes",
             "sse_resample", "sse_augment", "sse_mx_scale_bytes", "sse_mx_scale_offset", "sse_mx_quantize",
             "sse_mx_quantize_host", "sse_gemm_mx", "sse_pitch_shift_workspace_bytes", "sse_pitch_shift",
-            "sse_set_option", "sse_get_option", "sse_embed_ragged", "sse_gemm_lnfold", "sse_check_range")
+            "sse_set_option", "sse_get_option", "sse_embed_ragged", "sse_gemm_lnfold", "sse_check_range",
+            "sse_attention")
 
 
 class SSEError(RuntimeError):
@@ -147,6 +148,8 @@ def lib() -> ctypes.CDLL:
     L.sse_profile_stop.restype = i32
     L.sse_gemm.argtypes = [i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, vp]
     L.sse_gemm.restype = i32
+    L.sse_attention.argtypes = [vp, vp, i32, i32, i32, i32, i32, ctypes.c_float, i32, vp]
+    L.sse_attention.restype = i32
     L.sse_gemm_lnfold.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, ctypes.c_float, vp, vp]
     L.sse_gemm_lnfold.restype = i32
     L.sse_whisper_embed.argtypes = [vp, vp, i32, i32, vp, i32, vp, vp, i32, vp, vp, sz, vp]

@@ -1943,6 +1943,14 @@ int sse_mono(const float* d_in, int B, int C, int L, float* d_out, void* stream)
   return rc == -1 ? SSE_ERR_INVALID : (rc ? SSE_ERR_HIP : SSE_OK);
 }
 
+int sse_attention(const void* d_qkv, void* d_out, int B, int T, int H, int nh, int ldq, float scale, int q_log2,
+                  void* stream) {
+  if (!d_qkv || !d_out || B <= 0 || T <= 0 || nh <= 0 || H != nh * 64 || ldq < 3 * H || ldq % 8) return SSE_ERR_INVALID;
+  AttnArgs a{};
+  a.qkv = d_qkv; a.out = d_out; a.T = T; a.H = H; a.nh = nh; a.ldq = ldq; a.scale = scale; a.q_log2 = q_log2 ? 1 : 0;
+  return launch_attention<bf16>(a, B, (hipStream_t)stream) ? SSE_ERR_HIP : SSE_OK;
+}
+
 int sse_gemm(int dtype, const void* d_a, const void* d_b, const float* d_bias, const float* d_resid, float* d_cf,
              void* d_ct, int M, int N, int K, int act, const void* d_zero, void* stream) {
   if (!d_a || !d_b || !d_zero || M <= 0 || N <= 0 || K <= 0 || (!d_cf && !d_ct)) return SSE_ERR_INVALID;
