@@ -2010,8 +2010,10 @@ __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attention_flash3_kernel(
   // Scores arrive in log2 units (the host folded scale * log2 e into Q: AttnArgs::q_log2), and from the
   // second tile on the running max is subtracted by the matrix core: a fifth k-step of the S^T MFMA with
   // A (key side) = 1 at k = 0 and B (query side) = -m at k = 0 adds -m to every score of the query's
-  // column, so p = 2^(MFMA output) with no VALU op between.  m is kept a 16-bit (bf16 / fp16) value so
-  // that it enters the operand exactly.
+  // column, so p = 2^(MFMA output) with no VALU op between.  -m enters as three 16-bit terms (k = 0, 1,
+  // 2: hi + mid + lo carry all 24 bits of the fp32 value), so m is the exact row max: the dominant key's p
+  // is exactly 1, the same in the bf16 P of O and in the fp32 l (a 16-bit m would put up to 2^-9 between
+  // the numerator's and the denominator's weight of that key).
   const bf16 h_one = hbits<H16>(1.0f), h_zero = hbits<H16>(0.0f);
   bf16x8 aext, bext[QB];
   #pragma unroll
@@ -2020,7 +2022,17 @@ __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attention_flash3_kernel(
   for (int qb = 0; qb < QB; ++qb)
     #pragma unroll
     for (int e = 0; e < 8; ++e) bext[qb][e] = h_zero;
-  if (hw == 0) aext[0] = h_one;
+  if (hw == 0) aext[0] = aext[1] = aext[2] = h_one;
+  auto set_bext = [&](int qb, float m) {
+    const float nm = -m;
+    const bf16 t0 = hbits<H16>(nm);
+    const float r1 = nm - hval<H16>(t0);
+    const bf16 t1 = hbits<H16>(r1);
+    const bf16 t2 = hbits<H16>(r1 - hval<H16>(t1));
+    bext[qb][0] = hw == 0 ? t0 : h_zero;
+    bext[qb][1] = hw == 0 ? t1 : h_zero;
+    bext[qb][2] = hw == 0 ? t2 : h_zero;
+  };
   float m_run[QB], l_run[QB];
   #pragma unroll
   for (int qb = 0; qb < QB; ++qb) l_run[qb] = 0.f;
@@ -2091,9 +2103,9 @@ __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attention_flash3_kernel(
           }
       };
       if (first) {
-        // key 0 is valid (T >= 1), so the max is finite; m rounded to the operand type
-        m_run[qb] = hval<H16>(hbits<H16>(row_max()));
-        bext[qb][0] = hw == 0 ? hbits<H16>(-m_run[qb]) : h_zero;
+        // key 0 is valid (T >= 1), so the max is finite
+        m_run[qb] = row_max();
+        set_bext(qb, m_run[qb]);
         exp_tile(m_run[qb]);
       } else {
         // p = 2^(s - m) against the running max as it stands, with no max taken over this tile: the
@@ -2104,7 +2116,7 @@ __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attention_flash3_kernel(
         exp_tile(0.f);
         if (__any(!(lt <= lmax))) {
           const float tmax = row_max();   // relative to m_run
-          const float m_new = tmax > F2_TH ? hval<H16>(hbits<H16>(m_run[qb] + tmax)) : m_run[qb];
+          const float m_new = tmax > F2_TH ? m_run[qb] + tmax : m_run[qb];
           const float delta = m_new - m_run[qb];
           const float alpha = __builtin_amdgcn_exp2f(-delta);
           l_run[qb] *= alpha;
@@ -2113,7 +2125,7 @@ __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attention_flash3_kernel(
             #pragma unroll
             for (int e = 0; e < 16; ++e) o[qb][db][e] *= alpha;
           m_run[qb] = m_new;
-          bext[qb][0] = hw == 0 ? hbits<H16>(-m_run[qb]) : h_zero;
+          set_bext(qb, m_new);
           exp_tile(delta);
         }
       }
