@@ -475,6 +475,9 @@ int build_whisper(sse_model* m, Blob& bl, Arena& ar) {
   // bf16 / fp8 encoder: q also carries log2(e) (still one rounding of sWq to the operand type), so the
   // flash kernel's scores are log2-domain logits (AttnArgs::q_log2, scale ln 2 for any other consumer)
   const float qscale = m->bf() ? scale * 1.4426950408889634f : scale;
+  // bf16 encoder at D = 768 (whisper-small; the folded-LN GEMM epilogue takes three 256-column partials per
+  // row): each pre-LN folded into the GEMM that consumes it, as WavLM-base's post-LN (GemmArgs.apart)
+  const bool wfold = m->dtype == SSE_DTYPE_BF16 && D == 768;
   for (int l = 0; l < c.layers; ++l) {
     const float *qw = bl.take((size_t)D * D), *qb = bl.take(D), *kw = bl.take((size_t)D * D);
     const float *vw = bl.take((size_t)D * D), *vb = bl.take(D), *ow = bl.take((size_t)D * D), *ob = bl.take(D);
@@ -494,6 +497,10 @@ int build_whisper(sse_model* m, Blob& bl, Arena& ar) {
     L.qkv_w = X3 ? ar.put_x3(qkv, 3 * D, 1, D) : ar.put_elem(qkv, BF);
     L.qkv_b = ar.put_f32(qkvb.data(), 3 * D);
     m->ldq = 3 * D;
+    if (wfold) {   // pre-LN folded into QKV (self_attn_layer_norm) and fc1 (final_layer_norm)
+      put_folded(ar, qkv.data(), qkvb.data(), 3 * D, D, l1w, l1b, &L.qkv_wf, &L.qkv_c, &L.qkv_bf, false);
+      put_folded(ar, f1w, f1b, F, D, l2w, l2b, &L.f1_wf, &L.f1_c, &L.f1_bf, false);
+    }
     if (m->mx()) {
       L.qkv_q = ar.put_mx(qkv, 3 * D, D, &L.qkv_s);
       L.f1_q = ar.put_mx(std::vector<float>(f1w, f1w + (size_t)F * D), F, D, &L.f1_s);
@@ -514,6 +521,7 @@ int build_whisper(sse_model* m, Blob& bl, Arena& ar) {
     L.ln2_b = ar.put_f32(l2b, D);
     m->layers.push_back(L);
   }
+  m->ln_fold = wfold;
   const float *elw = bl.take(D), *elb = bl.take(D);
   if (!bl.ok) return SSE_ERR_WEIGHTS;
   if (elw) {
@@ -675,6 +683,7 @@ WavlmWs wavlm_plan(const sse_model* m, int B, int L, Plan& p) {
 
 struct WhisperWs {
   size_t zero, lm, mel, h1, x, xb, qkv, ctx, ff, xf;
+  size_t p1, p2;   // folded pre-LN: per-256-column (mean, M2) partials of the residual stream's rows
   size_t dx, dxb, dv, dq, dctx, dff, dxf;   // decoder rows [B][*]
 };
 
@@ -695,6 +704,11 @@ WhisperWs whisper_plan(const sse_model* m, int B, Plan& p) {
   w.ctx = p.add(M * D * ex);
   w.ff = p.add(M * (size_t)c.ffn * ex);
   w.xf = p.add(M * D * 4);
+  w.p1 = w.p2 = 0;
+  if (m->ln_fold) {
+    w.p1 = p.add(M * (D / 256) * 8);
+    w.p2 = p.add(M * (D / 256) * 8);
+  }
   if (c.decoder_layers > 0) {
     w.dx = p.add((size_t)B * D * 4);
     w.dxb = p.add((size_t)B * D * es);
@@ -1331,17 +1345,30 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
                          (!res && Ct ? (double)M * N * (Cs ? 1.0 + 1.0 / 32 : 2.0) : 0.0);
     return prof(m, s, tag, gflops(g), bytes, [&] { return launch_gemm8_mx(g, s); });
   };
+  // folded pre-LN (bf16 whisper-small): the residual GEMMs (oproj, fc2) also write per-256-column partial
+  // statistics of the rows they store (p1 after the attention, p2 after the FFN), and QKV / fc1 apply their
+  // LayerNorm from those partials through folded weights (rstd (x W'^T - mean acol) + b') -- no LayerNorm
+  // kernel and no normalised copy of the stream, except layer 0's QKV input (the conv stem has no partials)
+  const bool lnfold = sizeof(T) == 2 && !mx && m->ln_fold && !sse_opt(OPT_NO_LNFOLD);
+  const int nt = D / 256;
+  float2* p1 = (float2*)(ws + w.p1);
+  float2* p2 = (float2*)(ws + w.p2);
   for (int l = 0; l < c.layers; ++l) {
     const LayerW& Lw = m->layers[l];
     if (mx) {
       RC(launch_layernorm_mx<R>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, D, eps, xq, xq_s, s));
       RC(mx_gemm("gemm_mx:qkv", xq, xq_s, Lw.qkv_q, Lw.qkv_s, Lw.qkv_b, 3 * D, D, false, qkv, nullptr, ACT_NONE));
     } else {
-      RC((launch_layernorm<R, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, D, eps, ACT_NONE, nullptr,
-                                 xb, s)));
       GemmArgs g{};
       g.A = xb; g.B = m->ptr(Lw.qkv_w); g.M = M; g.N = 3 * D; g.K = D; g.rows_per_seg = M; g.lda = D;
       g.bias = m->ptr<float>(Lw.qkv_b); g.Ct = qkv; g.ldc = 3 * D; g.zero = zero;
+      if (lnfold && l > 0) {
+        g.A = x; g.B = m->ptr(Lw.qkv_wf); g.bias = m->ptr<float>(Lw.qkv_bf); g.acol = m->ptr<float>(Lw.qkv_c);
+        g.apart = p2; g.apart_nt = nt; g.ln_eps = eps;
+      } else {
+        RC((launch_layernorm<R, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, D, eps, ACT_NONE, nullptr,
+                                   xb, s)));
+      }
       RC(prof(m, s, "gemm:qkv", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     }
     GemmArgs g{};
@@ -1354,6 +1381,7 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
     g = GemmArgs{};
     g.A = ctx; g.B = m->ptr(Lw.o_w); g.M = M; g.N = D; g.K = D; g.rows_per_seg = M; g.lda = D;
     g.bias = m->ptr<float>(Lw.o_b); set_resid(g); g.ldc = D; g.zero = zero;
+    if (lnfold) g.opart = p1;
     RC(prof(m, s, "gemm:oproj", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     if (mx) {
       RC(launch_layernorm_mx<R>(x, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, D, eps, xq, xq_s, s));
@@ -1362,15 +1390,21 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
       if (l + 1 < c.layers) RC(sink.emit(l + 1, x));
       continue;
     }
-    RC((launch_layernorm<R, T>(x, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, D, eps, ACT_NONE, nullptr,
-                               xb, s)));
     g = GemmArgs{};
     g.A = xb; g.B = m->ptr(Lw.f1_w); g.M = M; g.N = F; g.K = D; g.rows_per_seg = M; g.lda = D;
     g.bias = m->ptr<float>(Lw.f1_b); g.Ct = ff; g.ldc = F; g.act = gelu_rounded_act<T>(); g.zero = zero;
+    if (lnfold) {
+      g.A = x; g.B = m->ptr(Lw.f1_wf); g.bias = m->ptr<float>(Lw.f1_bf); g.acol = m->ptr<float>(Lw.f1_c);
+      g.apart = p1; g.apart_nt = nt; g.ln_eps = eps;
+    } else {
+      RC((launch_layernorm<R, T>(x, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, D, eps, ACT_NONE, nullptr,
+                                 xb, s)));
+    }
     RC(prof(m, s, "gemm:ffn1", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     g = GemmArgs{};
     g.A = ff; g.B = m->ptr(Lw.f2_w); g.M = M; g.N = D; g.K = F; g.rows_per_seg = M; g.lda = F;
     g.bias = m->ptr<float>(Lw.f2_b); set_resid(g); g.ldc = D; g.zero = zero;
+    if (lnfold) g.opart = p2;
     RC(prof(m, s, "gemm:ffn2", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     if (l + 1 < c.layers) RC(sink.emit(l + 1, x));
   }
