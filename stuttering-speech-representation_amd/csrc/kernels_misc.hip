@@ -347,6 +347,7 @@ constexpr int C0M_C = 512;               // channels of the matrix-core conv0 (c
 // into whole 1 KiB row stores that drain while the next chunk computes (one short-lived block per
 // chunk, or lane-scattered 64-B row pieces, both left the kernel at half the fill bandwidth).
 // Wave w computes channel blocks cb = w, w+4, ..., both 16-frame blocks of the chunk.
+typedef unsigned int u32x4nt __attribute__((ext_vector_type(4)));
 constexpr int C0M_PAD = 16;              // bf16 per tile row of padding: row stride = 8 banks mod 64
 
 template <typename TO>   // bf16 or fp16 output (the products are split-bf16 either way)
@@ -419,7 +420,9 @@ __global__ __launch_bounds__(256) void conv0_mfma_kernel(const float* __restrict
     }
     __syncthreads();
     TO* ob = out + ((long long)b * T0 + t0) * C;
-    for (int r = wv; r < nt; r += 4) *(uint4*)(ob + (long long)r * C + lane * 8) = *(const uint4*)&tile[r][lane * 8];
+    // non-temporal: the 2.5 GB (B = 256) output streams past L2 (conv1 reads it back from HBM either way)
+    for (int r = wv; r < nt; r += 4)
+      __builtin_nontemporal_store(*(const u32x4nt*)&tile[r][lane * 8], (u32x4nt*)(ob + (long long)r * C + lane * 8));
   }
 }
 
