@@ -383,6 +383,7 @@ SSE_DEV float2 ln_part_stats(const float2* __restrict__ part, int nt, long long 
   switch (nt) {
     case 2: return ln_part_stats_n<2>(part, m, eps);
     case 4: return ln_part_stats_n<4>(part, m, eps);
+    case 5: return ln_part_stats_n<5>(part, m, eps);
     default: return ln_part_stats_n<3>(part, m, eps);
   }
 }

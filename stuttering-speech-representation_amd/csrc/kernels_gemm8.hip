@@ -500,7 +500,7 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
           if (g.rstats) st[u] = g.rstats[mc];
           else if (g.rpart) st[u] = ln_part_stats_n<3>(g.rpart, mc, g.ln_eps);
         }
-        if (fold) ast[u] = ln_part_stats_n<3>(g.apart, mc, g.ln_eps);
+        if (fold) ast[u] = ln_part_stats(g.apart, g.apart_nt, mc, g.ln_eps);
       }
       #pragma unroll
       for (int u = 0; u < UNR; ++u) {
@@ -776,7 +776,7 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
 // partials, 6 the bias, 7 acol) BEFORE that tile's prologue, so the epilogue issues no global
 // load at all: it never waits for the next tile's prologue (a global load issued after it could
 // only be waited for behind it: vector-memory ops retire in issue order).
-constexpr int G8P_EP = 2048 + 256 * 3 * 8;   // 8 KiB per slot
+constexpr int G8P_EP = 2048 + 256 * 5 * 8;   // 12 KiB per slot: row partials of up to 5 column tiles (H <= 1280)
 constexpr int G8P_SMEM = G8_OPS + 2 * G8P_EP;
 
 // Direct epilogue of one tile (acc holds C^T blocks, see gemm8_kernel<TR = true>): lane holds
@@ -786,7 +786,8 @@ constexpr int G8P_SMEM = G8_OPS + 2 * G8P_EP;
 //                                                                  is not formed, bit-identical to a plain add)
 // DBG (timing probes only, tools/gemm8_probe.hip; the library launches DBG = 0): 1 = math without the
 // stores (results kept live by an empty asm), 3 = stores of the raw accumulators without the math.
-template <int ACT, bool CT3, bool F16, bool has_bias, bool fold, int DBG = 0>
+// FNT: 256-column tiles per row of the folded LayerNorm's input (apart_nt: 3 for H = 768 .. 5 for 1280)
+template <int ACT, bool CT3, bool F16, bool has_bias, bool fold, int DBG = 0, int FNT = 3>
 SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, int n0, int wm, int wn, int q,
                           int r16, const char* ep) {
   const float alpha = F16 ? g.alpha : 1.f;   // split-fp16: the weights' 2^s undone (exact)
@@ -809,9 +810,17 @@ SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, i
     float2 ast[4];
     #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float2* p = (const float2*)(ep + 2048) + (mi * 128 + wm * 64 + i * 16 + r16) * 3;
-      const float2 v[3] = {p[0], p[1], p[2]};
-      const float2 st = ln_part_combine<3>(v, g.ln_eps);
+      const float2* p = (const float2*)(ep + 2048) + (mi * 128 + wm * 64 + i * 16 + r16) * FNT;
+      float2 st;
+      if constexpr (FNT == 3) {
+        const float2 v[3] = {p[0], p[1], p[2]};
+        st = ln_part_combine<3>(v, g.ln_eps);
+      } else {
+        float2 v[FNT];
+        #pragma unroll
+        for (int t = 0; t < FNT; ++t) v[t] = p[t];
+        st = ln_part_combine<FNT>(v, g.ln_eps);
+      }
       ast[i] = fold ? st : make_float2(0.f, alpha);
     }
     #pragma unroll
@@ -935,7 +944,7 @@ SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, i
 // EP: bit 0 = bias present, bit 1 = folded LayerNorm (apart/acol) -- compile-time, so an absent term
 // costs no epilogue instruction (runtime selects measured +5-6 % on conv1 / ffn1 when removed).
 // DBG (timing probes only): see g8p_epilogue; 2 = no epilogue at all (accumulators kept live).
-template <int ACT, bool CT3 = false, bool F16 = false, int EP = 1, int DBG = 0>
+template <int ACT, bool CT3 = false, bool F16 = false, int EP = 1, int DBG = 0, int FNT = 3>
 __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
   __shared__ __attribute__((aligned(16))) char smem[G8P_SMEM];   // operands | 2 epilogue slots: the ONLY shared object
   const int lane = threadIdx.x & 63;
@@ -996,32 +1005,63 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
                                                0);
     }
   };
-  // epilogue-parameter DMA of tile tl into slot: one 1 KiB piece per wave; absent operands read as
-  // an empty buffer (num_records 0, nothing is fetched; the epilogue ignores the slot bytes)
+  // epilogue-parameter DMA of tile tl into slot: 1 KiB pieces -- the row partials (2 FNT pieces), the bias,
+  // the folded column sums -- wave w issuing pieces w and w + 8 (FNT = 3: one per wave); absent operands read
+  // as an empty buffer (num_records 0, nothing is fetched; the epilogue ignores the slot bytes).  These DMAs
+  // precede the tile's prologue, so the counted waits retire them with it however many a wave issued.
   const void* zb = g.zero;
   auto ep_issue = [&](int tl, int slot) {
     const int m0 = (tl / n_tiles_n) * 256, n0 = (tl % n_tiles_n) * 256;
     char* dst = smem + G8_OPS + slot * G8P_EP;
-    __amdgpu_buffer_rsrc_t r;
-    unsigned soff;
-    int off;
-    if (wave < 6) {
-      r = __builtin_amdgcn_make_buffer_rsrc((void*)(fold ? (const void*)g.apart : zb), (short)0, fold ? M * 24 : 0,
-                                            0x00020000);
-      soff = (unsigned)(m0 * 24 + wave * 1024);
-      off = 2048 + wave * 1024;
-    } else if (wave == 6) {
-      r = __builtin_amdgcn_make_buffer_rsrc((void*)(has_bias ? (const void*)g.bias : zb), (short)0,
-                                            has_bias ? g.N * 4 : 0, 0x00020000);
-      soff = (unsigned)(n0 * 4);
-      off = 0;
-    } else {
-      r = __builtin_amdgcn_make_buffer_rsrc((void*)(fold ? (const void*)g.acol : zb), (short)0, fold ? g.N * 4 : 0,
-                                            0x00020000);
-      soff = (unsigned)(n0 * 4);
-      off = 1024;
+    if constexpr (FNT == 3) {   // one piece per wave: waves 0-5 the partials, 6 the bias, 7 the column sums
+      __amdgpu_buffer_rsrc_t r;
+      unsigned soff;
+      int off;
+      if (wave < 6) {
+        r = __builtin_amdgcn_make_buffer_rsrc((void*)(fold ? (const void*)g.apart : zb), (short)0, fold ? M * 24 : 0,
+                                              0x00020000);
+        soff = (unsigned)(m0 * 24 + wave * 1024);
+        off = 2048 + wave * 1024;
+      } else if (wave == 6) {
+        r = __builtin_amdgcn_make_buffer_rsrc((void*)(has_bias ? (const void*)g.bias : zb), (short)0,
+                                              has_bias ? g.N * 4 : 0, 0x00020000);
+        soff = (unsigned)(n0 * 4);
+        off = 0;
+      } else {
+        r = __builtin_amdgcn_make_buffer_rsrc((void*)(fold ? (const void*)g.acol : zb), (short)0, fold ? g.N * 4 : 0,
+                                              0x00020000);
+        soff = (unsigned)(n0 * 4);
+        off = 1024;
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, LPTR(dst + off), 16, (unsigned)lane * 16u, soff, 0, 0);
+      return;
     }
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, LPTR(dst + off), 16, (unsigned)lane * 16u, soff, 0, 0);
+    constexpr int NP = 2 * FNT + 2;
+    #pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int pc = wave + 8 * k;
+      if (pc >= NP) break;
+      __amdgpu_buffer_rsrc_t r;
+      unsigned soff;
+      int off;
+      if (pc < 2 * FNT) {
+        r = __builtin_amdgcn_make_buffer_rsrc((void*)(fold ? (const void*)g.apart : zb), (short)0,
+                                              fold ? M * FNT * 8 : 0, 0x00020000);
+        soff = (unsigned)(m0 * FNT * 8 + pc * 1024);
+        off = 2048 + pc * 1024;
+      } else if (pc == 2 * FNT) {
+        r = __builtin_amdgcn_make_buffer_rsrc((void*)(has_bias ? (const void*)g.bias : zb), (short)0,
+                                              has_bias ? g.N * 4 : 0, 0x00020000);
+        soff = (unsigned)(n0 * 4);
+        off = 0;
+      } else {
+        r = __builtin_amdgcn_make_buffer_rsrc((void*)(fold ? (const void*)g.acol : zb), (short)0, fold ? g.N * 4 : 0,
+                                              0x00020000);
+        soff = (unsigned)(n0 * 4);
+        off = 1024;
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, LPTR(dst + off), 16, (unsigned)lane * 16u, soff, 0, 0);
+    }
   };
 
   f32x4 acc[2][2][4][2];
@@ -1136,7 +1176,8 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
           #pragma unroll
           for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(acc[a][c][i][0]), "v"(acc[a][c][i][1]));
     } else {
-      g8p_epilogue<ACT, CT3, F16, has_bias, fold, DBG>(g, acc, m0, n0, wm, wn, q, r16, smem + G8_OPS + slot * G8P_EP);
+      g8p_epilogue<ACT, CT3, F16, has_bias, fold, DBG, FNT>(g, acc, m0, n0, wm, wn, q, r16,
+                                                           smem + G8_OPS + slot * G8P_EP);
     }
     if (next < 0) break;
     slot ^= 1;
@@ -1480,8 +1521,11 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
 
 int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
   if (a.M <= 0 || a.N % 256 || a.K % 64 || a.K <= 0) return -3;
-  // folded-LayerNorm partials: rows of 3 column tiles (H = 768); opart tiles = N / 256
-  if ((a.apart && a.apart_nt != 3) || (a.rpart && a.rpart_nt != 3) || (a.opart && a.N != 768)) return -3;
+  // folded-LayerNorm partials: rows of 3..5 column tiles (H = 768 .. 1280; the residual LayerNorm on the
+  // load, rpart, 3 only); opart tiles = N / 256
+  if ((a.apart && (a.apart_nt < 3 || a.apart_nt > 5)) || (a.rpart && a.rpart_nt != 3) ||
+      (a.opart && (a.N < 768 || a.N > 1280)) || (a.apart && !a.bias && a.apart_nt != 3))
+    return -3;
   dim3 grid((unsigned)(((a.M + 255) / 256) * (a.N / 256)));
   // OPT_GEMM_NONPERSIST (tests, A/B): the non-persistent LDS-staged kernel for every shape
   if (a.ct3 && (a.resid || a.resid_t || !a.Ct || !a.f16)) return -3;   // split output: persistent kernel only
@@ -1553,7 +1597,19 @@ int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
         case 0: hipLaunchKernelGGL((gemm8p_kernel<AC, C3, F, 0>), dim3(G), dim3(512), 0, s, a, n_tiles); break;
         case 1: hipLaunchKernelGGL((gemm8p_kernel<AC, C3, F, 1>), dim3(G), dim3(512), 0, s, a, n_tiles); break;
         case 2: hipLaunchKernelGGL((gemm8p_kernel<AC, C3, F, 2>), dim3(G), dim3(512), 0, s, a, n_tiles); break;
-        default: hipLaunchKernelGGL((gemm8p_kernel<AC, C3, F, 3>), dim3(G), dim3(512), 0, s, a, n_tiles); break;
+        default:
+          if constexpr (!F && !C3) {   // bf16 folded LayerNorm: the input's column-tile count
+            if (a.apart_nt == 4) {
+              hipLaunchKernelGGL((gemm8p_kernel<AC, C3, F, 3, 0, 4>), dim3(G), dim3(512), 0, s, a, n_tiles);
+              break;
+            }
+            if (a.apart_nt == 5) {
+              hipLaunchKernelGGL((gemm8p_kernel<AC, C3, F, 3, 0, 5>), dim3(G), dim3(512), 0, s, a, n_tiles);
+              break;
+            }
+          }
+          hipLaunchKernelGGL((gemm8p_kernel<AC, C3, F, 3>), dim3(G), dim3(512), 0, s, a, n_tiles);
+          break;
       }
     };
     using F_ = std::false_type;

@@ -475,9 +475,10 @@ int build_whisper(sse_model* m, Blob& bl, Arena& ar) {
   // bf16 / fp8 encoder: q also carries log2(e) (still one rounding of sWq to the operand type), so the
   // flash kernel's scores are log2-domain logits (AttnArgs::q_log2, scale ln 2 for any other consumer)
   const float qscale = m->bf() ? scale * 1.4426950408889634f : scale;
-  // bf16 encoder at D = 768 (whisper-small; the folded-LN GEMM epilogue takes three 256-column partials per
-  // row): each pre-LN folded into the GEMM that consumes it, as WavLM-base's post-LN (GemmArgs.apart)
-  const bool wfold = m->dtype == SSE_DTYPE_BF16 && D == 768;
+  // bf16 encoder at D = 768 .. 1280 (whisper-small / medium / large: the folded-LN GEMM epilogue takes 3 to 5
+  // 256-column partials per row): each pre-LN folded into the GEMM that consumes it, as WavLM-base's post-LN
+  // (GemmArgs.apart)
+  const bool wfold = m->dtype == SSE_DTYPE_BF16 && D % 256 == 0 && D >= 768 && D <= 1280;
   for (int l = 0; l < c.layers; ++l) {
     const float *qw = bl.take((size_t)D * D), *qb = bl.take(D), *kw = bl.take((size_t)D * D);
     const float *vw = bl.take((size_t)D * D), *vb = bl.take(D), *ow = bl.take((size_t)D * D), *ob = bl.take(D);
@@ -499,7 +500,7 @@ int build_whisper(sse_model* m, Blob& bl, Arena& ar) {
     m->ldq = 3 * D;
     if (wfold) {   // pre-LN folded into QKV (self_attn_layer_norm) and fc1 (final_layer_norm)
       put_folded(ar, qkv.data(), qkvb.data(), 3 * D, D, l1w, l1b, &L.qkv_wf, &L.qkv_c, &L.qkv_bf, false);
-      put_folded(ar, f1w, f1b, F, D, l2w, l2b, &L.f1_wf, &L.f1_c, &L.f1_bf, false);
+      if (D == 768) put_folded(ar, f1w, f1b, F, D, l2w, l2b, &L.f1_wf, &L.f1_c, &L.f1_bf, false);   // see f1fold
     }
     if (m->mx()) {
       L.qkv_q = ar.put_mx(qkv, 3 * D, D, &L.qkv_s);
@@ -1350,6 +1351,9 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
   // LayerNorm from those partials through folded weights (rstd (x W'^T - mean acol) + b') -- no LayerNorm
   // kernel and no normalised copy of the stream, except layer 0's QKV input (the conv stem has no partials)
   const bool lnfold = sizeof(T) == 2 && !mx && m->ln_fold && !sse_opt(OPT_NO_LNFOLD);
+  // fc1's fold only at D = 768: its GELU epilogue with 4-5 partials per row spills (the LayerNorm kernel
+  // plus the plain fc1 are the faster pair there); QKV folds at every D
+  const bool f1fold = lnfold && D == 768;
   const int nt = D / 256;
   float2* p1 = (float2*)(ws + w.p1);
   float2* p2 = (float2*)(ws + w.p2);
@@ -1381,7 +1385,7 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
     g = GemmArgs{};
     g.A = ctx; g.B = m->ptr(Lw.o_w); g.M = M; g.N = D; g.K = D; g.rows_per_seg = M; g.lda = D;
     g.bias = m->ptr<float>(Lw.o_b); set_resid(g); g.ldc = D; g.zero = zero;
-    if (lnfold) g.opart = p1;
+    if (f1fold) g.opart = p1;
     RC(prof(m, s, "gemm:oproj", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     if (mx) {
       RC(launch_layernorm_mx<R>(x, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, D, eps, xq, xq_s, s));
@@ -1393,7 +1397,7 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
     g = GemmArgs{};
     g.A = xb; g.B = m->ptr(Lw.f1_w); g.M = M; g.N = F; g.K = D; g.rows_per_seg = M; g.lda = D;
     g.bias = m->ptr<float>(Lw.f1_b); g.Ct = ff; g.ldc = F; g.act = gelu_rounded_act<T>(); g.zero = zero;
-    if (lnfold) {
+    if (f1fold) {
       g.A = x; g.B = m->ptr(Lw.f1_wf); g.bias = m->ptr<float>(Lw.f1_bf); g.acol = m->ptr<float>(Lw.f1_c);
       g.apart = p1; g.apart_nt = nt; g.ln_eps = eps;
     } else {
