@@ -217,11 +217,42 @@ int sse_gemm(int dtype, const void* d_a, const void* d_b, const float* d_bias, c
 
 /* The Whisper (no-bias) flash attention of the bf16 / fp8 encoder (test hook): d_out bf16 [B*T][H] =
  * softmax(scale * q k^T) v per head (nh heads of 64), q | k | v the bf16 rows of d_qkv [B*T][ldq]
- * (q at column 0, k at H, v at 2H).  q_log2 = 1: q already carries scale' * log2(e) and scale is ln 2
- * (the encoder's layout; the 32x32 kernel, option attn_long picks the variant); q_log2 = 0: any scale,
- * the 16x16 kernel.  REF/whisper_embeddings_large.py:250 -> HF WhisperAttention (SDPA). */
+ * (q at column 0, k at H, v at 2H).  q_log2 = 1: q already carries scale' * log2(e) and scale must be
+ * ln 2 = 0.6931471805599453f (else SSE_ERR_INVALID; the encoder's layout; the 32x32 kernel, option attn_long
+ * picks the variant); q_log2 = 0: any scale, the 16x16 kernel.  REF/whisper_embeddings_large.py:250 -> HF WhisperAttention (SDPA). */
 int sse_attention(const void* d_qkv, void* d_out, int B, int T, int H, int nh, int ldq, float scale, int q_log2,
                   void* stream);
+
+/* Every epilogue form of the path's GEMMs behind one test hook (guard-band and epilogue tests; no
+ * reference counterpart).  C[M][N] = A[M][K] . B[N][K]^T with, by the non-null fields:
+ *   bias[N]; act (0 none, 1 erf-GELU, 2 the bf16 path's GELU);
+ *   apart / acol / apart_nt: the folded LayerNorm of A (rstd_m (acc - mean_m acol[n]) + bias[n], (mean, rstd)
+ *     from apart [M][apart_nt] float2 partials, eps ln_eps);
+ *   resid [M][ldc] fp32, or resid_t [M][ldc] 16-bit (the bf16 / fp16 residual stream), optionally
+ *     LayerNorm'd in the epilogue from rpart [M][3] float2 partials and rln_w / rln_b [N];
+ *   opart [M][N / 256] float2: (mean, M2) of every 256 output columns of each written row;
+ * written to cf (fp32) and / or ct (dtype: bf16, fp16 or fp32) with row stride ldc >= N.  dtype:
+ * SSE_DTYPE_BF16, SSE_DTYPE_FP16 (fp16 operands, 8-phase kernels only) or SSE_DTYPE_F32.  The dispatch is
+ * the model's own (launch_gemm<T>): a shape / field combination no kernel takes returns SSE_ERR_INVALID. */
+typedef struct sse_gemm_desc {
+  int dtype, M, N, K, ldc, act, apart_nt;
+  float ln_eps;
+  const void* a;
+  const void* b;
+  const float* bias;
+  const float* acol;
+  const float* apart;
+  const float* resid;
+  const void* resid_t;
+  const float* rpart;
+  const float* rln_w;
+  const float* rln_b;
+  float* opart;
+  float* cf;
+  void* ct;
+  const void* zero;   /* >= 64 zero bytes of device memory */
+} sse_gemm_desc;
+int sse_gemm_ex(const sse_gemm_desc* d, void* stream);
 
 /* The folded-LayerNorm GEMM of the bf16 post-LN path (test hook): d_ct bf16 [M][N] =
  * act(rstd_m * (A B^T)[m][n] + bias[n] - rstd_m mean_m acol[n]), (mean_m, rstd_m) combined from the
@@ -263,14 +294,14 @@ const char* sse_version(void);
  *   "gelu_exact"        1 = erf-GELU in the bf16 path's epilogues
  *   "conv0_valu"        1 = VALU conv0 + GroupNorm kernel instead of the matrix-core one
  *   "posconv_gemm"      1 = grouped GEMM for the bf16 positional conv
- *   "no_lnfold"         1 = materialise the post-LN LayerNorm outputs (bf16 WavLM-base)
+ *   "no_lnfold"         1 = materialise the LayerNorm outputs (bf16 WavLM-base: per call; bf16 Whisper-small /
+ *                       -large: read at sse_model_create, the folded model holds no plain QKV weights past layer 0)
  *   "gemm_mx_staged"    1 = LDS-staged epilogue for every MX-fp8 GEMM
  *   "no_split"          1 = WavLM batches run as one stream (no two-stream half-batch split)
  *   "logmel_v1"         1 = the one-frame-per-wave log-mel kernel
- *   "split_parts"       3 / 4 = WavLM batches split into that many streams (default 2)
  *   "ln_x3_v1", "attn_x3_f32", "ln_rows_v1", "posconv_2cl"   earlier kernels kept for A/B and bit-identity tests
  *   "attn_short"        short-T (<= 160 frames) attention: 0 = head-pipelined (production), 1 = one head
- *                       at a time, 2 = three-deep ring (all three bit-identical)
+ *                       at a time (bit-identical; the reference of tests/test_gpu_attention_pipe.py)
  *   "attn_long"         Whisper bf16 / fp8 encoder attention: 0 = the 32x32 swapped-product kernel with two
  *                       32-query blocks per wave (production), 2 = the same with one (identical outputs),
  *                       1 = the 16x16 flash kernel (same bar, not bit-identical)

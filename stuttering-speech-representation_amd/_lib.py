@@ -21,6 +21,7 @@ SSE_DTYPE_BF16 = 1
 SSE_DTYPE_FP8 = 2   # bf16 activations + MX-fp8 encoder-layer GEMMs (Whisper)
 SSE_DTYPE_FP16X3 = 3   # fp32 activations, split-fp16 (hi/lo) GEMMs: fp32-class results (WavLM-base)
 SSE_DTYPE_FP16 = 4   # the bf16 path with fp16 activations / weights / MFMA operands (WavLM-base)
+SSE_ERR_INVALID = -1
 SSE_ERR_OOM = -6
 SSE_ERR_RANGE = -7   # an fp16-range call wrote a non-finite value (sse_check_range)
 
@@ -33,7 +34,7 @@ EXPORTED = ("sse_weight_floats", "sse_model_create", "sse_model_destroy", "sse_o
             "sse_resample", "sse_augment", "sse_mx_scale_bytes", "sse_mx_scale_offset", "sse_mx_quantize",
             "sse_mx_quantize_host", "sse_gemm_mx", "sse_pitch_shift_workspace_bytes", "sse_pitch_shift",
             "sse_set_option", "sse_get_option", "sse_embed_ragged", "sse_gemm_lnfold", "sse_check_range",
-            "sse_attention")
+            "sse_attention", "sse_gemm_ex")
 
 
 class SSEError(RuntimeError):
@@ -49,6 +50,14 @@ class SSEOutOfMemoryError(SSEError, MemoryError):
 class SSERangeError(SSEError, OverflowError):
     """An fp16-range dtype (fp16, fp16x3) produced a non-finite output: an activation left the fp16
     range somewhere in the forward (sse_check_range)."""
+
+
+class sse_gemm_desc(ctypes.Structure):
+    """include/sse.h sse_gemm_desc (the sse_gemm_ex test hook)."""
+    _fields_ = [(n, ctypes.c_int32) for n in ("dtype", "M", "N", "K", "ldc", "act", "apart_nt")] + \
+        [("ln_eps", ctypes.c_float)] + \
+        [(n, ctypes.c_void_p) for n in ("a", "b", "bias", "acol", "apart", "resid", "resid_t", "rpart", "rln_w",
+                                         "rln_b", "opart", "cf", "ct", "zero")]
 
 
 class sse_cfg(ctypes.Structure):
@@ -150,6 +159,8 @@ def lib() -> ctypes.CDLL:
     L.sse_gemm.restype = i32
     L.sse_attention.argtypes = [vp, vp, i32, i32, i32, i32, i32, ctypes.c_float, i32, vp]
     L.sse_attention.restype = i32
+    L.sse_gemm_ex.argtypes = [ctypes.POINTER(sse_gemm_desc), vp]
+    L.sse_gemm_ex.restype = i32
     L.sse_gemm_lnfold.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, ctypes.c_float, vp, vp]
     L.sse_gemm_lnfold.restype = i32
     L.sse_whisper_embed.argtypes = [vp, vp, i32, i32, vp, i32, vp, vp, i32, vp, vp, sz, vp]

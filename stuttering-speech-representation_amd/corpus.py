@@ -205,9 +205,7 @@ def extract_corpus(clip_source: Callable[[int, int], object], n_items: int,
             nxt = fetch(i + 1)             # staged (host pack + async copy) while batch i computes
         if res is not None and res.data_ptr() != local[s - start:e - start].data_ptr():
             local[s - start:e - start] = res
-    finish = getattr(embed_fn, "finish", None)
-    if callable(finish):
-        finish()
+    _finish_all(getattr(embed_fn, "finish", None), dist, group, world, rank, start, stop, dev)
     if not dist.is_initialized():
         return local[:n_items]
     full = torch.empty((world * per,) + tuple(out_shape), dtype=torch.float32, device=dev)
@@ -215,6 +213,38 @@ def extract_corpus(clip_source: Callable[[int, int], object], n_items: int,
     if bounds is None:
         return full[:n_items]
     return torch.cat([full[r * per:r * per + bounds[r + 1] - bounds[r]] for r in range(world)])
+
+
+class ShardFinishError(RuntimeError):
+    """Raised on every rank whose own ``finish()`` passed when another rank's failed (extract_corpus)."""
+
+
+def _finish_all(finish, dist, group, world: int, rank: int, start: int, stop: int, dev) -> None:
+    """Run the rank's ``finish()`` (sse_embed_fn: the fp16-range check) and agree on the outcome before the
+    exchange: one all-reduce of a per-rank failure vector, then every rank raises together -- the failing
+    ranks their own error with their shard bounds appended, the others ShardFinishError naming the failing
+    ranks -- instead of one rank raising while the others block in all_gather until the collective times out."""
+    err = None
+    if callable(finish):
+        try:
+            finish()
+        except Exception as e:   # re-raised below, after every rank knows
+            err = e
+    where = f"rank {rank}, shard [{start}, {stop})"
+    if dist.is_initialized() and world > 1:
+        on_dev = dist.get_backend(group) == "nccl"
+        bad = torch.zeros(world, dtype=torch.float32, device=dev if on_dev else "cpu")
+        bad[rank] = 1.0 if err is not None else 0.0
+        dist.all_reduce(bad, group=group)
+        failed = [r for r in range(world) if bad[r].item() > 0]
+    else:
+        failed = [rank] if err is not None else []
+    if err is not None:
+        if err.args and isinstance(err.args[0], str):
+            err.args = (f"{err.args[0]} [{where}]",) + tuple(err.args[1:])
+        raise err
+    if failed:
+        raise ShardFinishError(f"{where}: finish() failed on rank(s) {failed}; no all-gather was issued")
 
 
 def sse_embed_fn(model, layer_indices) -> Callable[..., torch.Tensor]:

@@ -276,12 +276,11 @@ enum {
   OPT_GEMM_MX_STAGED,   // 1: LDS-staged epilogue for every MX-fp8 GEMM
   OPT_NO_SPLIT,         // 1: WavLM batches run as one stream (no two-stream half-batch split)
   OPT_LOGMEL_V1,        // 1: the round-2 log-mel kernel (one frame per wave) instead of 4 frames per wave
-  OPT_SPLIT_PARTS,      // 3 or 4: WavLM batches split into that many streams (default 2)
   OPT_LN_X3_V1,         // 1: the one-row-per-wave split-fp16 LayerNorm (A/B, bit-identity test)
   OPT_ATTN_X3_F32,      // 1: the split-fp16 path's attention on the exact-f32 MFMA (A/B, tests)
   OPT_LN_ROWS_V1,       // 1: 16-bit LayerNorm rows over 512 columns on the one-row-per-wave kernel (A/B, tests)
   OPT_POSCONV_2CL,      // 1: the 16-bit positional conv at 2 clips per block for every shape (A/B, tests)
-  OPT_ATTN_SHORT,       // short-T attention: 0 head-pipelined (default), 1 one head at a time, 2 three-deep (A/B, tests)
+  OPT_ATTN_SHORT,       // short-T attention: 0 head-pipelined (default), 1 one head at a time (bit-identity tests)
   OPT_ATTN_LONG,        // no-bias (Whisper) flash attention: 0 32x32 swapped form, 2 query blocks per wave (default);
                         // 2 the same with one; 1 the 16x16 flash2 kernel
   OPT_COUNT

@@ -839,9 +839,12 @@ SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, i
           }
           acc[mi][ni][i][j] = o;
         }
-      // without the fold: the row block's 8 pairs through one lockstep polynomial (gelu_out2_n: 8
-      // independent chains keep the VALU issuing; one chain at a time is latency-bound with a hazard nop
-      // per dependent packed fma).  The fold's extra live registers make the 8-wide form spill.
+      // the row block's 8 pairs through one lockstep polynomial (gelu_out2_n: 8 independent chains keep the
+      // VALU issuing; one chain at a time is latency-bound with a hazard nop per dependent packed fma), with
+      // or without the fold: since the row statistics are read per half, the folded GELU_FAST kernel
+      // (gemm8p_kernel<ACT_GELU_FAST, false, false, 3, 0, 3>, WavLM-base ffn1) holds 256 VGPRs, 0 spilled
+      // (hipcc -Rpass-analysis=kernel-resource-usage, round 5); FNT = 4 / 5 spill 8 / 15 and are not launched
+      // with GELU (the Whisper-large-v2 fc1 keeps its LayerNorm kernel).
       if constexpr (ACT == ACT_GELU_FAST) {
         f32x2 o2[8];
         #pragma unroll
@@ -1526,6 +1529,9 @@ int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
   if ((a.apart && (a.apart_nt < 3 || a.apart_nt > 5)) || (a.rpart && a.rpart_nt != 3) ||
       (a.opart && (a.N < 768 || a.N > 1280)) || (a.apart && !a.bias && a.apart_nt != 3))
     return -3;
+  // the FNT = 4 / 5 fold kernels are instantiated for the plain bf16 persistent GEMM only: an fp16 or split
+  // fold with 4-5 partials per row would otherwise run the FNT = 3 kernel and read the partials wrongly
+  if (a.apart && a.apart_nt != 3 && (a.h16 || a.f16 || a.ct3)) return -3;
   dim3 grid((unsigned)(((a.M + 255) / 256) * (a.N / 256)));
   // OPT_GEMM_NONPERSIST (tests, A/B): the non-persistent LDS-staged kernel for every shape
   if (a.ct3 && (a.resid || a.resid_t || !a.Ct || !a.f16)) return -3;   // split output: persistent kernel only

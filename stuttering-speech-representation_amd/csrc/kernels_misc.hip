@@ -2423,7 +2423,7 @@ typedef unsigned int u32x4a __attribute__((ext_vector_type(4)));
 // One head of one 16-query block (one wave): S = K Q^T from the LDS images (K fragments first, then the
 // 2 x NKB MFMAs as NKB independent chains), the gated-bias softmax over the whole padded row, O^T = V^T P^T,
 // and the 4 output stores (exactly 4 buffer stores: the pipelined kernels' counted vmcnt relies on it).
-// Shared by attention_pipe_kernel and attention_pipe3_kernel, instruction for instruction the per-query-
+// Used by attention_pipe_kernel, instruction for instruction the per-query-
 // block body of attention_full_kernel (bit-identical results).
 template <bool BIAS, int NKB, bool RAG, bool H16>
 SSE_DEV void attn_head_body(const char* Ks, const char* Vs, const char* grow, const bf16x8 (&qf)[2], const float2* rbp,
@@ -2639,131 +2639,12 @@ __global__ __launch_bounds__(64 * NKB, 1) void attention_pipe_kernel(AttnArgs a,
   }
 }
 
-// Three-deep form (option attn_short = 2): K / V / gate-row images in a 3-slot LDS ring (heads hh + 1 and
-// hh + 2 in flight while hh computes: ~2 x 43 KB of loads per CU in flight instead of 63 KB every other
-// head).  Q has one image: each wave stages only its own 16 rows (two 8-row pieces), reads its fragments
-// into registers right after the barrier and then re-issues its rows for the next head -- no other wave
-// reads them, so no barrier guards the reuse.  LDS (NKB 10): 3 x 43 KB + 20 KB + the bias rows, so at most
-// 6 heads per block.
-template <bool BIAS, int NKB, bool RAG, bool H16 = false>
-__global__ __launch_bounds__(64 * NKB, 1) void attention_pipe3_kernel(AttnArgs a, int hpb) {
-  constexpr int TP = NKB * 16;
-  constexpr int NW = NKB;
-  constexpr int KS = TP * 128;
-  constexpr int NGP = (TP + 63) / 64;
-  constexpr int SLOT = 2 * KS + NGP * 1024;   // K | V | gate rows
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* Qimg = smem + 3 * SLOT;                // [TP][128 B]
-  float2* rb2 = (float2*)(Qimg + KS);          // [hpb][2 * TP] bias pairs, then [hpb] gate constants
-  float* gcs = (float*)(rb2 + hpb * 2 * TP);
-
-  const int h0 = blockIdx.x * hpb, b = blockIdx.y;
-  const int TS = a.T, T = a.tlen ? a.tlen[b] : a.T, H = a.H, H3 = a.ldq;
-  if (T > TP) return;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4, r16 = lane & 15;
-  const bf16* qkv = (const bf16*)a.qkv + (long long)b * TS * H3;
-  const float LOG2E = 1.4426950408889634f;
-  const __amdgpu_buffer_rsrc_t orsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)((bf16*)a.out + (long long)b * TS * H), (short)0, T * H * 2, 0x00020000);
-  const int swk = (r16 >> 1) & 7;
-  const int koff0 = r16 * 128 + ((g ^ swk) << 4), koff1 = r16 * 128 + (((g + 4) ^ swk) << 4);
-  const int rowv = 4 * g + (r16 >> 2), swv = ((rowv >> 1) & 3) << 1;
-  int voffs[4];
-  #pragma unroll
-  for (int db = 0; db < 4; ++db) voffs[db] = rowv * 128 + (((2 * db + ((r16 & 3) >> 1)) ^ swv) << 4) + 8 * (r16 & 1);
-  const u32x4a crs = {(unsigned)(size_t)qkv, (unsigned)((size_t)qkv >> 32) & 0xffffu, (unsigned)(T * H3 * 2), 0x00020000u};
-  const unsigned sbase = (unsigned)(size_t)LPTR(smem);
-  auto dma = [&](unsigned lds, unsigned voff) {
-    asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(crs), "{m0}"(lds) : "memory");
-  };
-  const int nd = 4 + ((BIAS && wave < NGP) ? 1 : 0);   // this wave's K / V / gate DMA per head
-  auto issue = [&](int hh) {
-    const int h = h0 + hh;
-    const unsigned base = sbase + (unsigned)((hh % 3) * SLOT);
-    #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int p = wave + NW * u;
-      const int row = 8 * p + (lane >> 3);
-      const unsigned rbase = (unsigned)(row * H3 * 2);
-      const unsigned kch = (unsigned)(((lane & 7) ^ ((row >> 1) & 7)) << 4);
-      const unsigned vch = (unsigned)(((lane & 7) ^ (((row >> 1) & 3) << 1)) << 4);
-      dma(base + p * 1024, rbase + kch + (unsigned)((H + h * AT_HD) * 2));
-      dma(base + KS + p * 1024, rbase + vch + (unsigned)((2 * H + h * AT_HD) * 2));
-    }
-    if (BIAS && wave < NGP) dma(base + 2 * KS + wave * 1024, (unsigned)((64 * wave + lane) * H3 * 2 + (3 * H + 8 * h) * 2));
-  };
-  // this wave's own Q rows (16 qb .. 16 qb + 15) of head hh, the K image's swizzle
-  const int qb = wave, qi = qb * 16 + r16;
-  auto qissue = [&](int hh) {
-    #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int p = 2 * qb + e;
-      const int row = 8 * p + (lane >> 3);
-      const unsigned kch = (unsigned)(((lane & 7) ^ ((row >> 1) & 7)) << 4);
-      dma(sbase + 3 * SLOT + p * 1024, (unsigned)(row * H3 * 2) + kch + (unsigned)((h0 + hh) * AT_HD * 2));
-    }
-  };
-  qissue(0);
-  issue(0);
-  if (1 < hpb) issue(1);
-  if (BIAS) {
-    // pairs (bias[j], bias[j + 1]) per head, j < 2 TP (bias[j] = 0 for j >= 2 TP - 1)
-    for (int i = tid; i < hpb * 2 * TP; i += 64 * NW) {
-      const int hh = i / (2 * TP), j = i - hh * 2 * TP;
-      const float* rh = a.relb + (long long)(h0 + hh) * (2 * a.maxd + 1) + a.maxd;
-      float v[2];
-      #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        v[e] = 0.f;
-        if (j + e < 2 * TP - 1) {
-          int d = j + e - (TP - 1);
-          d = d < -a.maxd ? -a.maxd : (d > a.maxd ? a.maxd : d);
-          v[e] = rh[d];
-        }
-      }
-      rb2[i] = make_float2(v[0], v[1]);
-    }
-    if (tid < hpb) gcs[tid] = a.gconst[h0 + tid];
-  }
-  const float sl2 = a.scale * LOG2E;
-  for (int hh = 0; hh < hpb; ++hh) {
-    // Q(hh) and slot hh % 3 have landed: younger are only the DMA of head hh + 1 (issued after Q(hh))
-    // and the 4 stores of head hh - 1 (head 0: Q(0) precedes DMA(0), whose younger ops are DMA(1))
-    const int n = hh == 0 ? (1 < hpb ? nd : 0) : ((hh + 1 < hpb ? nd : 0) + 4);
-    switch (n) {
-      case 4: asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory"); break;
-      case 5: asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory"); break;
-      case 8: asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory"); break;
-      case 9: asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)" ::: "memory"); break;
-      default: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); break;
-    }
-    attn_barrier();   // every wave's slot hh % 3 has landed; every wave is done with slot (hh + 2) % 3
-    const int h = h0 + hh;
-    bf16x8 qf[2];
-    qf[0] = *(const bf16x8*)(Qimg + qb * 2048 + koff0);
-    qf[1] = *(const bf16x8*)(Qimg + qb * 2048 + koff1);
-    if (hh + 1 < hpb) {
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(qf[0]), "+v"(qf[1])::"memory");   // own rows read: reuse them
-      qissue(hh + 1);
-    }
-    if (hh + 2 < hpb) issue(hh + 2);
-    const char* base = smem + (hh % 3) * SLOT;
-    int Th = T;   // opaque per head (see attention_pipe_kernel)
-    if constexpr (RAG) asm volatile("" : "+s"(Th));
-    attn_head_body<BIAS, NKB, RAG, H16>(base, base + KS, base + 2 * KS + qi * 16, qf, rb2 + hh * 2 * TP,
-                                        BIAS ? gcs[hh] : 0.f, Th, qi, g, koff0, koff1, voffs, sl2, orsrc,
-                                        (unsigned)((qi * H + h * AT_HD) * 2));
-  }
-}
-
-template <bool BIAS, int NKB, bool RAG, bool H16, int DBG = 0, bool P3 = false>
+template <bool BIAS, int NKB, bool RAG, bool H16, int DBG = 0>
 int launch_attention_pipe(const AttnArgs& a, int B, hipStream_t s) {
   constexpr int TP = NKB * 16;
-  // pipe: 2 x (K | V | Q | gate rows); pipe3: 3 x (K | V | gate rows)
-  constexpr int IMG = P3 ? 3 * (2 * TP * 128 + ((TP + 63) / 64) * 1024) + TP * 128 : 2 * (3 * TP * 128 + ((TP + 63) / 64) * 1024);
-  const auto kern = P3 ? attention_pipe3_kernel<BIAS, NKB, RAG, H16> : attention_pipe_kernel<BIAS, NKB, RAG, H16, DBG>;
+  // 2 x (K | V | Q | gate rows)
+  constexpr int IMG = 2 * (3 * TP * 128 + ((TP + 63) / 64) * 1024);
+  const auto kern = attention_pipe_kernel<BIAS, NKB, RAG, H16, DBG>;
   constexpr int NT = 64 * NKB;
   static int per_cu[64][13] = {{0}}, cus[64] = {0};
   int dev = 0;
@@ -2798,8 +2679,7 @@ int launch_attention_pipe(const AttnArgs& a, int B, hipStream_t s) {
 
 template <bool BIAS, int NKB, bool RAG, bool H16>
 int launch_attention_short(const AttnArgs& a, int B, hipStream_t s) {
-  const int o = sse_opt(OPT_ATTN_SHORT);   // 0 (default): pipelined; 1: one head at a time; 2: three-deep ring
-  if (o == 2) return launch_attention_pipe<BIAS, NKB, RAG, H16, 0, true>(a, B, s);
+  const int o = sse_opt(OPT_ATTN_SHORT);   // 0 (default): pipelined; 1: one head at a time (the bit-identity reference)
   return o == 1 ? launch_attention_full<BIAS, NKB, RAG, H16>(a, B, s) : launch_attention_pipe<BIAS, NKB, RAG, H16>(a, B, s);
 }
 

@@ -34,7 +34,7 @@
 static int g_opt[OPT_COUNT] = {0};
 static const char* const g_opt_name[OPT_COUNT] = {"gemm_cfg", "gemm_nonpersist", "gelu_exact", "conv0_valu",
                                                    "posconv_gemm", "no_lnfold", "gemm_mx_staged", "no_split",
-                                                   "logmel_v1", "split_parts", "ln_x3_v1", "attn_x3_f32", "ln_rows_v1", "posconv_2cl",
+                                                   "logmel_v1", "ln_x3_v1", "attn_x3_f32", "ln_rows_v1", "posconv_2cl",
                                                    "attn_short", "attn_long"};
 int sse_opt(int id) { return __atomic_load_n(&g_opt[id], __ATOMIC_RELAXED); }
 
@@ -475,10 +475,12 @@ int build_whisper(sse_model* m, Blob& bl, Arena& ar) {
   // bf16 / fp8 encoder: q also carries log2(e) (still one rounding of sWq to the operand type), so the
   // flash kernel's scores are log2-domain logits (AttnArgs::q_log2, scale ln 2 for any other consumer)
   const float qscale = m->bf() ? scale * 1.4426950408889634f : scale;
-  // bf16 encoder at D = 768 .. 1280 (whisper-small / medium / large: the folded-LN GEMM epilogue takes 3 to 5
-  // 256-column partials per row): each pre-LN folded into the GEMM that consumes it, as WavLM-base's post-LN
-  // (GemmArgs.apart)
-  const bool wfold = m->dtype == SSE_DTYPE_BF16 && D % 256 == 0 && D >= 768 && D <= 1280;
+  // bf16 encoder at D = 768 (whisper-small) and 1280 (whisper-large: the folded-LN GEMM epilogue takes 3 / 5
+  // 256-column partials per row; D = 1024 has no fixture, so it keeps the LayerNorm kernel): each pre-LN
+  // folded into the GEMM that consumes it, as WavLM-base's post-LN (GemmArgs.apart).  The choice is made
+  // here, at load (option no_lnfold read at sse_model_create): a folded model stores the plain QKV weights
+  // for layer 0 only (its input has no partials) -- 305 MB less for large-v2 than keeping both forms.
+  const bool wfold = m->dtype == SSE_DTYPE_BF16 && (D == 768 || D == 1280) && !sse_opt(OPT_NO_LNFOLD);
   for (int l = 0; l < c.layers; ++l) {
     const float *qw = bl.take((size_t)D * D), *qb = bl.take(D), *kw = bl.take((size_t)D * D);
     const float *vw = bl.take((size_t)D * D), *vb = bl.take(D), *ow = bl.take((size_t)D * D), *ob = bl.take(D);
@@ -495,7 +497,7 @@ int build_whisper(sse_model* m, Blob& bl, Arena& ar) {
     for (int i = 0; i < D; ++i) qkvb[i] = qb[i] * qscale;
     std::memcpy(qkvb.data() + 2 * D, vb, D * 4);                           // k_proj has no bias
     const bool X3 = m->x3();   // split-fp16 encoder GEMMs (Arena::put_x3), the decoder and convs fp32
-    L.qkv_w = X3 ? ar.put_x3(qkv, 3 * D, 1, D) : ar.put_elem(qkv, BF);
+    if (!wfold || l == 0) L.qkv_w = X3 ? ar.put_x3(qkv, 3 * D, 1, D) : ar.put_elem(qkv, BF);
     L.qkv_b = ar.put_f32(qkvb.data(), 3 * D);
     m->ldq = 3 * D;
     if (wfold) {   // pre-LN folded into QKV (self_attn_layer_norm) and fc1 (final_layer_norm)
@@ -1350,7 +1352,7 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
   // statistics of the rows they store (p1 after the attention, p2 after the FFN), and QKV / fc1 apply their
   // LayerNorm from those partials through folded weights (rstd (x W'^T - mean acol) + b') -- no LayerNorm
   // kernel and no normalised copy of the stream, except layer 0's QKV input (the conv stem has no partials)
-  const bool lnfold = sizeof(T) == 2 && !mx && m->ln_fold && !sse_opt(OPT_NO_LNFOLD);
+  const bool lnfold = sizeof(T) == 2 && !mx && m->ln_fold;   // fixed at load (build_whisper: wfold)
   // fc1's fold only at D = 768: its GELU epilogue with 4-5 partials per row spills (the LayerNorm kernel
   // plus the plain fc1 are the faster pair there); QKV folds at every D
   const bool f1fold = lnfold && D == 768;
@@ -1514,13 +1516,8 @@ int whisper_forward_x3(sse_model* m, const float* wave, int B, int L, const Sink
 // single-stream call (every clip's result is independent of the batch it is in).  Not for hidden-state
 // calls, Whisper (1500-frame clips already give full rounds) or when OPT_NO_SPLIT is set.
 constexpr int SPLIT_MIN = 128;
-// parts of a split call: 2 (sse_set_option "split_parts" 3 or 4 for A/B runs), at least 64 clips each
-int split_parts(int B) {
-  const int o = sse_opt(OPT_SPLIT_PARTS);
-  int P = o >= 2 && o <= sse_model::MAX_PARTS ? o : 2;
-  while (P > 2 && B / P < 64) --P;
-  return P;
-}
+// parts of a split call: 2 (three or four streams measured slower in rounds 3 and 4)
+int split_parts(int) { return 2; }
 bool split_applies(const sse_model* m, int B, const Sink* sink) {
   return m->cfg.kind == SSE_KIND_WAVLM && B >= SPLIT_MIN && !sse_opt(OPT_NO_SPLIT) && (!sink || !sink->hs);
 }
@@ -1984,6 +1981,9 @@ int sse_mono(const float* d_in, int B, int C, int L, float* d_out, void* stream)
 int sse_attention(const void* d_qkv, void* d_out, int B, int T, int H, int nh, int ldq, float scale, int q_log2,
                   void* stream) {
   if (!d_qkv || !d_out || B <= 0 || T <= 0 || nh <= 0 || H != nh * 64 || ldq < 3 * H || ldq % 8) return SSE_ERR_INVALID;
+  // q_log2: the scores are already log2-domain logits, which every kernel reads as scale = ln 2; any other
+  // scale would be honoured by the short-T kernels (T <= 160) and ignored by the 32x32 flash kernel
+  if (q_log2 && scale != 0.6931471805599453f) return SSE_ERR_INVALID;
   AttnArgs a{};
   a.qkv = d_qkv; a.out = d_out; a.T = T; a.H = H; a.nh = nh; a.ldq = ldq; a.scale = scale; a.q_log2 = q_log2 ? 1 : 0;
   return launch_attention<bf16>(a, B, (hipStream_t)stream) ? SSE_ERR_HIP : SSE_OK;
@@ -1997,6 +1997,27 @@ int sse_gemm(int dtype, const void* d_a, const void* d_b, const float* d_bias, c
   g.bias = d_bias; g.resid = d_resid; g.Cf = d_cf; g.Ct = d_ct; g.ldc = N; g.act = act; g.zero = d_zero;
   return dtype == SSE_DTYPE_BF16 ? launch_gemm_bf16(g, AMODE_SEG, 1, (hipStream_t)stream)
                                  : launch_gemm_f32(g, AMODE_SEG, 1, (hipStream_t)stream);
+}
+
+int sse_gemm_ex(const sse_gemm_desc* d, void* stream) {
+  if (!d || !d->a || !d->b || !d->zero || d->M <= 0 || d->N <= 0 || d->K <= 0 || d->ldc < d->N || (!d->cf && !d->ct))
+    return SSE_ERR_INVALID;
+  if (d->dtype != SSE_DTYPE_BF16 && d->dtype != SSE_DTYPE_FP16 && d->dtype != SSE_DTYPE_F32) return SSE_ERR_INVALID;
+  if ((d->apart != nullptr) != (d->acol != nullptr) || (d->rpart && (!d->rln_w || !d->rln_b)) ||
+      (d->resid && d->resid_t) || (d->rpart && !d->resid && !d->resid_t))
+    return SSE_ERR_INVALID;
+  GemmArgs g{};
+  g.A = d->a; g.B = d->b; g.M = d->M; g.N = d->N; g.K = d->K; g.rows_per_seg = d->M; g.lda = d->K;
+  g.bias = d->bias; g.act = d->act; g.Cf = d->cf; g.Ct = d->ct; g.ldc = d->ldc; g.zero = d->zero;
+  g.acol = d->acol; g.apart = (const float2*)d->apart; g.apart_nt = d->apart_nt; g.ln_eps = d->ln_eps;
+  g.resid = d->resid; g.resid_t = (const bf16*)d->resid_t;
+  g.rpart = (const float2*)d->rpart; g.rpart_nt = d->rpart ? 3 : 0; g.rln_w = d->rln_w; g.rln_b = d->rln_b;
+  g.opart = (float2*)d->opart;
+  hipStream_t s = (hipStream_t)stream;
+  const int rc = d->dtype == SSE_DTYPE_BF16   ? launch_gemm<bf16>(g, AMODE_SEG, 1, s)
+                 : d->dtype == SSE_DTYPE_FP16 ? launch_gemm<f16>(g, AMODE_SEG, 1, s)
+                                              : launch_gemm<float>(g, AMODE_SEG, 1, s);
+  return rc == -3 ? SSE_ERR_INVALID : (rc ? SSE_ERR_HIP : SSE_OK);
 }
 
 int sse_gemm_lnfold(const void* d_a, const void* d_b, const float* d_bias, const float* d_acol, const float* d_apart,

@@ -102,6 +102,54 @@ class WhisperFeatureExtractor:
 WhisperProcessor = WhisperFeatureExtractor
 
 
+def _shape_key(spec):
+    """A spec with the name dropped and the decoder FFN width made explicit (0 without a decoder)."""
+    import dataclasses
+    if isinstance(spec, C.WhisperSpec):
+        spec = dataclasses.replace(spec, dec_ffn=spec.dec_ffn_dim if spec.decoder_layers else 0)
+    return dataclasses.replace(spec, name="")
+
+
+def _canonical(spec, known):
+    """The named spec of ``known`` with the same shape as ``spec`` (else ``spec`` itself)."""
+    return next((k for k in known if _shape_key(k) == _shape_key(spec)), spec)
+
+
+def wavlm_spec_from_config(c) -> C.WavLMSpec:
+    """transformers ``WavLMConfig`` -> ``WavLMSpec`` (host only, no GPU): the shape fields the
+    reference's hub checkpoints set (HF/models/wavlm/configuration_wavlm.py:159-213), read by
+    ``WavLMModel.from_hf`` (REF/WavLM_embeddings.py:482-483 loads the HF model this maps).
+    ``WavLMConfig()`` maps to ``C.WAVLM_BASE``, the wavlm-large shape to ``C.WAVLM_LARGE``."""
+    if c.feat_extract_norm not in ("group", "layer"):
+        raise NotImplementedError(f"feat_extract_norm={c.feat_extract_norm!r}")
+    spec = C.WavLMSpec(hidden=c.hidden_size, layers=c.num_hidden_layers, heads=c.num_attention_heads,
+                       ffn=c.intermediate_size, conv_dim=tuple(c.conv_dim), conv_kernel=tuple(c.conv_kernel),
+                       conv_stride=tuple(c.conv_stride), conv_bias=bool(c.conv_bias),
+                       feat_norm_layer=c.feat_extract_norm == "layer",
+                       stable_layer_norm=bool(c.do_stable_layer_norm), pos_kernel=c.num_conv_pos_embeddings,
+                       pos_groups=c.num_conv_pos_embedding_groups, num_buckets=c.num_buckets,
+                       max_distance=c.max_bucket_distance, ln_eps=c.layer_norm_eps,
+                       name=getattr(c, "_name_or_path", "") or "wavlm")
+    return _canonical(spec, (C.WAVLM_BASE, C.WAVLM_LARGE))
+
+
+def whisper_spec_from_config(c, with_decoder: bool = True) -> C.WhisperSpec:
+    """transformers ``WhisperConfig`` -> ``WhisperSpec`` (host only, no GPU), read by
+    ``WhisperModel.from_hf`` (REF/whisper_embeddings_large.py:437-438 loads the HF model this maps).
+    The whisper-tiny / -small / -large-v2 shapes map to the named ``C.WHISPER_*`` specs (``*_DEC``
+    with the decoder)."""
+    if c.decoder_attention_heads != c.encoder_attention_heads:
+        raise NotImplementedError("decoder and encoder head counts differ")
+    spec = C.WhisperSpec(d_model=c.d_model, layers=c.encoder_layers, heads=c.encoder_attention_heads,
+                         ffn=c.encoder_ffn_dim, n_mels=c.num_mel_bins, max_positions=c.max_source_positions,
+                         decoder_layers=c.decoder_layers if with_decoder else 0, dec_ffn=c.decoder_ffn_dim,
+                         vocab_size=c.vocab_size, max_target_positions=c.max_target_positions,
+                         name=getattr(c, "_name_or_path", "") or "whisper")
+    known = ((C.WHISPER_TINY_DEC, C.WHISPER_SMALL_DEC, C.WHISPER_LARGE_V2_DEC) if with_decoder
+             else (C.WHISPER_TINY, C.WHISPER_SMALL, C.WHISPER_LARGE_V2))
+    return _canonical(spec, known)
+
+
 class _DuckModel:
     def __init__(self, sse: SSEModel):
         self.sse = sse
@@ -139,15 +187,7 @@ class WavLMModel(_DuckModel):
 
     @classmethod
     def from_hf(cls, hf_model, device="cuda:0", dtype="fp32"):
-        c = hf_model.config
-        spec = C.WavLMSpec(hidden=c.hidden_size, layers=c.num_hidden_layers, heads=c.num_attention_heads,
-                           ffn=c.intermediate_size, conv_dim=tuple(c.conv_dim), conv_kernel=tuple(c.conv_kernel),
-                           conv_stride=tuple(c.conv_stride), conv_bias=bool(c.conv_bias),
-                           feat_norm_layer=c.feat_extract_norm == "layer",
-                           stable_layer_norm=bool(c.do_stable_layer_norm), pos_kernel=c.num_conv_pos_embeddings,
-                           pos_groups=c.num_conv_pos_embedding_groups, num_buckets=c.num_buckets,
-                           max_distance=c.max_bucket_distance, ln_eps=c.layer_norm_eps)
-        return cls.from_state_dict(spec, hf_model.state_dict(), device, dtype)
+        return cls.from_state_dict(wavlm_spec_from_config(hf_model.config), hf_model.state_dict(), device, dtype)
 
     def __call__(self, input_values, attention_mask=None, output_hidden_states=None, return_dict=True, **_):
         if attention_mask is not None:
@@ -205,12 +245,5 @@ class WhisperModel(_DuckModel):
 
     @classmethod
     def from_hf(cls, hf_model, device="cuda:0", dtype="fp32", with_decoder=True):
-        c = hf_model.config
-        if c.decoder_attention_heads != c.encoder_attention_heads:
-            raise NotImplementedError("decoder and encoder head counts differ")
-        spec = C.WhisperSpec(d_model=c.d_model, layers=c.encoder_layers, heads=c.encoder_attention_heads,
-                             ffn=c.encoder_ffn_dim, n_mels=c.num_mel_bins, max_positions=c.max_source_positions,
-                             decoder_layers=c.decoder_layers if with_decoder else 0, dec_ffn=c.decoder_ffn_dim,
-                             vocab_size=c.vocab_size, max_target_positions=c.max_target_positions,
-                             name=getattr(c, "_name_or_path", "") or "whisper")
+        spec = whisper_spec_from_config(hf_model.config, with_decoder=with_decoder)
         return cls.from_state_dict(spec, hf_model.state_dict(), device, dtype)

@@ -252,3 +252,52 @@ def test_step_gather_two_slots_and_drain(world, steps):
             exp = np.concatenate([np.arange(3, dtype=np.float32)[:, None, None] + rr * 1000 + last
                                   for rr in range(world)])
             assert np.array_equal(gathered[slot], np.broadcast_to(exp, (world * 3, 2, 4))), (r, slot)
+
+
+def _finish_fail_worker(rank, world, port, q):
+    import importlib
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    importlib.import_module("stuttering-speech-representation_amd")
+    import torch.distributed as dist
+    from ssr_amd import _lib
+    from ssr_amd.corpus import ShardFinishError, extract_corpus
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def fn(wave):
+        return _embed(wave)
+
+    def fail():   # the fp16-range check of sse_embed_fn, failing on rank 1 only
+        if rank == 1:
+            raise _lib.SSERangeError(_lib.SSE_ERR_RANGE, "sse_check_range")
+    fn.finish = fail
+    try:
+        extract_corpus(lambda s, e: _clips(s, e, 66), 9, fn, (2, 3), "cpu", batch=2)
+        q.put((rank, "no error"))
+    except ShardFinishError as e:
+        q.put((rank, "peer: " + str(e)))
+    except _lib.SSERangeError as e:
+        q.put((rank, "own: " + str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_finish_failure_raises_on_every_rank():
+    """one rank's fp16-range failure used to raise there while the other ranks blocked in the
+    all-gather until the collective timed out.  Now every rank raises together: the failing rank its own
+    SSERangeError with its shard bounds, the others ShardFinishError naming it -- and nobody hangs."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 34600 + (os.getpid() % 1000)
+    procs = [ctx.Process(target=_finish_fail_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[1].startswith("own: ") and "rank 1, shard [3, 6)" in res[1], res[1]
+    for r in (0, 2):
+        assert res[r].startswith("peer: ") and "rank(s) [1]" in res[r], res[r]

@@ -94,3 +94,5 @@ def test_flash_attention_rejects_bad_shapes():
     assert L.sse_attention(x.data_ptr(), out.data_ptr(), 1, 64, 130, 2, 3 * 128, 1.0, 0, None) < 0   # H != 64 nh
     assert L.sse_attention(x.data_ptr(), out.data_ptr(), 1, 64, 128, 2, 200, 1.0, 0, None) < 0       # ldq < 3H
     assert L.sse_attention(None, out.data_ptr(), 1, 64, 128, 2, 3 * 128, 1.0, 0, None) < 0
+    # q_log2 = 1 with a scale other than ln 2 (the 32x32 kernel would ignore it: ADVICE r4)
+    assert L.sse_attention(x.data_ptr(), out.data_ptr(), 1, 64, 128, 2, 3 * 128, 1.0, 1, None) < 0

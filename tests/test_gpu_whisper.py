@@ -286,3 +286,32 @@ def test_whisper_flash3_matches_flash2(dtype, tol):
         rel = _rel(a[q].cpu().numpy(), g["emb"][q]).max()
         print(dtype, "flash3 whisper-small rel-L2", q, rel)
         assert rel <= tol
+
+
+def test_whisper_small_folded_vs_materialised_layernorm():
+    """the bf16 Whisper pre-LN fold (QKV and fc1 read the un-normalised bf16 stream, the
+    LayerNorm applied in the GEMM epilogue from the residual GEMMs' per-256-column partials) against a
+    model built with no_lnfold = 1 (read at sse_model_create: LayerNorm kernels and the plain weights).
+    The fold moves rounding points, so the bar is tolerance, not bit-identity; both forms stay at the
+    reference's bf16 bar on its whisper-small fixture."""
+    p = os.path.join(GOLDEN, "whisper_small.npz")
+    if not os.path.exists(p):
+        pytest.skip("whisper-small fixture not generated")
+    from ssr_amd import _lib, config as C, synth
+    from ssr_amd.model import SSEModel
+    g = np.load(p)
+    sd = synth.synth_whisper_state_dict(C.WHISPER_SMALL, seed=11)
+    idx = [int(i) for i in g["layer_indices"]]
+    w = torch.zeros((2, 480000), device="cuda:0")
+    for i, c in enumerate(_clips(None, [3.0, 12.0])):
+        w[i, :c.shape[0]] = torch.from_numpy(c)
+    folded = SSEModel(C.WHISPER_SMALL, sd, device="cuda:0", dtype="bf16")
+    with _lib.option("no_lnfold", 1):
+        plain = SSEModel(C.WHISPER_SMALL, sd, device="cuda:0", dtype="bf16")
+    a = folded.embed(w, idx).cpu().numpy()
+    b = plain.embed(w, idx).cpu().numpy()   # the option is back at 0: the model's load-time choice holds
+    d = _rel(a, b).max()
+    ra, rb = _rel(a, g["emb"]).max(), _rel(b, g["emb"]).max()
+    print("whisper-small bf16 folded vs materialised", d, "vs fixture", ra, rb)
+    assert np.isfinite(a).all() and d <= 1.5e-2
+    assert ra <= 3e-2 and rb <= 3e-2

@@ -89,3 +89,13 @@ def test_options_are_explicit_only():
             assert L.sse_get_option(name) == 1
         assert L.sse_get_option(name) == 0
     assert L.sse_set_option(b"no_such_switch", 1) < 0
+
+
+def test_attention_hook_rejects_q_log2_with_other_scale():
+    """sse_attention validates before any device work: q_log2 = 1 requires scale = ln 2 (the 32x32 flash
+    kernel reads log2-domain logits and never applies a scale; the short-T kernels would)."""
+    from ssr_amd import _lib
+    L = _lib.lib()
+    fake = ctypes.c_void_p(256)   # never dereferenced: rejected on the arguments alone
+    assert L.sse_attention(fake, fake, 1, 300, 128, 2, 384, 1.0, 1, None) == _lib.SSE_ERR_INVALID
+    assert L.sse_attention(fake, fake, 1, 300, 128, 2, 384, 0.125, 1, None) == _lib.SSE_ERR_INVALID
