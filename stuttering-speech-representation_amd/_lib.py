@@ -159,8 +159,9 @@ def lib() -> ctypes.CDLL:
     L.sse_gemm.restype = i32
     L.sse_attention.argtypes = [vp, vp, i32, i32, i32, i32, i32, ctypes.c_float, i32, vp]
     L.sse_attention.restype = i32
-    L.sse_gemm_ex.argtypes = [ctypes.POINTER(sse_gemm_desc), vp]
-    L.sse_gemm_ex.restype = i32
+    if hasattr(L, "sse_gemm_ex"):   # (absent from pre-round-5 builds loaded for A/B runs via set_lib_path)
+        L.sse_gemm_ex.argtypes = [ctypes.POINTER(sse_gemm_desc), vp]
+        L.sse_gemm_ex.restype = i32
     L.sse_gemm_lnfold.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, ctypes.c_float, vp, vp]
     L.sse_gemm_lnfold.restype = i32
     L.sse_whisper_embed.argtypes = [vp, vp, i32, i32, vp, i32, vp, vp, i32, vp, vp, sz, vp]

@@ -790,6 +790,13 @@ constexpr int G8P_SMEM = G8_OPS + 2 * G8P_EP;
 template <int ACT, bool CT3, bool F16, bool has_bias, bool fold, int DBG = 0, int FNT = 3>
 SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, int n0, int wm, int wn, int q,
                           int r16, const char* ep) {
+  {   // lane-derived values recomputed here from an opaque lane id: the compiler hoisted them out of the tile
+      // loop, where they held ~12 VGPRs through the main loop (246 -> 234 VGPRs, round 5)
+    int ln = (int)(threadIdx.x & 63);
+    asm volatile("" : "+v"(ln));
+    q = ln >> 4;
+    r16 = ln & 15;
+  }
   const float alpha = F16 ? g.alpha : 1.f;   // split-fp16: the weights' 2^s undone (exact)
   f32x4 bv[2][2], ac[2][2];
   #pragma unroll
@@ -946,7 +953,8 @@ SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, i
 // ======================================================================================
 // EP: bit 0 = bias present, bit 1 = folded LayerNorm (apart/acol) -- compile-time, so an absent term
 // costs no epilogue instruction (runtime selects measured +5-6 % on conv1 / ffn1 when removed).
-// DBG (timing probes only): see g8p_epilogue; 2 = no epilogue at all (accumulators kept live).
+// DBG (timing probes only): see g8p_epilogue; 2 = no epilogue at all (accumulators kept live); 4 = no epilogue and
+// no MFMA (the LDS fragment reads kept live); 5 = no epilogue and no main-loop LDS-DMA.
 template <int ACT, bool CT3 = false, bool F16 = false, int EP = 1, int DBG = 0, int FNT = 3>
 __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
   __shared__ __attribute__((aligned(16))) char smem[G8P_SMEM];   // operands | 2 epilogue slots: the ONLY shared object
@@ -966,6 +974,12 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
   int round = 0;
   int tile = g8p_tile(b, 0, G, n_tiles);
   if (tile < 0) return;
+  if constexpr (DBG >= 6) {   // probe: half of each XCD's blocks start (DBG - 5) x 6 us late (desynchronised epilogues)
+    if ((b >> 3) & 1) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (__builtin_amdgcn_s_memrealtime() - t0 < 600ull * (DBG - 5)) __builtin_amdgcn_s_sleep(8);
+    }
+  }
 
   constexpr int NREC = 0x7FFFFFF0;
   __amdgpu_buffer_rsrc_t a_rsrc, b_rsrc;
@@ -1091,12 +1105,22 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
-    #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    if constexpr (DBG == 4) {   // probe: no MFMA (the fragment reads kept live)
       #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int ks = 0; ks < 2; ++ks) {
         #pragma unroll
-        for (int j = 0; j < 2; ++j) c[i][j] = g8_mfma<F16>(bf[j][ks], af[i][ks], c[i][j]);
+        for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(af[i][ks]));
+        #pragma unroll
+        for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(bf[j][ks]));
+      }
+    } else {
+      #pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        #pragma unroll
+        for (int i = 0; i < 4; ++i)
+          #pragma unroll
+          for (int j = 0; j < 2; ++j) c[i][j] = g8_mfma<F16>(bf[j][ks], af[i][ks], c[i][j]);
+    }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -1128,7 +1152,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
       const char* buf = smem + (t & 1) * G8_BUF;
       const int k = 4 * t;
       auto issue_wait = [&](int kk) {
-        issue(kk);
+        if constexpr (DBG != 5) issue(kk);   // probe 5: no main-loop DMA
         if constexpr (FI) {
           g8_vmcnt_dyn<false>(g8_count<false>(kk, nk) + S);
         } else if constexpr (ST) {
@@ -1171,7 +1195,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
       setup(next);
       for (int k = -6; k < 0; ++k) issue(k);
     }
-    if constexpr (DBG == 2) {
+    if constexpr (DBG == 2 || DBG == 4 || DBG == 5) {   // (DBG 6, 7: the library epilogue)
       #pragma unroll
       for (int a = 0; a < 2; ++a)
         #pragma unroll
@@ -1184,7 +1208,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
     }
     if (next < 0) break;
     slot ^= 1;
-    S = (DBG == 1 || DBG == 2) ? 0 : (m0 + 256 <= M ? s_full : 0);
+    S = DBG == 1 || DBG == 2 || DBG == 4 || DBG == 5 ? 0 : (m0 + 256 <= M ? s_full : 0);
     tile = next;
   }
 }
@@ -1201,10 +1225,177 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
 // LayerNorm partials of the written rows (OPART, the folded post-LN path): per row, each wave
 // reduces its 64 columns (16 in-lane values, lanes q = 0..3) to (mean_c, M2_c), the 4 waves' chunks
 // meet in LDS and one thread per row combines them (Chan) into the 256-column (mean_t, M2_t).
-// ======================================================================================
-template <bool LN, bool OPART, bool RB, bool F16 = false>
+// LDS of gemm8r_kernel<RB = true>: operands (2 x 64 KiB) | epilogue parameters | row-chunk statistics
+constexpr int G8R_PAR = G8_OPS;                  // [0, 1K) bias | [1K, 2K) rln_w | [2K, 3K) rln_b | [3K, 9K) partials
+constexpr int G8R_CST = G8_OPS + 9 * 1024;       // [2 halves][128 rows][4 waves] float2
+constexpr int G8R_SMEM_RB = G8R_CST + 8 * 1024;
+
+// Epilogue of gemm8r_kernel<RB = true> (below): o = acc + bias + LN?(resid) rounded to the 16-bit stream type, the
+// out-partials of the written rows (OPART), stores through per-16-row-block buffer resources.  The residual rows and
+// the parameters are in LDS (see gemm8r_kernel); half 1's residual DMA is in flight on entry.
+// DBG (probes only): 5 = no stores (results kept live), 6 = no out-partials, 7 = no math (raw accumulators stored)
+template <bool LN, bool OPART_, bool F16, int DBG, typename ResDma>
+SSE_DEV void g8r_epilogue_rb(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], char* smem, int m0, int n0, int wm, int wn,
+                             int q, int r16, int nk, bool has_bias, ResDma&& res_dma) {
+  constexpr bool OPART = OPART_ && DBG != 6;
+  const int M = g.M;
+  res_dma(1, (nk - 1) & 1);                         // every read of that buffer is done (the barrier before)
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // parameters and half 0 landed; half 1's 8 pieces in flight
+  __syncthreads();
+  float2* cst = (float2*)(smem + G8R_CST);
+  const char* par = smem + G8R_PAR;
+  // 16-B store-layout chunk of (i, ni): columns ni*128 + wn*32 + (q&1)*16 + (q>>1)*8 .. +7 = logical chunk c
+  const int cl = wn * 4 + (q & 1) * 2 + (q >> 1);
+  auto finish_half = [&](int mi) {
+    if constexpr (DBG == 7) return;
+    // compiler memory barrier: the column parameters are re-read from LDS per half
+    asm volatile("" ::: "memory");
+    const char* rb = smem + (mi ? (nk - 1) & 1 : nk & 1) * G8_BUF;
+    f32x4 rv[4][2][2];
+    #pragma unroll
+    for (int i = 0; i < 4; ++i)
+      #pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const int row = wm * 64 + i * 16 + r16;   // row & 15 == r16
+        const uint4 v = *(const uint4*)(rb + row * 512 + ((ni * 16 + (cl ^ r16)) << 4));
+        const auto x = __builtin_amdgcn_permlane16_swap(v.x, v.z, false, false);
+        const auto y = __builtin_amdgcn_permlane16_swap(v.y, v.w, false, false);
+        rv[i][ni][0] = unpack_h4<F16>(make_uint2(x[0], y[0]));   // bf16, or fp16 (h16 path)
+        rv[i][ni][1] = unpack_h4<F16>(make_uint2(x[1], y[1]));
+      }
+    // the four row blocks' statistics side by side: four independent chains through every step (one row block
+    // at a time, the sum -> two lane-group swaps -> mean -> 16-long dependent M2 fma chain -> two swaps was
+    // latency-bound: 8.3 of the oproj launch's 25 us of epilogue, round-5 probe)
+    float sum[4];
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float2 st = make_float2(0.f, 1.f);
+      if constexpr (LN) {
+        const float2* p = (const float2*)(par + 3072) + (mi * 128 + wm * 64 + i * 16 + r16) * 3;
+        const float2 v[3] = {p[0], p[1], p[2]};
+        st = ln_part_combine<3>(v, g.ln_eps);
+      }
+      float sp[4];
+      #pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+        #pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int c = ni * 128 + wn * 32 + j * 16 + q * 4;
+          f32x4 r = rv[i][ni][j];
+          if constexpr (LN) {   // LayerNorm of the residual, the exact expression of layernorm_kernel
+            const f32x4 lw = *(const f32x4*)(par + 1024 + c * 4), lb = *(const f32x4*)(par + 2048 + c * 4);
+            #pragma unroll
+            for (int e = 0; e < 4; ++e) r[e] = fmaf((r[e] - st.x) * st.y, lw[e], lb[e]);
+          }
+          const f32x4 bvv = *(const f32x4*)(par + c * 4);
+          const f32x4 bv = has_bias ? bvv : f32x4{0.f, 0.f, 0.f, 0.f};
+          f32x4 o = (acc[mi][ni][i][j] + bv) + r;
+          #pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = round_h<F16>(o[e]);   // the statistics describe the rounded values
+          acc[mi][ni][i][j] = o;
+          sp[ni * 2 + j] = (o[0] + o[1]) + (o[2] + o[3]);
+        }
+      sum[i] = (sp[0] + sp[1]) + (sp[2] + sp[3]);
+    }
+    if constexpr (OPART) {   // this wave's 64 columns of each row: lanes r16 + 16q (sums over q by lane-group swaps)
+      auto qsum4 = [](float (&v)[4]) {
+        #pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const auto t = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i]), false, false);
+          v[i] = __uint_as_float(t[0]) + __uint_as_float(t[1]);
+        }
+        #pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const auto t = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i]), false, false);
+          v[i] = __uint_as_float(t[0]) + __uint_as_float(t[1]);
+        }
+      };
+      qsum4(sum);
+      float m2[4];
+      #pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float mc = sum[i] * (1.0f / 64.0f);
+        float p[4];
+        #pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const f32x4 d = acc[mi][u >> 1][i][u & 1] - mc;
+          p[u] = fmaf(d[3], d[3], fmaf(d[2], d[2], fmaf(d[1], d[1], d[0] * d[0])));
+        }
+        m2[i] = (p[0] + p[1]) + (p[2] + p[3]);
+        sum[i] = mc;
+      }
+      qsum4(m2);
+      if (q == 0) {
+        #pragma unroll
+        for (int i = 0; i < 4; ++i) cst[(mi * 128 + wm * 64 + i * 16 + r16) * 4 + wn] = make_float2(sum[i], m2[i]);
+      }
+    }
+  };
+  // one resource per 16-row block based at (m0 + mi*128 + 16 i, n0), num_records ending at row M: rows >= M dropped
+  const unsigned lane_off = (unsigned)(((wm * 64 + r16) * g.ldc + wn * 32 + (q & 1) * 16 + (q >> 1) * 8) * 2);
+  auto store_half = [&](int mi) {
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const long long r0 = (long long)m0 + mi * 128 + 16 * i, rows = (long long)M - r0;
+      const long long nrec = rows > 0 ? (rows * g.ldc - n0) * 2 : 0;
+      const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)((bf16*)g.Ct + (rows > 0 ? r0 * g.ldc + n0 : 0)), (short)0, (int)min(nrec, (long long)0x7FFFFFF0),
+          0x00020000);
+      #pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const uint2 X = pack_h4<F16>(acc[mi][ni][i][0]), Y = pack_h4<F16>(acc[mi][ni][i][1]);
+        const auto s0 = __builtin_amdgcn_permlane16_swap(X.x, Y.x, false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(X.y, Y.y, false, false);
+        if constexpr (DBG == 5) {
+          asm volatile("" ::"v"(s0[0]), "v"(s0[1]), "v"(s1[0]), "v"(s1[1]));
+          continue;
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{s0[0], s1[0], s0[1], s1[1]}, cr, lane_off + (unsigned)(ni * 256), 0u, 0);
+      }
+    }
+  };
+  finish_half(0);
+  __builtin_amdgcn_sched_barrier(0);
+  store_half(0);
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (DBG == 5) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // half 1's residual landed (younger: half 0's 8 stores)
+  __syncthreads();
+  finish_half(1);
+  __builtin_amdgcn_sched_barrier(0);
+  store_half(1);
+  if constexpr (OPART) {
+    __syncthreads();
+    if (threadIdx.x < 256) {
+      const int r = threadIdx.x, m = m0 + r;
+      const float2* c = cst + r * 4;
+      const float2 c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3];
+      const float mean = 0.25f * ((c0.x + c1.x) + (c2.x + c3.x));
+      const float d0 = c0.x - mean, d1 = c1.x - mean, d2 = c2.x - mean, d3 = c3.x - mean;
+      const float m2 = ((c0.y + c1.y) + (c2.y + c3.y)) + 64.f * ((d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3));
+      if (m < M) g.opart[(long long)m * (g.N >> 8) + (n0 >> 8)] = make_float2(mean, m2);
+    }
+  }
+}
+
+// RB (the 16-bit residual stream, round 5): the epilogue no longer waits on global memory after the main loop --
+//   1. its parameters (bias, rln_w, rln_b: 1 KiB each; the residual rows' LayerNorm partials [256][3]: 6 KiB) go
+//      into LDS by DMA at kernel START, before the operand prologue (retired by the first counted wait);
+//   2. the residual rows of half 0 (128 x 256 16-bit = 64 KiB, 8 DMA pieces per wave) are DMA'd during the LAST
+//      K-tile into the operand buffer K-tile nk - 2 used (free: its last reads precede that K-tile's phase-2
+//      barrier), half 1 into the other buffer right after the main loop; both images are swizzled on the source
+//      side (16-B chunk c of row r at chunk c ^ (r & 15)) so the store-layout ds_read_b128 of 16 rows is
+//      conflict-free;
+//   3. the row-block stores go through a buffer resource per 16-row block (rows >= M dropped by its range check),
+//      the cross-lane sums of the out-partials through v_permlane16/32_swap instead of ds_bpermute.
+// Probe (tools/gemm8_probe.hip, oproj 38144 x 768 x 768, round 5 before the change): 65.9 us per launch against
+// 37.3 with no epilogue; 7.8 of the 28.6 us were the residual loads, 2.6 the parameter wait.
+// DBG (timing probes only, tools/gemm8_probe.hip; the library launches DBG = 0): 2 = no epilogue (accumulators
+// kept live).
+template <bool LN, bool OPART, bool RB, bool F16 = false, int DBG = 0>
 __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) char smem[G8_OPS];   // the ONLY shared object
+  // RB: operands | epilogue parameters (9 KiB, staged at kernel start) | row-chunk statistics (8 KiB)
+  __shared__ __attribute__((aligned(16))) char smem[RB ? G8R_SMEM_RB : G8_OPS];   // the ONLY shared object
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 2, wn = wave & 3;
@@ -1300,6 +1491,55 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   };
+  const bool has_bias = g.bias != nullptr;
+  // RB: epilogue parameters into LDS before the prologue (wave w < 6: partials piece w; 6: bias; 7: rln_w, rln_b)
+  if constexpr (RB) {
+    __amdgpu_buffer_rsrc_t r;
+    unsigned soff = 0;
+    int off = 0;
+    bool go = true;
+    if (wave < 6) {
+      go = LN;
+      r = __builtin_amdgcn_make_buffer_rsrc((void*)(LN ? (const void*)g.rpart : g.zero), (short)0, LN ? M * 24 : 0,
+                                            0x00020000);
+      soff = (unsigned)(m0 * 24 + wave * 1024);
+      off = 3072 + wave * 1024;
+    } else if (wave == 6) {
+      go = has_bias;
+      r = __builtin_amdgcn_make_buffer_rsrc((void*)(has_bias ? (const void*)g.bias : g.zero), (short)0,
+                                            has_bias ? g.N * 4 : 0, 0x00020000);
+      soff = (unsigned)(n0 * 4);
+    } else {
+      go = LN;
+      r = __builtin_amdgcn_make_buffer_rsrc((void*)(LN ? (const void*)g.rln_w : g.zero), (short)0, LN ? g.N * 4 : 0,
+                                            0x00020000);
+      soff = (unsigned)(n0 * 4);
+      off = 1024;
+    }
+    if (go) __builtin_amdgcn_raw_ptr_buffer_load_lds(r, LPTR(smem + G8R_PAR + off), 16, (unsigned)lane * 16u, soff, 0, 0);
+    if (LN && wave == 7) {
+      r = __builtin_amdgcn_make_buffer_rsrc((void*)g.rln_b, (short)0, g.N * 4, 0x00020000);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, LPTR(smem + G8R_PAR + 2048), 16, (unsigned)lane * 16u, soff, 0, 0);
+    }
+  }
+  // RB: residual rows of half mi (128 x 256 16-bit values, 512 B per row) into the 64 KiB operand buffer `dst`:
+  // wave w's piece e (1 KiB) holds rows 2u, 2u + 1 (u = 8w + e); lane l writes 16-B chunk l & 31 of row
+  // 2u + (l >> 5), which holds logical chunk (l & 31) ^ (row & 15).  Rows >= M read as zeros (never stored).
+  auto res_dma = [&](int mi, int buf) {
+    if constexpr (RB) {
+      const long long r0 = (long long)m0 + mi * 128, rows = (long long)M - r0;
+      const long long nrec = rows > 0 ? (rows * g.ldc - n0) * 2 : 0;
+      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(g.resid_t + (rows > 0 ? r0 * g.ldc + n0 : 0)), (short)0, (int)min(nrec, (long long)0x7FFFFFF0),
+          0x00020000);
+      #pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int u = wave * 8 + e, row = 2 * u + (lane >> 5), c = (lane & 31) ^ (row & 15);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, LPTR(smem + buf * G8_BUF + u * 1024), 16,
+                                                 (unsigned)((row * g.ldc + c * 8) * 2), 0u, 0, 0);
+      }
+    }
+  };
   for (int k = -6; k < 0; ++k) issue(k);
   g8_wait<false>(-1, nk);
   g8_barrier();
@@ -1308,10 +1548,13 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
     constexpr bool ST = decltype(steady)::value;
     const char* buf = smem + (t & 1) * G8_BUF;
     const int k = 4 * t;
+    // RB, last K-tile: half 0's residual rows go out in phase 0 (the tail waits leave those 8 in flight)
+    const int xr = (RB && !ST && t == nk - 1) ? 8 : 0;
+    if (xr) res_dma(0, nk & 1);
     auto issue_wait = [&](int kk) {
       issue(kk);
       if constexpr (ST) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else g8_wait<false>(kk, nk);
+      else g8_vmcnt_dyn<false>(g8_count<false>(kk, nk) + xr);
     };
     read_a(buf);
     read_b(buf + 2 * G8_HALF, b0f);
@@ -1338,12 +1581,34 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
   for (; t + 2 < nk; ++t) run_tile(t, std::integral_constant<bool, true>{});
   for (; t < nk; ++t) run_tile(t, std::integral_constant<bool, false>{});
   if (wm == 0) g8_barrier();   // balance group 1's extra barrier: every wave's LDS reads are done
+  if constexpr (RB) {
+    if constexpr (DBG == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      #pragma unroll
+      for (int a = 0; a < 2; ++a)
+        #pragma unroll
+        for (int c = 0; c < 2; ++c)
+          #pragma unroll
+          for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(acc[a][c][i][0]), "v"(acc[a][c][i][1]));
+      return;
+    }
+    g8r_epilogue_rb<LN, OPART, F16, DBG>(g, acc, smem, m0, n0, wm, wn, q, r16, nk, has_bias, res_dma);
+    return;
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (DBG == 2) {
+    #pragma unroll
+    for (int a = 0; a < 2; ++a)
+      #pragma unroll
+      for (int c = 0; c < 2; ++c)
+        #pragma unroll
+        for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(acc[a][c][i][0]), "v"(acc[a][c][i][1]));
+    return;
+  }
 
   // ---- epilogue ----
   // LDS (operand area, free now): [0, 1K) bias | [1K, 2K) rln_w | [2K, 3K) rln_b | [3K, 9K) partials
   // [256][3] | [16K, 24K) chunk statistics [2 halves][128 rows][4 waves] float2
-  const bool has_bias = g.bias != nullptr;
   {
     __amdgpu_buffer_rsrc_t r;
     unsigned soff = 0;
@@ -1378,6 +1643,18 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
   f32x4 rv[4][2][2];
   uint4 rvb[4][2];
   auto load_half = [&](int mi) {
+    if constexpr (DBG == 3) {
+      #pragma unroll
+      for (int i = 0; i < 4; ++i)
+        #pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          int z = 0;
+          asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+          rvb[i][ni] = make_uint4(z, z, z, z);
+          rv[i][ni][0] = rv[i][ni][1] = f32x4{(float)z, (float)z, (float)z, (float)z};
+        }
+      return;
+    }
     #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = m0 + mi * 128 + wm * 64 + i * 16 + r16;
@@ -1411,7 +1688,7 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
   };
   __builtin_amdgcn_sched_barrier(0);
   load_half(0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // parameter DMA (and half 0's rows) landed
+  if constexpr (DBG != 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // parameter DMA (and half 0's rows) landed
   __syncthreads();
   __builtin_amdgcn_sched_barrier(0);
   // column parameters are read from LDS where they are used (registers hold acc + one half's rows)

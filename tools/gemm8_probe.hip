@@ -1,6 +1,8 @@
 // Where the persistent bf16 GEMM's time goes outside the main loop (round-4 probe, not product code).
 // Times gemm8p_kernel in four builds on the WavLM-base B = 256 shapes, interleaved in one process:
 //   DBG 0 = the library kernel, 1 = epilogue math without stores, 2 = no epilogue, 3 = stores without math,
+//   4 = no epilogue and no MFMA (memory side of the main loop), 5 = no epilogue and no DMA (MFMA / LDS side),
+//   6 / 7 = the library kernel with half of every XCD's blocks starting 6 / 12 us late (are the epilogue stores a burst?),
 // (round 4 also timed, then removed from the kernel: full-line store patterns, non-temporal stores, stores
 // into one L2-resident tile, half the stores, stores spread over the main loop and deferred stores -- the
 // measurements and why they were not kept are in DESIGN.md §3 "GEMM epilogue")
@@ -39,7 +41,22 @@ static kfn pick(int dbg) {
     case 1: return gemm8p_kernel<ACT, false, false, EP, 1>;
     case 2: return gemm8p_kernel<ACT, false, false, EP, 2>;
     case 3: return gemm8p_kernel<ACT, false, false, EP, 3>;
+    case 4: return gemm8p_kernel<ACT, false, false, EP, 4>;
+    case 5: return gemm8p_kernel<ACT, false, false, EP, 5>;
+    case 6: return gemm8p_kernel<ACT, false, false, EP, 6>;
+    case 7: return gemm8p_kernel<ACT, false, false, EP, 7>;
     default: return gemm8p_kernel<ACT, false, false, EP, 0>;
+  }
+}
+
+typedef void (*kfr)(GemmArgs);
+static kfr pick_r(int dbg) {   // the folded post-LN residual GEMM (oproj / ffn2 of WavLM-base bf16)
+  switch (dbg) {
+    case 2: return gemm8r_kernel<true, true, true, false, 2>;
+    case 5: return gemm8r_kernel<true, true, true, false, 5>;
+    case 6: return gemm8r_kernel<true, true, true, false, 6>;
+    case 7: return gemm8r_kernel<true, true, true, false, 7>;
+    default: return gemm8r_kernel<true, true, true, false, 0>;
   }
 }
 
@@ -79,6 +96,42 @@ int main() {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const int ROUNDS = 3, IT = 20;
+  {   // residual GEMMs: oproj (K = 768) and ffn2 (K = 3072), N = 768, bf16 stream + LayerNorm partials in / out
+    bf16* rs;
+    float *lw, *lb;
+    float2* op;
+    CK(hipMalloc(&rs, 38144LL * 768 * 2)); CK(hipMalloc(&lw, 768 * 4)); CK(hipMalloc(&lb, 768 * 4));
+    CK(hipMalloc(&op, 38144LL * 3 * 8));
+    hipLaunchKernelGGL(fill_bf16, dim3(2048), dim3(256), 0, 0, rs, 38144LL * 768, 5u, 1.0f);
+    CK(hipMemcpy(lw, bias, 768 * 4, hipMemcpyDeviceToDevice)); CK(hipMemcpy(lb, bias, 768 * 4, hipMemcpyDeviceToDevice));
+    for (int K : {768, 3072}) {
+      GemmArgs g{};
+      g.A = a; g.B = b; g.M = 38144; g.N = 768; g.K = K; g.rows_per_seg = g.M; g.lda = K;
+      g.bias = bias; g.Ct = c; g.ldc = 768; g.zero = zero; g.resid_t = rs; g.rpart = apart; g.rpart_nt = 3;
+      g.rln_w = lw; g.rln_b = lb; g.ln_eps = 1e-5f; g.opart = op;
+      const int tiles = 149 * 3;
+      double best[8] = {1e30, 1e30, 1e30, 1e30, 1e30, 1e30, 1e30, 1e30};
+      for (int r = 0; r < ROUNDS; ++r)
+        for (int dbg : {0, 2, 5, 6, 7}) {
+          kfr k = pick_r(dbg);
+          for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(k, dim3(tiles), dim3(512), 0, 0, g);
+          CK(hipEventRecord(e0, 0));
+          for (int i = 0; i < IT; ++i) hipLaunchKernelGGL(k, dim3(tiles), dim3(512), 0, 0, g);
+          CK(hipEventRecord(e1, 0));
+          CK(hipEventSynchronize(e1));
+          float ms;
+          CK(hipEventElapsedTime(&ms, e0, e1));
+          ms /= IT;
+          if (ms < best[dbg]) best[dbg] = ms;
+        }
+      const double tf = 2.0 * 38144 * 768 * K / 1e12;
+      printf("%-10s M=38144 N=768 K=%d tiles=%d (gemm8r, one tile per block)\n", K == 768 ? "oproj" : "ffn2", K, tiles);
+      const char* nm[8] = {"full", "", "no-epilogue", "", "", "no-stores", "no-opart", "no-math"};
+      for (int d : {0, 2, 5, 6, 7})
+        printf("   %-14s %8.1f us  %7.1f TF/s\n", nm[d], best[d] * 1e3, tf / (best[d] * 1e-3));
+      fflush(stdout);
+    }
+  }
   for (const Shape& s : shapes) {
     GemmArgs g{};
     g.A = a; g.B = b; g.M = s.M; g.N = s.N; g.K = s.K; g.rows_per_seg = s.M; g.lda = s.K;
@@ -88,9 +141,9 @@ int main() {
     const int n_tiles = ((s.M + 255) / 256) * (s.N / 256);
     const int G = n_tiles < cus ? n_tiles : cus;
     const double tf = 2.0 * s.M * s.N * s.K / 1e12;
-    double best[4] = {1e30, 1e30, 1e30, 1e30};
+    double best[8] = {1e30, 1e30, 1e30, 1e30, 1e30, 1e30, 1e30, 1e30};
     for (int r = 0; r < ROUNDS; ++r)
-      for (int dbg = 0; dbg < 4; ++dbg) {
+      for (int dbg = 0; dbg < 8; ++dbg) {
         kfn k;
         if (s.act == ACT_GELU_FAST) k = s.ep == 3 ? pick<ACT_GELU_FAST, 3>(dbg) : (s.ep == 1 ? pick<ACT_GELU_FAST, 1>(dbg) : pick<ACT_GELU_FAST, 0>(dbg));
         else k = s.ep == 3 ? pick<ACT_NONE, 3>(dbg) : (s.ep == 1 ? pick<ACT_NONE, 1>(dbg) : pick<ACT_NONE, 0>(dbg));
@@ -106,8 +159,9 @@ int main() {
       }
     const double rounds = (double)n_tiles / cus;
     printf("%-10s M=%d N=%d K=%d tiles=%d (%.2f rounds)\n", s.name, s.M, s.N, s.K, n_tiles, rounds);
-    const char* nm[4] = {"full", "math,no-store", "no-epilogue", "store,no-math"};
-    for (int d = 0; d < 4; ++d)
+    const char* nm[8] = {"full", "math,no-store", "no-epilogue", "store,no-math", "no-ep,no-mfma", "no-ep,no-dma",
+                         "full,odd+6us", "full,odd+12us"};
+    for (int d = 0; d < 8; ++d)
       printf("   %-14s %8.1f us  %7.1f TF/s  per-round %.2f us\n", nm[d], best[d] * 1e3, tf / (best[d] * 1e-3),
              best[d] * 1e3 / __builtin_ceil(rounds));
     fflush(stdout);
