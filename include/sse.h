@@ -232,8 +232,10 @@ int sse_attention(const void* d_qkv, void* d_out, int B, int T, int H, int nh, i
  *     LayerNorm'd in the epilogue from rpart [M][3] float2 partials and rln_w / rln_b [N];
  *   opart [M][N / 256] float2: (mean, M2) of every 256 output columns of each written row;
  * written to cf (fp32) and / or ct (dtype: bf16, fp16 or fp32) with row stride ldc >= N.  dtype:
- * SSE_DTYPE_BF16, SSE_DTYPE_FP16 (fp16 operands, 8-phase kernels only) or SSE_DTYPE_F32.  The dispatch is
- * the model's own (launch_gemm<T>): a shape / field combination no kernel takes returns SSE_ERR_INVALID. */
+ * SSE_DTYPE_BF16, SSE_DTYPE_FP16 (fp16 operands, 8-phase kernels only), SSE_DTYPE_F32, or SSE_DTYPE_FP8: a / b
+ * MX-fp8 operands with their tiled scales a_scale / b_scale (sse_mx_quantize), ldc == N, out bf16 ct (optionally
+ * with the bf16 residual stream resid_t, in place as the Whisper fc2 runs it) or fp32 cf.  The dispatch is the
+ * model's own (launch_gemm<T> / launch_gemm8_mx): a combination no kernel takes returns SSE_ERR_INVALID. */
 typedef struct sse_gemm_desc {
   int dtype, M, N, K, ldc, act, apart_nt;
   float ln_eps;
@@ -251,6 +253,8 @@ typedef struct sse_gemm_desc {
   float* cf;
   void* ct;
   const void* zero;   /* >= 64 zero bytes of device memory */
+  const uint8_t* a_scale;   /* SSE_DTYPE_FP8 only */
+  const uint8_t* b_scale;
 } sse_gemm_desc;
 int sse_gemm_ex(const sse_gemm_desc* d, void* stream);
 

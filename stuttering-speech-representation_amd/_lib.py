@@ -57,7 +57,7 @@ class sse_gemm_desc(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in ("dtype", "M", "N", "K", "ldc", "act", "apart_nt")] + \
         [("ln_eps", ctypes.c_float)] + \
         [(n, ctypes.c_void_p) for n in ("a", "b", "bias", "acol", "apart", "resid", "resid_t", "rpart", "rln_w",
-                                         "rln_b", "opart", "cf", "ct", "zero")]
+                                         "rln_b", "opart", "cf", "ct", "zero", "a_scale", "b_scale")]
 
 
 class sse_cfg(ctypes.Structure):

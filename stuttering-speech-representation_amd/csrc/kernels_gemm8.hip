@@ -155,14 +155,16 @@ SSE_DEV i32x8 g8_cat(bf16x8 lo, bf16x8 hi) {
 }
 
 // DBG = 1 (timing experiments only, not launched by the library): no epilogue, a checksum keeps the MFMAs live.
-template <bool RES, bool Q8 = false>
+template <bool RES, bool Q8 = false, bool RB = false>
 SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, int n0, int wm, int wn,
                                 int q, int r16);
 
 // TR = true: the MFMAs compute C^T blocks (the B fragment is the MFMA's A operand), so every
 // lane ends up holding 4 consecutive output columns of one row and the epilogue stores straight
 // from registers (see g8_epilogue_direct).  TR = false: C blocks, LDS-staged epilogue.
-template <int DBG, bool TR, bool NT, bool MX = false>
+// RBE (MX, TR): this instantiation's epilogue is the bf16-residual one only (a kernel holding both it and the
+// fp8-out epilogue spilled 178 VGPRs).
+template <int DBG, bool TR, bool NT, bool MX = false, bool RBE = false>
 __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[MX ? G8_SMEM_MX : G8_SMEM];   // the ONLY shared object
   const int lane = threadIdx.x & 63;
@@ -424,8 +426,9 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
   }
 
   if constexpr (TR) {
-    if constexpr (MX) {   // no residual on this path (launch_gemm8_mx): fp8 (Q8) or bf16 / fp32 out
-      if (g.c_scale) g8_epilogue_direct<false, true>(g, acc, m0, n0, wm, wn, q, r16);
+    if constexpr (MX) {   // fp8 (Q8) or bf16 / fp32 out; the bf16 residual stream in place (fc2, RB)
+      if constexpr (RBE) g8_epilogue_direct<true, false, true>(g, acc, m0, n0, wm, wn, q, r16);
+      else if (g.c_scale) g8_epilogue_direct<false, true>(g, acc, m0, n0, wm, wn, q, r16);
       else g8_epilogue_direct<false>(g, acc, m0, n0, wm, wn, q, r16);
     } else {
       if (g.resid) g8_epilogue_direct<true>(g, acc, m0, n0, wm, wn, q, r16);
@@ -595,10 +598,13 @@ SSE_DEV int g8p_tile(int b, int r, int G, int n_tiles) {
 // the mi = 0 stores go out.
 // RES = false compiles the residual out (the caller guarantees g.resid == nullptr).
 // Q8 = true: Ct is MX-fp8 (e4m3 + g.c_scale, see store_half_q8).
-template <bool RES, bool Q8>
+// RB = true (with RES): the residual is the bf16 stream g.resid_t (MX fc2, in place: resid_t == Ct), read in the
+// store layout (one 16-B load per (i, ni)) and redistributed with the inverse v_permlane16_swap when it is used;
+// the same fp32 expression as the LDS-staged epilogue (o = acc + bias; o += r), so the results are bit-identical.
+template <bool RES, bool Q8, bool RB>
 SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, int n0, int wm, int wn,
                                 int q, int r16) {
-  const bool has_bias = g.bias != nullptr, has_res = RES && g.resid != nullptr;
+  const bool has_bias = g.bias != nullptr, has_res = RES && (RB ? g.resid_t != nullptr : g.resid != nullptr);
   const bool ln = RES && (g.rstats != nullptr || g.rpart != nullptr);
   const bool gelu = g.act == ACT_GELU, gelu_fast = g.act == ACT_GELU_FAST;
   f32x4 bv[2][2], lw[2][2], lb[2][2];
@@ -612,6 +618,7 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
       lb[ni][j] = ln ? *(const f32x4*)(g.rln_b + n) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   f32x4 rv[4][2][2];
+  uint4 rvb[4][2];   // RB: the raw 16-B store-layout rows, unpacked where they are used
   float2 st[4];
   auto load_half = [&](int mi) {
     if (!has_res) return;
@@ -621,10 +628,15 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
       const int mc = m < g.M ? m : 0;
       const long long rrow = g.resid_rows ? (long long)(mc % g.resid_rows) * g.ldc : (long long)mc * g.ldc;
       #pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
-        #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          rv[i][ni][j] = *(const f32x4*)(g.resid + rrow + n0 + ni * 128 + wn * 32 + j * 16 + q * 4);
+      for (int ni = 0; ni < 2; ++ni) {
+        if constexpr (RB) {
+          rvb[i][ni] = *(const uint4*)(g.resid_t + rrow + n0 + ni * 128 + wn * 32 + (q & 1) * 16 + (q >> 1) * 8);
+        } else {
+          #pragma unroll
+          for (int j = 0; j < 2; ++j)
+            rv[i][ni][j] = *(const f32x4*)(g.resid + rrow + n0 + ni * 128 + wn * 32 + j * 16 + q * 4);
+        }
+      }
       st[i] = !ln ? make_float2(0.f, 1.f) : (g.rstats ? g.rstats[mc] : ln_part_stats_n<3>(g.rpart, mc, g.ln_eps));
     }
   };
@@ -664,7 +676,15 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
             o = f32x4{lo.x, lo.y, hi.x, hi.y};
           }
           if (has_res) {
-            f32x4 r = rv[i][ni][j];
+            f32x4 r;
+            if constexpr (RB) {
+              const uint4 v = rvb[i][ni];
+              const auto x = __builtin_amdgcn_permlane16_swap(v.x, v.z, false, false);
+              const auto y = __builtin_amdgcn_permlane16_swap(v.y, v.w, false, false);
+              r = unpack_h4<false>(j ? make_uint2(x[1], y[1]) : make_uint2(x[0], y[0]));
+            } else {
+              r = rv[i][ni][j];
+            }
             if (ln) {   // LayerNorm of the residual, the exact expression of layernorm_kernel
               #pragma unroll
               for (int e = 0; e < 4; ++e) r[e] = fmaf((r[e] - st[i].x) * st[i].y, lw[ni][j][e], lb[ni][j][e]);
@@ -1927,11 +1947,17 @@ int launch_gemm8_mx(const GemmArgs& a, hipStream_t s) {
   if (a.c_scale && (a.Cf || !a.Ct)) return -3;
   dim3 grid((unsigned)(((a.M + 255) / 256) * (a.N / 256)));
   // Non-persistent for every MX shape: the persistent kernel exceeds 256 VGPRs with the MX operand
-  // tuples and would spill inside the counted-vmcnt main loop.  Without a residual the MFMAs
-  // compute C^T and the epilogue stores from registers (no LDS round trip; OPT_GEMM_MX_STAGED
-  // keeps the LDS-staged epilogue for A/B runs); residual GEMMs take the staged epilogue.
+  // tuples and would spill inside the counted-vmcnt main loop.  Without a residual, or with the bf16
+  // residual stream (fc2, round 5), the MFMAs compute C^T and the epilogue stores from registers (no LDS
+  // round trip; OPT_GEMM_MX_STAGED keeps the LDS-staged epilogue for A/B runs); fp32 residuals take the
+  // staged epilogue.
   if (a.resid && a.resid_t) return -3;
-  if (!a.resid && !a.resid_t && !sse_opt(OPT_GEMM_MX_STAGED))
+  // register-direct (C^T) epilogue: no residual, or the bf16 residual stream (fc2: resid_t in place, no fp32 out)
+  const bool direct = !a.resid && (!a.resid_t || (a.Ct && !a.Cf && !a.c_scale && !a.rstats && !a.rpart && !a.opart &&
+                                                   !a.resid_rows));
+  if (direct && a.resid_t && !sse_opt(OPT_GEMM_MX_STAGED))
+    hipLaunchKernelGGL((gemm8_kernel<0, true, false, true, true>), grid, dim3(512), 0, s, a);
+  else if (direct && !sse_opt(OPT_GEMM_MX_STAGED))
     hipLaunchKernelGGL((gemm8_kernel<0, true, false, true>), grid, dim3(512), 0, s, a);
   else
     hipLaunchKernelGGL((gemm8_kernel<0, false, false, true>), grid, dim3(512), 0, s, a);

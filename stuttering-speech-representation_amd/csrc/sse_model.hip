@@ -2002,7 +2002,18 @@ int sse_gemm(int dtype, const void* d_a, const void* d_b, const float* d_bias, c
 int sse_gemm_ex(const sse_gemm_desc* d, void* stream) {
   if (!d || !d->a || !d->b || !d->zero || d->M <= 0 || d->N <= 0 || d->K <= 0 || d->ldc < d->N || (!d->cf && !d->ct))
     return SSE_ERR_INVALID;
-  if (d->dtype != SSE_DTYPE_BF16 && d->dtype != SSE_DTYPE_FP16 && d->dtype != SSE_DTYPE_F32) return SSE_ERR_INVALID;
+  if (d->dtype != SSE_DTYPE_BF16 && d->dtype != SSE_DTYPE_FP16 && d->dtype != SSE_DTYPE_F32 && d->dtype != SSE_DTYPE_FP8)
+    return SSE_ERR_INVALID;
+  if (d->dtype == SSE_DTYPE_FP8) {
+    if (!d->a_scale || !d->b_scale || d->ldc != d->N || d->apart || d->rpart || d->opart) return SSE_ERR_INVALID;
+    if (d->N % 256 || d->K % 128) return SSE_ERR_UNSUPPORTED;
+    GemmArgs g{};
+    g.A = d->a; g.a_scale = d->a_scale; g.B = d->b; g.b_scale = d->b_scale; g.M = d->M; g.N = d->N; g.K = d->K;
+    g.rows_per_seg = d->M; g.lda = d->K; g.bias = d->bias; g.resid = d->resid; g.resid_t = (const bf16*)d->resid_t;
+    g.Cf = d->cf; g.Ct = d->ct; g.ldc = d->N; g.act = d->act; g.zero = d->zero;
+    const int rc = launch_gemm8_mx(g, (hipStream_t)stream);
+    return rc == -3 ? SSE_ERR_INVALID : (rc ? SSE_ERR_HIP : SSE_OK);
+  }
   if ((d->apart != nullptr) != (d->acol != nullptr) || (d->rpart && (!d->rln_w || !d->rln_b)) ||
       (d->resid && d->resid_t) || (d->rpart && !d->resid && !d->resid_t))
     return SSE_ERR_INVALID;

@@ -114,6 +114,7 @@ def _gemm_ex(dtype_code, a, b, M, N, K, ldc, **kw):
     d.a, d.b, d.zero = a.data_ptr(), b.data_ptr(), _zero().data_ptr()
     for k, v in kw.items():
         setattr(d, k, None if v is None else (v if isinstance(v, int) else v.data_ptr()))
+    # (resid_t / ct may be passed as raw pointers: the in-place residual forms)
     rc = _lib.lib().sse_gemm_ex(ctypes.byref(d), _stream())
     _lib.check(rc, "sse_gemm_ex")
 
@@ -338,3 +339,35 @@ def test_embed_output_and_workspace_guard_bands(wavlm_sd, dtype):
     out2.check("pooled ragged")
     assert bool((ws[need:] == PAT[torch.uint8]).all()), "ragged: store past the workspace"
 
+
+
+@pytest.mark.parametrize("M", [257, 511, 3000])
+def test_gemm_mx_bf16_residual_in_place(M):
+    """The Whisper fp8 fc2 form: MX-fp8 operands, the bf16 residual stream read and rewritten in place
+    (resid_t == ct).  Round 5 moved it from the LDS-staged epilogue to the register-direct one
+    (gemm8_kernel<.., MX, RBE>): the same fp32 expression (acc + bias, + residual, rounded once), so the
+    result equals the staged kernel's (option gemm_mx_staged = 1) bit for bit; guard rows stay untouched
+    and the values match the dequantised product."""
+    from oracle import mx
+    from ssr_amd import _lib
+    N, K = 512, 384
+    rng = np.random.default_rng(M + 1)
+    a = rng.standard_normal((M, K)).astype(np.float32)
+    bw = (rng.standard_normal((N, K)) / np.sqrt(K)).astype(np.float32)
+    qa, sa, ea = mx.quantize(a, 0)
+    qb, sb, eb = mx.quantize(bw, 1)
+    dev = lambda v: torch.from_numpy(v).cuda()
+    qa_, sa_, qb_, sb_ = dev(qa), dev(sa), dev(qb), dev(sb)
+    bias = torch.from_numpy(rng.standard_normal(N).astype(np.float32)).cuda()
+    res0 = torch.from_numpy(rng.standard_normal((M, N)).astype(np.float32)).cuda().to(torch.bfloat16)
+    ref = torch.from_numpy(mx.dequantize(qa, ea) @ mx.dequantize(qb, eb).T).cuda() + bias + res0.float()
+    outs = []
+    for staged in (0, 1):
+        c = Guarded(M, N, N, torch.bfloat16)
+        c.out.copy_(res0)
+        with _lib.option("gemm_mx_staged", staged):
+            _gemm_ex(2, qa_, qb_, M, N, K, N, bias=bias, resid_t=c.ptr(), ct=c.ptr(), a_scale=sa_, b_scale=sb_)
+        c.check(f"mx resid staged={staged}")
+        outs.append(c.out.clone())
+    assert torch.equal(outs[0], outs[1])
+    assert _rel(outs[0], ref) <= 1e-2
