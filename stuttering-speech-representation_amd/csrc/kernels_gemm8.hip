@@ -155,16 +155,18 @@ SSE_DEV i32x8 g8_cat(bf16x8 lo, bf16x8 hi) {
 }
 
 // DBG = 1 (timing experiments only, not launched by the library): no epilogue, a checksum keeps the MFMAs live.
-template <bool RES, bool Q8 = false, bool RB = false>
+template <bool RES, bool Q8 = false, bool RB = false, int FX = 0>
 SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, int n0, int wm, int wn,
                                 int q, int r16);
 
 // TR = true: the MFMAs compute C^T blocks (the B fragment is the MFMA's A operand), so every
 // lane ends up holding 4 consecutive output columns of one row and the epilogue stores straight
 // from registers (see g8_epilogue_direct).  TR = false: C blocks, LDS-staged epilogue.
-// RBE (MX, TR): this instantiation's epilogue is the bf16-residual one only (a kernel holding both it and the
-// fp8-out epilogue spilled 178 VGPRs).
-template <int DBG, bool TR, bool NT, bool MX = false, bool RBE = false>
+// MXE (MX, TR): the epilogue fixed at compile time -- 0: runtime selection (tests, any combination); 1: fc1
+// (bias, ACT_GELU_FAST, MX-fp8 out); 2: fc2 (bias, the bf16 residual stream in place; a kernel holding both
+// it and the fp8-out epilogue spilled 178 VGPRs); 3: qkv (bias, bf16 out).  Runtime selects in the persistent
+// bf16 kernel's epilogue measured +5-6 %.
+template <int DBG, bool TR, bool NT, bool MX = false, int MXE = 0>
 __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[MX ? G8_SMEM_MX : G8_SMEM];   // the ONLY shared object
   const int lane = threadIdx.x & 63;
@@ -427,7 +429,9 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
 
   if constexpr (TR) {
     if constexpr (MX) {   // fp8 (Q8) or bf16 / fp32 out; the bf16 residual stream in place (fc2, RB)
-      if constexpr (RBE) g8_epilogue_direct<true, false, true>(g, acc, m0, n0, wm, wn, q, r16);
+      if constexpr (MXE == 1) g8_epilogue_direct<false, true, false, 1>(g, acc, m0, n0, wm, wn, q, r16);
+      else if constexpr (MXE == 2) g8_epilogue_direct<true, false, true, 2>(g, acc, m0, n0, wm, wn, q, r16);
+      else if constexpr (MXE == 3) g8_epilogue_direct<false, false, false, 2>(g, acc, m0, n0, wm, wn, q, r16);
       else if (g.c_scale) g8_epilogue_direct<false, true>(g, acc, m0, n0, wm, wn, q, r16);
       else g8_epilogue_direct<false>(g, acc, m0, n0, wm, wn, q, r16);
     } else {
@@ -601,12 +605,15 @@ SSE_DEV int g8p_tile(int b, int r, int G, int n_tiles) {
 // RB = true (with RES): the residual is the bf16 stream g.resid_t (MX fc2, in place: resid_t == Ct), read in the
 // store layout (one 16-B load per (i, ni)) and redistributed with the inverse v_permlane16_swap when it is used;
 // the same fp32 expression as the LDS-staged epilogue (o = acc + bias; o += r), so the results are bit-identical.
-template <bool RES, bool Q8, bool RB>
+// FX: 0 = bias / activation read from g at run time; 1 = bias + ACT_GELU_FAST, 2 = bias, no activation (fixed at
+// compile time: the caller guarantees g agrees)
+template <bool RES, bool Q8, bool RB, int FX>
 SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, int n0, int wm, int wn,
                                 int q, int r16) {
-  const bool has_bias = g.bias != nullptr, has_res = RES && (RB ? g.resid_t != nullptr : g.resid != nullptr);
-  const bool ln = RES && (g.rstats != nullptr || g.rpart != nullptr);
-  const bool gelu = g.act == ACT_GELU, gelu_fast = g.act == ACT_GELU_FAST;
+  const bool has_bias = FX ? true : g.bias != nullptr;
+  const bool has_res = RES && (FX ? true : (RB ? g.resid_t != nullptr : g.resid != nullptr));
+  const bool ln = RES && !FX && (g.rstats != nullptr || g.rpart != nullptr);
+  const bool gelu = !FX && g.act == ACT_GELU, gelu_fast = FX == 1 || (!FX && g.act == ACT_GELU_FAST);
   f32x4 bv[2][2], lw[2][2], lb[2][2];
   #pragma unroll
   for (int ni = 0; ni < 2; ++ni)
@@ -1955,11 +1962,18 @@ int launch_gemm8_mx(const GemmArgs& a, hipStream_t s) {
   // register-direct (C^T) epilogue: no residual, or the bf16 residual stream (fc2: resid_t in place, no fp32 out)
   const bool direct = !a.resid && (!a.resid_t || (a.Ct && !a.Cf && !a.c_scale && !a.rstats && !a.rpart && !a.opart &&
                                                    !a.resid_rows));
-  if (direct && a.resid_t && !sse_opt(OPT_GEMM_MX_STAGED))
-    hipLaunchKernelGGL((gemm8_kernel<0, true, false, true, true>), grid, dim3(512), 0, s, a);
-  else if (direct && !sse_opt(OPT_GEMM_MX_STAGED))
-    hipLaunchKernelGGL((gemm8_kernel<0, true, false, true>), grid, dim3(512), 0, s, a);
-  else
+  const bool plain = a.bias && !a.resid && !a.Cf && a.Ct && !a.rstats && !a.rpart && !a.opart && !a.resid_rows;
+  if (direct && !sse_opt(OPT_GEMM_MX_STAGED)) {
+    if (a.resid_t)   // fc2 (direct implies Ct, no Cf / fp8 out / LayerNorm)
+      hipLaunchKernelGGL((gemm8_kernel<0, true, false, true, 2>), grid, dim3(512), 0, s, a);
+    else if (plain && a.c_scale && a.act == ACT_GELU_FAST)   // fc1
+      hipLaunchKernelGGL((gemm8_kernel<0, true, false, true, 1>), grid, dim3(512), 0, s, a);
+    else if (plain && !a.c_scale && a.act == ACT_NONE)      // qkv
+      hipLaunchKernelGGL((gemm8_kernel<0, true, false, true, 3>), grid, dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL((gemm8_kernel<0, true, false, true>), grid, dim3(512), 0, s, a);
+  } else {
     hipLaunchKernelGGL((gemm8_kernel<0, false, false, true>), grid, dim3(512), 0, s, a);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

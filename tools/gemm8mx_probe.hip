@@ -31,7 +31,7 @@ __global__ void fill_u8(unsigned char* p, long long n, unsigned seed, int scale_
 
 typedef void (*kfn)(GemmArgs);
 
-struct Shape { const char* name; int M, N, K; };
+struct Shape { const char* name; int M, N, K; int mode = 0; };   // mode 1: fc1 (GELU, MX-fp8 out); 2: fc2 (bf16 residual)
 
 int main() {
   int cus = 256;
@@ -39,14 +39,17 @@ int main() {
   const Shape shapes[] = {
       {"qkv", 192000, 3840, 1280}, {"ffn1", 192000, 5120, 1280}, {"ffn2", 192000, 1280, 5120},
       {"k640", 192000, 1280, 640}, {"k1280", 192000, 1280, 1280}, {"k2560", 192000, 1280, 2560},
+      {"fc1_q8", 192000, 5120, 1280, 1}, {"fc2_res", 192000, 1280, 5120, 2},
   };
   const long long maxA = 192000LL * 5120, maxB = 5120LL * 5120, maxC = 192000LL * 5120;
-  unsigned char *a, *b, *sa, *sb;
+  unsigned char *a, *b, *sa, *sb, *cs;
   bf16* c;
+  float* bias;
   void* zero;
   CK(hipMalloc(&a, maxA)); CK(hipMalloc(&b, maxB)); CK(hipMalloc(&c, maxC * 2));
   CK(hipMalloc(&sa, maxA / 32 + 4096)); CK(hipMalloc(&sb, maxB / 32 + 4096));
   CK(hipMalloc(&zero, 256)); CK(hipMemset(zero, 0, 256));
+  CK(hipMalloc(&cs, maxC / 32 + 4096)); CK(hipMalloc(&bias, 5120 * 4)); CK(hipMemset(bias, 0, 5120 * 4));
   hipLaunchKernelGGL(fill_u8, dim3(2048), dim3(256), 0, 0, a, maxA, 17u, 0);
   hipLaunchKernelGGL(fill_u8, dim3(2048), dim3(256), 0, 0, b, maxB, 91u, 0);
   hipLaunchKernelGGL(fill_u8, dim3(2048), dim3(256), 0, 0, sa, maxA / 32 + 4096, 5u, 1);
@@ -58,13 +61,17 @@ int main() {
   for (const Shape& s : shapes) {
     GemmArgs g{};
     g.A = a; g.B = b; g.M = s.M; g.N = s.N; g.K = s.K; g.rows_per_seg = s.M; g.lda = s.K;
-    g.Ct = c; g.ldc = s.N; g.act = ACT_NONE; g.zero = zero; g.a_scale = sa; g.b_scale = sb;
+    g.Ct = c; g.ldc = s.N; g.act = ACT_NONE; g.zero = zero; g.a_scale = sa; g.b_scale = sb; g.bias = bias;
+    if (s.mode == 1) { g.act = ACT_GELU_FAST; g.c_scale = cs; g.bias = bias; }
+    if (s.mode == 2) { g.resid_t = c; g.bias = bias; }
     const int n_tiles = ((s.M + 255) / 256) * (s.N / 256);
     const double tf = 2.0 * s.M * s.N * s.K / 1e12;
     double best[2] = {1e30, 1e30};
     for (int r = 0; r < ROUNDS; ++r)
       for (int dbg = 0; dbg < 2; ++dbg) {
-        kfn k = dbg ? gemm8_kernel<1, true, false, true> : gemm8_kernel<0, true, false, true>;
+        kfn k = dbg ? gemm8_kernel<1, true, false, true>
+                    : (s.mode == 2 ? gemm8_kernel<0, true, false, true, 2>
+                                   : (s.mode == 1 ? gemm8_kernel<0, true, false, true, 1> : gemm8_kernel<0, true, false, true, 3>));
         for (int w = 0; w < 2; ++w) hipLaunchKernelGGL(k, dim3(n_tiles), dim3(512), 0, 0, g);
         CK(hipEventRecord(e0, 0));
         for (int i = 0; i < IT; ++i) hipLaunchKernelGGL(k, dim3(n_tiles), dim3(512), 0, 0, g);
