@@ -223,6 +223,16 @@ int sse_gemm(int dtype, const void* d_a, const void* d_b, const float* d_bias, c
 int sse_attention(const void* d_qkv, void* d_out, int B, int T, int H, int nh, int ldq, float scale, int q_log2,
                   void* stream);
 
+/* The fp8 encoder's attention (test hook; the SSE_DTYPE_FP8 Whisper path's default, option fp8_attn_bf16 = 1
+ * keeps the bf16 one): d_out bf16 [B*T][H] = softmax(q k^T) v per head (nh heads of 64; q carries the softmax
+ * scale * log2(e), so the scores are log2-domain logits), q | k MX-fp8 [B*T][2H] e4m3 with their E8M0 scales
+ * row-major [B*T][2H / 32] (blocks of 32 columns: the c_scale_rm output of sse_gemm_ex), v bf16 [B*T][H],
+ * d_vamax [B][H] the float bits of max |bf16 v| per (clip, column) (the vamax output of sse_gemm_ex).  Both
+ * products on the block-scaled fp8 MFMA: P in e4m3, V in e4m3 with one power-of-two scale per (clip, head).
+ * REF/whisper_embeddings_large.py:250-254 (fp8 encoder) -> HF WhisperAttention (SDPA). */
+int sse_attention_f8(const uint8_t* d_qk, const uint8_t* d_qk_scale, const void* d_v, const uint32_t* d_vamax,
+                     void* d_out, int B, int T, int H, int nh, void* stream);
+
 /* Every epilogue form of the path's GEMMs behind one test hook (guard-band and epilogue tests; no
  * reference counterpart).  C[M][N] = A[M][K] . B[N][K]^T with, by the non-null fields:
  *   bias[N]; act (0 none, 1 erf-GELU, 2 the bf16 path's GELU);
@@ -255,6 +265,18 @@ typedef struct sse_gemm_desc {
   const void* zero;   /* >= 64 zero bytes of device memory */
   const uint8_t* a_scale;   /* SSE_DTYPE_FP8 only */
   const uint8_t* b_scale;
+  /* SSE_DTYPE_FP8 outputs of the fp8 attention's operands: c_scale != NULL makes ct MX-fp8 (e4m3) with its
+   * scales in c_scale, row-major [M][N / 32] when c_scale_rm = 1 (else the tiled A layout of a following GEMM);
+   * vamax != NULL (bf16 ct): atomicMax of the float bits of max |bf16 C[m][n]| over each segment of vamax_rows
+   * rows into vamax [M / vamax_rows][N] (zeroed by the caller) */
+  uint8_t* c_scale;
+  uint32_t* vamax;
+  int c_scale_rm, vamax_rows;
+  /* n_split > 0 (SSE_DTYPE_FP8, the encoder's fused QKV form): columns [0, n_split) go to ct as MX-fp8 with
+   * row-major c_scale (c_scale_rm = 1, ldc = n_split), columns [n_split, N) to ct2 [M][ldc2] bf16 (column
+   * n - n_split) with their vamax [M / vamax_rows][N - n_split] */
+  void* ct2;
+  int n_split, ldc2;
 } sse_gemm_desc;
 int sse_gemm_ex(const sse_gemm_desc* d, void* stream);
 

@@ -34,7 +34,7 @@ EXPORTED = ("sse_weight_floats", "sse_model_create", "sse_model_destroy", "sse_o
             "sse_resample", "sse_augment", "sse_mx_scale_bytes", "sse_mx_scale_offset", "sse_mx_quantize",
             "sse_mx_quantize_host", "sse_gemm_mx", "sse_pitch_shift_workspace_bytes", "sse_pitch_shift",
             "sse_set_option", "sse_get_option", "sse_embed_ragged", "sse_gemm_lnfold", "sse_check_range",
-            "sse_attention", "sse_gemm_ex")
+            "sse_attention", "sse_gemm_ex", "sse_attention_f8")
 
 
 class SSEError(RuntimeError):
@@ -57,7 +57,10 @@ class sse_gemm_desc(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in ("dtype", "M", "N", "K", "ldc", "act", "apart_nt")] + \
         [("ln_eps", ctypes.c_float)] + \
         [(n, ctypes.c_void_p) for n in ("a", "b", "bias", "acol", "apart", "resid", "resid_t", "rpart", "rln_w",
-                                         "rln_b", "opart", "cf", "ct", "zero", "a_scale", "b_scale")]
+                                         "rln_b", "opart", "cf", "ct", "zero", "a_scale", "b_scale", "c_scale",
+                                         "vamax")] + \
+        [(n, ctypes.c_int32) for n in ("c_scale_rm", "vamax_rows")] + \
+        [("ct2", ctypes.c_void_p)] + [(n, ctypes.c_int32) for n in ("n_split", "ldc2")]
 
 
 class sse_cfg(ctypes.Structure):
@@ -162,6 +165,9 @@ def lib() -> ctypes.CDLL:
     if hasattr(L, "sse_gemm_ex"):   # (absent from pre-round-5 builds loaded for A/B runs via set_lib_path)
         L.sse_gemm_ex.argtypes = [ctypes.POINTER(sse_gemm_desc), vp]
         L.sse_gemm_ex.restype = i32
+    if hasattr(L, "sse_attention_f8"):
+        L.sse_attention_f8.argtypes = [vp, vp, vp, vp, vp, i32, i32, i32, i32, vp]
+        L.sse_attention_f8.restype = i32
     L.sse_gemm_lnfold.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, ctypes.c_float, vp, vp]
     L.sse_gemm_lnfold.restype = i32
     L.sse_whisper_embed.argtypes = [vp, vp, i32, i32, vp, i32, vp, vp, i32, vp, vp, sz, vp]

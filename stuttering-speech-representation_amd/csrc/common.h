@@ -283,6 +283,7 @@ enum {
   OPT_ATTN_SHORT,       // short-T attention: 0 head-pipelined (default), 1 one head at a time (bit-identity tests)
   OPT_ATTN_LONG,        // no-bias (Whisper) flash attention: 0 32x32 swapped form, 2 query blocks per wave (default);
                         // 2 the same with one; 1 the 16x16 flash2 kernel
+  OPT_FP8_ATTN_BF16,    // 1: the fp8 (MX) Whisper path keeps the bf16 QKV output and the bf16 flash attention
   OPT_COUNT
 };
 int sse_opt(int id);
@@ -352,6 +353,19 @@ struct GemmArgs {
   // plain fp16 GEMM (SSE_DTYPE_FP16): A, B, Ct and resid_t are fp16 instead of bf16, the f16 MFMA, no
   // scale; otherwise exactly the bf16 path (launch_gemm<f16> sets it)
   int h16;
+  // MX-fp8 out with ROW-MAJOR scales (launch_gemm8_mx): c_scale[m * (N / 32) + n / 32] instead of the A tile
+  // layout (the fp8 attention's Q / K operand, read per row)
+  int c_scale_rm;
+  // bf16 out of launch_gemm8_mx: per-segment column amax of the stored values, atomicMax of the float bits of
+  // max |bf16(C[m][n])| over the rows m of segment m / vamax_rows into vamax[(m / vamax_rows) * N + n] (the fp8
+  // attention's per-(clip, column) V scale; the caller zeroes vamax)
+  unsigned* vamax;
+  int vamax_rows;
+  // the fp8 attention's fused QKV GEMM (launch_gemm8_mx, n_split > 0): columns [0, n_split) are written as the
+  // MX-fp8 Ct with row-major c_scale (ldc = n_split), columns [n_split, N) as bf16 into ct2 [M][ldc2] (column
+  // n - n_split) with vamax over them (vamax[s][n - n_split])
+  void* ct2;
+  int n_split, ldc2;
 };
 
 // (mean, rstd) of a row of 256 * NT values from its per-tile partials (mean_t, M2_t), Chan's pairwise

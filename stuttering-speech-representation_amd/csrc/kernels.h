@@ -84,7 +84,15 @@ struct AttnArgs {
                          // flash3 kernel (which requires it) takes the scores as log2-domain logits
   int out3;              // fp32 kernel: write the output tripled for a split-fp16 GEMM ([hi | lo' | hi],
                          // rows of 3H fp16, x3_split4) instead of fp32 (SSE_DTYPE_FP16X3)
+  // fp8 Whisper attention (launch_attention_f8; qkv unused): Q | K MX-fp8 [B*T][2H] bytes (q carries
+  // scale * log2 e: q_log2), their E8M0 scales row-major [B*T][2H / 32]; V bf16 [B*T][H]; vamax [B][H]
+  // the float bits of max |V| per (clip, column) (the V GEMM's GemmArgs::vamax)
+  const unsigned char* qk8;
+  const unsigned char* qks;
+  const void* v16;
+  const unsigned* vamax;
 };
+int launch_attention_f8(const AttnArgs& a, int B, hipStream_t s);
 template <typename T>
 int launch_attention(const AttnArgs& a, int B, hipStream_t s);
 

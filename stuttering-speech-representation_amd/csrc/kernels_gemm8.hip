@@ -52,6 +52,7 @@ typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef short v2i16g8 __attribute__((ext_vector_type(2)));
 
 // phase k = 4t + p (k >= -8) -> the (tile, half) whose LDS-DMA it issues
 SSE_DEV void g8_target(int k, int& tile, int& half) {
@@ -155,7 +156,7 @@ SSE_DEV i32x8 g8_cat(bf16x8 lo, bf16x8 hi) {
 }
 
 // DBG = 1 (timing experiments only, not launched by the library): no epilogue, a checksum keeps the MFMAs live.
-template <bool RES, bool Q8 = false, bool RB = false, int FX = 0>
+template <bool RES, bool Q8 = false, bool RB = false, int FX = 0, bool RSC = false, bool VAM = false>
 SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, int n0, int wm, int wn,
                                 int q, int r16);
 
@@ -164,8 +165,9 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
 // from registers (see g8_epilogue_direct).  TR = false: C blocks, LDS-staged epilogue.
 // MXE (MX, TR): the epilogue fixed at compile time -- 0: runtime selection (tests, any combination); 1: fc1
 // (bias, ACT_GELU_FAST, MX-fp8 out); 2: fc2 (bias, the bf16 residual stream in place; a kernel holding both
-// it and the fp8-out epilogue spilled 178 VGPRs); 3: qkv (bias, bf16 out).  Runtime selects in the persistent
-// bf16 kernel's epilogue measured +5-6 %.
+// it and the fp8-out epilogue spilled 178 VGPRs); 3: qkv (bias, bf16 out); 4: the fp8 attention's Q / K (bias,
+// MX-fp8 out, row-major scales); 5: its V (bias, bf16 out, per-clip column amax).  Runtime selects in the
+// persistent bf16 kernel's epilogue measured +5-6 %.
 template <int DBG, bool TR, bool NT, bool MX = false, int MXE = 0>
 __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[MX ? G8_SMEM_MX : G8_SMEM];   // the ONLY shared object
@@ -432,6 +434,23 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
       if constexpr (MXE == 1) g8_epilogue_direct<false, true, false, 1>(g, acc, m0, n0, wm, wn, q, r16);
       else if constexpr (MXE == 2) g8_epilogue_direct<true, false, true, 2>(g, acc, m0, n0, wm, wn, q, r16);
       else if constexpr (MXE == 3) g8_epilogue_direct<false, false, false, 2>(g, acc, m0, n0, wm, wn, q, r16);
+      else if constexpr (MXE == 4) g8_epilogue_direct<false, true, false, 2, true>(g, acc, m0, n0, wm, wn, q, r16);
+      else if constexpr (MXE == 5) g8_epilogue_direct<false, false, false, 2, false, true>(g, acc, m0, n0, wm, wn, q, r16);
+      else if constexpr (MXE == 6) {   // fused Q|K (MX-fp8, row-major scales) | V (bf16 + vamax): uniform per tile
+        if (n0 < g.n_split) {
+          GemmArgs g1 = g;
+          g1.N = g.n_split;
+          g1.ldc = g.n_split;
+          g8_epilogue_direct<false, true, false, 2, true>(g1, acc, m0, n0, wm, wn, q, r16);
+        } else {   // the V frame: column n - n_split of ct2 / vamax, bias from column n_split on
+          GemmArgs g2 = g;
+          g2.Ct = g.ct2;
+          g2.ldc = g.ldc2;
+          g2.N = g.N - g.n_split;
+          g2.bias = g.bias + g.n_split;
+          g8_epilogue_direct<false, false, false, 2, false, true>(g2, acc, m0, n0 - g.n_split, wm, wn, q, r16);
+        }
+      }
       else if (g.c_scale) g8_epilogue_direct<false, true>(g, acc, m0, n0, wm, wn, q, r16);
       else g8_epilogue_direct<false>(g, acc, m0, n0, wm, wn, q, r16);
     } else {
@@ -607,7 +626,9 @@ SSE_DEV int g8p_tile(int b, int r, int G, int n_tiles) {
 // the same fp32 expression as the LDS-staged epilogue (o = acc + bias; o += r), so the results are bit-identical.
 // FX: 0 = bias / activation read from g at run time; 1 = bias + ACT_GELU_FAST, 2 = bias, no activation (fixed at
 // compile time: the caller guarantees g agrees)
-template <bool RES, bool Q8, bool RB, int FX>
+// RSC (with Q8): the scales row-major, c_scale[m * (N / 32) + n / 32] (GemmArgs::c_scale_rm).
+// VAM (bf16 out): the per-segment column amax of GemmArgs::vamax (see vamax_half below).
+template <bool RES, bool Q8, bool RB, int FX, bool RSC, bool VAM>
 SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, int n0, int wm, int wn,
                                 int q, int r16) {
   const bool has_bias = FX ? true : g.bias != nullptr;
@@ -770,23 +791,115 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
           a = fmaxf(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
         }
         const int e = mx_scale_exp(a);
-        const float inv = mx_inv_scale(e);
-        int x0 = __builtin_amdgcn_cvt_pk_fp8_f32(o0[0] * inv, o0[1] * inv, 0, false);
-        x0 = __builtin_amdgcn_cvt_pk_fp8_f32(o0[2] * inv, o0[3] * inv, x0, true);
-        int x1 = __builtin_amdgcn_cvt_pk_fp8_f32(o1[0] * inv, o1[1] * inv, 0, false);
-        x1 = __builtin_amdgcn_cvt_pk_fp8_f32(o1[2] * inv, o1[3] * inv, x1, true);
+        // e4m3 = RNE(x / 2^(e - 127)) by the scaled conversion (the scale's exponent field only: tools/probe_cvt.hip
+        // checks it against cvt_pk_fp8_f32(x * 2^-E) bit for bit); a block of zeros / denormals (e = 0) divides by
+        // 2^-126 instead of 2^-127
+        const float sc = __builtin_bit_cast(float, (unsigned)(e > 0 ? e : 1) << 23);
+        v2i16g8 w0 = {0, 0}, w1 = {0, 0};
+        w0 = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(w0, o0[0], o0[1], sc, false);
+        w0 = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(w0, o0[2], o0[3], sc, true);
+        w1 = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(w1, o1[0], o1[1], sc, false);
+        w1 = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(w1, o1[2], o1[3], sc, true);
+        const int x0 = __builtin_bit_cast(int, w0), x1 = __builtin_bit_cast(int, w1);
         const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)x0, (unsigned)x1, false, false);
         __builtin_amdgcn_raw_buffer_store_b64(u32x2{sw[0], sw[1]}, ct_rsrc_of(mi, i, 1), lane_off1 + (unsigned)(ni * 128), 0u, 0);
-        scw[mi][ni] |= (unsigned)e << (8 * i);
+        if constexpr (RSC) {   // the row's four q lanes hold the same exponent: lane q == i stores it
+          if (q == i && ok) g.c_scale[(long long)m * (g.N >> 5) + ((n0 + ni * 128 + wn * 32) >> 5)] = (unsigned char)e;
+        } else {
+          scw[mi][ni] |= (unsigned)e << (8 * i);
+        }
       }
     }
   };
+  // VAM: max |C| over this wave's 64 rows of half mi (m = mb + 16 i + r16) per column and row segment
+  // (m / vamax_rows: at most two segments, vamax_rows >= 64), rows >= M excluded.  Per lane the 16 columns
+  // (ni, j, e) are first reduced over its 4 rows, then over the 16 r16 lanes by a halving butterfly (DPP
+  // row_mirror, row_half_mirror, quad xor 2, xor 1: each step keeps half the columns, so lane r16 ends with
+  // column k = r16 = 8 ni + 4 j + e) and rounded to bf16 (RNE is monotone: bf16(max |x|) = max |bf16(x)|).
+  // The atomicMax of the float bits (one per lane and segment) is issued after the last store (vam_flush): an
+  // atomic stays in vmcnt for thousands of cycles under contention, and any later wait would take it along.
+  float vres[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+  int vseg[2][2] = {{-1, -1}, {-1, -1}};
+  auto vamax_half = [&](int mi) {
+    const int R = g.vamax_rows;
+    const int mb = m0 + mi * 128 + wm * 64;
+    if (mb >= g.M) return;
+    const int c0 = mb / R, c1 = min(mb + 63, g.M - 1) / R;
+    #pragma unroll
+    for (int part = 0; part < 2; ++part) {
+      const int cs = c0 + part;
+      if (cs > c1) break;
+      const int lo = cs * R, hi = min(lo + R, g.M);
+      float v[16];
+      if (lo <= mb && hi >= mb + 64) {   // every row of the block in this segment (wave-uniform)
+        #pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          #pragma unroll
+          for (int j = 0; j < 2; ++j)
+            #pragma unroll
+            for (int e = 0; e < 4; ++e)
+              v[ni * 8 + j * 4 + e] = __builtin_elementwise_maximum(
+                  __builtin_elementwise_maximum(fabsf(acc[mi][ni][0][j][e]), fabsf(acc[mi][ni][1][j][e])),
+                  __builtin_elementwise_maximum(fabsf(acc[mi][ni][2][j][e]), fabsf(acc[mi][ni][3][j][e])));
+      } else {
+        bool ok[4];
+        #pragma unroll
+        for (int i = 0; i < 4; ++i) ok[i] = mb + i * 16 + r16 >= lo && mb + i * 16 + r16 < hi;
+        #pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          #pragma unroll
+          for (int j = 0; j < 2; ++j)
+            #pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float t = 0.f;
+              #pragma unroll
+              for (int i = 0; i < 4; ++i) t = __builtin_elementwise_maximum(t, ok[i] ? fabsf(acc[mi][ni][i][j][e]) : 0.f);
+              v[ni * 8 + j * 4 + e] = t;
+            }
+      }
+      auto step = [&](auto hc, int bit, auto ctl) {
+        constexpr int h = decltype(hc)::value;
+        const bool up = (r16 >> bit) & 1;
+        #pragma unroll
+        for (int k = 0; k < h; ++k) {
+          const float snd = up ? v[k] : v[k + h];
+          const float kp = up ? v[k + h] : v[k];
+          const float rc = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(snd), decltype(ctl)::value, 0xF, 0xF, false));
+          v[k] = __builtin_elementwise_maximum(kp, rc);
+        }
+      };
+      step(std::integral_constant<int, 8>{}, 3, std::integral_constant<int, 0x140>{});   // row_mirror
+      step(std::integral_constant<int, 4>{}, 2, std::integral_constant<int, 0x141>{});   // row_half_mirror
+      step(std::integral_constant<int, 2>{}, 1, std::integral_constant<int, 0x4E>{});    // quad [2,3,0,1]
+      step(std::integral_constant<int, 1>{}, 0, std::integral_constant<int, 0xB1>{});    // quad [1,0,3,2]
+      vres[mi][part] = (float)(bf16)v[0];
+      vseg[mi][part] = cs;
+    }
+  };
+  auto vam_flush = [&]() {
+    const int k = r16;
+    const int n = n0 + (k >> 3) * 128 + wn * 32 + ((k >> 2) & 1) * 16 + q * 4 + (k & 3);
+    #pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+      #pragma unroll
+      for (int part = 0; part < 2; ++part)
+        if (vseg[mi][part] >= 0)
+          __hip_atomic_fetch_max(g.vamax + (long long)vseg[mi][part] * g.N + n, __float_as_uint(vres[mi][part]),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
   load_half(0);
   finish_half(0);
+  if constexpr (VAM) vamax_half(0);
   load_half(1);
   if constexpr (Q8) store_half_q8(0); else store_half(0);
   finish_half(1);
-  if constexpr (Q8) {
+  if constexpr (VAM) vamax_half(1);
+  if constexpr (VAM) {
+    store_half(1);
+    vam_flush();
+  } else if constexpr (Q8 && RSC) {
+    store_half_q8(1);
+  } else if constexpr (Q8) {
     store_half_q8(1);
     const int mi = q >> 1, ni = q & 1;
     const unsigned v = mi ? (ni ? scw[1][1] : scw[1][0]) : (ni ? scw[0][1] : scw[0][0]);
@@ -1963,6 +2076,24 @@ int launch_gemm8_mx(const GemmArgs& a, hipStream_t s) {
   const bool direct = !a.resid && (!a.resid_t || (a.Ct && !a.Cf && !a.c_scale && !a.rstats && !a.rpart && !a.opart &&
                                                    !a.resid_rows));
   const bool plain = a.bias && !a.resid && !a.Cf && a.Ct && !a.rstats && !a.rpart && !a.opart && !a.resid_rows;
+  // the fp8 attention's operands: only as the two compile-time forms below
+  if (a.n_split) {   // fused Q|K | V (both forms below at once)
+    if (!plain || a.resid_t || a.act != ACT_NONE || !a.c_scale || !a.c_scale_rm || !a.vamax || !a.ct2 ||
+        a.vamax_rows < 64 || a.n_split % 256 || a.n_split >= a.N || a.ldc != a.n_split || a.ldc2 < a.N - a.n_split)
+      return -3;
+    hipLaunchKernelGGL((gemm8_kernel<0, true, false, true, 6>), grid, dim3(512), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+  }
+  if (a.c_scale_rm || a.vamax) {
+    if (!plain || a.resid_t || a.act != ACT_NONE || (a.c_scale_rm && !a.c_scale) || (a.vamax && a.c_scale) ||
+        (a.vamax && a.vamax_rows < 64))
+      return -3;
+    if (a.c_scale_rm)
+      hipLaunchKernelGGL((gemm8_kernel<0, true, false, true, 4>), grid, dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL((gemm8_kernel<0, true, false, true, 5>), grid, dim3(512), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+  }
   if (direct && !sse_opt(OPT_GEMM_MX_STAGED)) {
     if (a.resid_t)   // fc2 (direct implies Ct, no Cf / fp8 out / LayerNorm)
       hipLaunchKernelGGL((gemm8_kernel<0, true, false, true, 2>), grid, dim3(512), 0, s, a);

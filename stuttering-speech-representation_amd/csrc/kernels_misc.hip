@@ -2183,6 +2183,299 @@ __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attention_flash3_kernel(
   }
 }
 
+// fp8 Whisper attention (round 5, SSE_DTYPE_FP8): flash3's structure -- S^T = K Q^T so that a lane holds the
+// scores of ONE query, the running max subtracted by a bf16 "ext" MFMA k-step, the max taken only when a lane's
+// row sum shows it moved -- with both products on the block-scaled fp8 MFMA v_mfma_scale_f32_32x32x64_f8f6f4
+// (twice the bf16 rate; tools/probe_f8attn.hip fixed its layouts on gfx950):
+//   operands: lane l is row (A) / column (B) l % 32; byte t of its 32 holds K index 32 (t / 16) + 16 (l / 32) +
+//   t % 16, and the E8M0 scale of K block t / 16 of row r comes from lane r + 32 (t / 16); C as the bf16
+//   32x32x16 (element e of lane l: row 8 (e / 4) + 4 (l / 32) + e % 4, column l % 32).
+//   S^T: one MFMA per 32-key block covers d = 64.  A = K rows (e4m3 from the Q|K GEMM), B = Q, the scales
+//        the GEMM's row-major MX scales (blocks of 32 dims).
+//   P.V: O^T = V^T P^T.  B = P^T is the lane's own 32 probabilities in e4m3 in the order they come out of
+//        S^T (byte 16 kb + e), so key(hw, 16 kb + e) = 32 kb + 8 (e / 4) + 4 hw + e % 4; A = V^T in that key
+//        order, gathered by ds_read_b64_tr_b8 (a 16-lane group's 16 addresses as 8 rows x 2 halves: lane i
+//        gets byte i % 8 of the rows of lanes 2k + i / 8, k = 0..7) from row-major e4m3 V in LDS.
+//   V is quantised while it is staged (bf16 loads -> e4m3 with one power-of-two scale per (clip, head),
+//   mx_scale_exp of the max of the V GEMM's column amax), that scale being the A scale of every key block.
+// e4m3 P needs p <= 448: the row-sum trigger is 448 (every p of a lane below it), and a triggered tile moves
+// the max past a 3 (log2) slack, so p <= 8 afterwards.  The row sum l adds the fp32 p before rounding
+// (oracle/emulate_whisper.py: the format costs the large-v2 fixture 0.0665 -> 0.0667 rel-L2).
+// Block = 4 waves x 2 query blocks of 32 (256 queries), 64-key tiles of K | V (4 KiB each, e4m3) double-
+// buffered in LDS.
+constexpr float F8_TH = 3.0f;
+constexpr int F8_KV = 64 * 64;      // one 64-key tile of K or V, e4m3
+constexpr int F8_BUF = 2 * F8_KV;   // K | V
+typedef int i32x8f8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4f8 __attribute__((ext_vector_type(4)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) i32x2 lds_i32x2;
+typedef short v2i16f8 __attribute__((ext_vector_type(2)));
+typedef __bf16 v2bf16f8 __attribute__((ext_vector_type(2)));
+
+__global__ __launch_bounds__(256, 2) void attention_f8_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * F8_BUF];
+  int qc, h, b;
+  attn_block_xcd(qc, h, b);
+  const int T = a.T, H = a.H, L8 = 2 * H, LS = (2 * H) >> 5;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = lane & 31, hw = lane >> 5, g16 = (lane >> 4) & 1, i16 = lane & 15;
+  const int nkt = (T + 63) / 64;
+  const long long row0 = (long long)b * T;
+  // the clip's T rows of Q|K, their scales and V (rows past T read as zeros)
+  const auto rq = __builtin_amdgcn_make_buffer_rsrc((void*)(a.qk8 + row0 * L8), (short)0, T * L8, 0x00020000);
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.qks + row0 * LS), (short)0, T * LS, 0x00020000);
+  const auto rv = __builtin_amdgcn_make_buffer_rsrc((void*)((const bf16*)a.v16 + row0 * H), (short)0, T * H * 2,
+                                                    0x00020000);
+  const int q0 = qc * 256 + wave * 64 + j;   // this lane's query in block qb: q0 + 32 qb
+  i32x8f8 qf[2];
+  int qsc[2];
+  #pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int qo = (q0 + 32 * qb) * L8 + 64 * h + 16 * hw;
+    const u32x4f8 lo = __builtin_bit_cast(u32x4f8, __builtin_amdgcn_raw_buffer_load_b128(rq, qo, 0, 0));
+    const u32x4f8 hi = __builtin_bit_cast(u32x4f8, __builtin_amdgcn_raw_buffer_load_b128(rq, qo + 32, 0, 0));
+    qf[qb] = i32x8f8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    qsc[qb] = __builtin_amdgcn_raw_buffer_load_b8(rs, (q0 + 32 * qb) * LS + 2 * h + hw, 0, 0);
+  }
+  // V scale: one power of two per (clip, head), from the max of the head's 64 column amax (the e4m3 normal range
+  // spans 14 binades below it, so a per-column scale buys nothing measurable: oracle/emulate_whisper.py
+  // qk8pv8x 0.06673 vs qk8pv8h 0.06683) -- the A scale of every V^T block and its inverse for the staging
+  const int kch = tid & 7;
+  int vsc;
+  {
+    const unsigned* vam = a.vamax + (long long)b * H + 64 * h;
+    unsigned vm = max(vam[j], vam[32 + j]);   // non-negative float bits order as unsigned
+    #pragma unroll
+    for (int o = 1; o < 32; o <<= 1) vm = max(vm, (unsigned)__shfl_xor((int)vm, o, 64));
+    vsc = mx_scale_exp(__uint_as_float(vm));
+  }
+  // staging: K row tid >> 2, 16-B chunk tid & 3 (swizzled by (row >> 2) & 3: the S^T reads of 16 rows at one
+  // chunk hit 16 distinct bank groups); V rows tid >> 3 (+32), dims 8 kch (16-B chunks swizzled by
+  // (row >> 3) & 3: a transpose read's rows r and r + 8 apart)
+  const int kr = tid >> 2, kc = tid & 3, vr = tid >> 3;
+  const int ko = kr * L8 + H + 64 * h + 16 * kc;
+  const int kw = kr * 64 + 16 * (kc ^ ((kr >> 2) & 3));
+  const int vo = (vr * H + 64 * h + 8 * kch) * 2;
+  u32x4f8 kreg;
+  bf16x8 vreg[2];
+  int ksn[2];   // K scales of the tile in flight: lane (hw, r) = key 32 kb + r, dim block hw
+  auto load_tile = [&](int kt) {
+    kreg = __builtin_bit_cast(u32x4f8, __builtin_amdgcn_raw_buffer_load_b128(rq, ko + kt * 64 * L8, 0, 0));
+    #pragma unroll
+    for (int u = 0; u < 2; ++u)
+      vreg[u] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rv, vo + (kt * 64 + 32 * u) * H * 2, 0, 0));
+    #pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+      ksn[kb] = __builtin_amdgcn_raw_buffer_load_b8(rs, (kt * 64 + 32 * kb + j) * LS + (LS >> 1) + 2 * h + hw, 0, 0);
+  };
+  // bf16 pairs -> e4m3 / 2^E in one v_cvt_scalef32_pk_fp8_bf16 each (tools/probe_cvt.hip: x / 2^exponent(scale),
+  // RNE, the same bytes as cvt_pk_fp8_f32(x * 2^-E))
+  const float vdiv = __builtin_bit_cast(float, (unsigned)(vsc > 0 ? vsc : 1) << 23);
+  auto store_tile = [&](int buf) {
+    char* Ks = smem + buf * F8_BUF;
+    char* Vs = Ks + F8_KV;
+    *(u32x4f8*)(Ks + kw) = kreg;
+    #pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int row = vr + 32 * u;
+      const bf16x8 x = vreg[u];
+      v2i16f8 w0 = {0, 0}, w1 = {0, 0};
+      w0 = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(w0, v2bf16f8{x[0], x[1]}, vdiv, false);
+      w0 = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(w0, v2bf16f8{x[2], x[3]}, vdiv, true);
+      w1 = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(w1, v2bf16f8{x[4], x[5]}, vdiv, false);
+      w1 = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(w1, v2bf16f8{x[6], x[7]}, vdiv, true);
+      *(i32x2*)(Vs + row * 64 + 16 * ((kch >> 1) ^ ((row >> 3) & 3)) + 8 * (kch & 1)) =
+          i32x2{__builtin_bit_cast(int, w0), __builtin_bit_cast(int, w1)};
+    }
+  };
+  // S^T A-operand reads: key row 32 kb + j, dim chunks hw and 2 + hw (kb = 1: + 2048, the same swizzle)
+  const int koff0 = j * 64 + 16 * (hw ^ ((j >> 2) & 3)), koff1 = j * 64 + 16 * ((2 + hw) ^ ((j >> 2) & 3));
+  // V^T transpose-read addresses (this lane as a source of its 16-lane group: k = i16 >> 1, half i16 & 1):
+  // read rho (bytes 8 rho .. +7 of the operand) -> key row 32 (rho >> 1) + 16 (rho & 1) + 8 (k >> 2) + 4 hw + k % 4
+  // (rho >> 1 adds 2048 with the same swizzle)
+  int voff[2][2];
+  {
+    const int k = i16 >> 1, hh = i16 & 1;
+    #pragma unroll
+    for (int db = 0; db < 2; ++db)
+      #pragma unroll
+      for (int r1 = 0; r1 < 2; ++r1) {
+        const int row = 16 * r1 + 8 * (k >> 2) + 4 * hw + (k & 3);
+        voff[db][r1] = row * 64 + 16 * ((2 * db + g16) ^ ((row >> 3) & 3)) + 8 * hh;
+      }
+  }
+  f32x16 o[2][2];
+  #pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+    #pragma unroll
+    for (int e = 0; e < 16; ++e) o[qb][0][e] = o[qb][1][e] = 0.f;
+  // the running max enters S^T as a bf16 k-step (flash3): A (key side) = 1 at k = 0..2, B = -m in 3 terms
+  bf16x8 aext, bext[2];
+  #pragma unroll
+  for (int e = 0; e < 8; ++e) aext[e] = (bf16)0.0f;
+  #pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+    #pragma unroll
+    for (int e = 0; e < 8; ++e) bext[qb][e] = (bf16)0.0f;
+  if (hw == 0) aext[0] = aext[1] = aext[2] = (bf16)1.0f;
+  auto set_bext = [&](int qb, float m) {
+    const float nm = -m;
+    const bf16 t0 = (bf16)nm;
+    const float r1 = nm - (float)t0;
+    const bf16 t1 = (bf16)r1;
+    const bf16 t2 = (bf16)(r1 - (float)t1);
+    bext[qb][0] = hw == 0 ? t0 : (bf16)0.0f;
+    bext[qb][1] = hw == 0 ? t1 : (bf16)0.0f;
+    bext[qb][2] = hw == 0 ? t2 : (bf16)0.0f;
+  };
+  float m_run[2], l_run[2] = {0.f, 0.f};
+  constexpr float lmax = 448.f;
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  auto tile_step = [&](int kt, int cur, auto first_c, auto last_c) {
+    constexpr bool first = decltype(first_c)::value, last = decltype(last_c)::value;
+    const int ksc0 = ksn[0], ksc1 = ksn[1];
+    if (kt + 1 < nkt) load_tile(kt + 1);
+    const char* Ks = smem + cur * F8_BUF;
+    const char* Vs = Ks + F8_KV;
+    const int kbase = kt * 64;
+    f32x16 st[2][2];
+    #pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const u32x4f8 lo = *(const u32x4f8*)(Ks + 2048 * kb + koff0);
+      const u32x4f8 hi = *(const u32x4f8*)(Ks + 2048 * kb + koff1);
+      const i32x8f8 kf = {(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      #pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        #pragma unroll
+        for (int e = 0; e < 16; ++e) st[qb][kb][e] = 0.f;
+        if (!first) st[qb][kb] = mfma32_h<false>(aext, bext[qb], st[qb][kb]);
+        st[qb][kb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf[qb], st[qb][kb], 0, 0, 0, kb ? ksc1 : ksc0,
+                                                                     0, qsc[qb]);
+      }
+    }
+    if (last) {   // element e of key block kb is key 32 kb + 8 (e / 4) + 4 hw + e % 4
+      #pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+        #pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+          #pragma unroll
+          for (int e = 0; e < 16; ++e)
+            if (kbase + 32 * kb + 8 * (e >> 2) + 4 * hw + (e & 3) >= T) st[qb][kb][e] = -INFINITY;
+    }
+    i32x8f8 pf[2];
+    #pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      auto row_max = [&]() {
+        float ta = __builtin_elementwise_maximum(st[qb][0][0], st[qb][0][1]);
+        float tb = __builtin_elementwise_maximum(st[qb][1][0], st[qb][1][1]);
+        #pragma unroll
+        for (int e = 2; e < 16; e += 2) {
+          ta = __builtin_elementwise_maximum(__builtin_elementwise_maximum(ta, st[qb][0][e]), st[qb][0][e + 1]);
+          tb = __builtin_elementwise_maximum(__builtin_elementwise_maximum(tb, st[qb][1][e]), st[qb][1][e + 1]);
+        }
+        const float t = __builtin_elementwise_maximum(ta, tb);
+        const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(t), __float_as_uint(t), false, false);
+        return __builtin_elementwise_maximum(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
+      };
+      float lt;
+      auto exp_tile = [&](float sub) {
+        lt = 0.f;
+        #pragma unroll
+        for (int w = 0; w < 8; ++w) {   // dword w: bytes 4 w .. 4 w + 3 = (kb, e) = (w / 4, 4 (w % 4) ..)
+          const int kb = w >> 2, e0 = 4 * (w & 3);
+          const float p0 = __builtin_amdgcn_exp2f(st[qb][kb][e0] - sub);
+          const float p1 = __builtin_amdgcn_exp2f(st[qb][kb][e0 + 1] - sub);
+          const float p2 = __builtin_amdgcn_exp2f(st[qb][kb][e0 + 2] - sub);
+          const float p3 = __builtin_amdgcn_exp2f(st[qb][kb][e0 + 3] - sub);
+          lt += p0;
+          lt += p1;
+          lt += p2;
+          lt += p3;
+          int x = __builtin_amdgcn_cvt_pk_fp8_f32(p0, p1, 0, false);
+          pf[qb][w] = __builtin_amdgcn_cvt_pk_fp8_f32(p2, p3, x, true);
+        }
+      };
+      if (first) {
+        m_run[qb] = row_max();
+        set_bext(qb, m_run[qb]);
+        exp_tile(m_run[qb]);
+      } else {
+        exp_tile(0.f);
+        if (__any(!(lt <= lmax))) {
+          const float tmax = row_max();   // relative to m_run
+          const float m_new = tmax > F8_TH ? m_run[qb] + tmax : m_run[qb];
+          const float delta = m_new - m_run[qb];
+          const float alpha = __builtin_amdgcn_exp2f(-delta);
+          l_run[qb] *= alpha;
+          #pragma unroll
+          for (int db = 0; db < 2; ++db)
+            #pragma unroll
+            for (int e = 0; e < 16; ++e) o[qb][db][e] *= alpha;
+          m_run[qb] = m_new;
+          set_bext(qb, m_new);
+          exp_tile(delta);
+        }
+      }
+      l_run[qb] += lt;
+    }
+    #pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      i32x8f8 vf;
+      #pragma unroll
+      for (int rho = 0; rho < 4; ++rho) {
+        const i32x2 r = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_i32x2*)(Vs + 2048 * (rho >> 1) + voff[db][rho & 1]));
+        vf[2 * rho] = r[0];
+        vf[2 * rho + 1] = r[1];
+      }
+      #pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+        o[qb][db] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf[qb], o[qb][db], 0, 0, 0, vsc, 0, 0x7F);
+    }
+    if (kt + 1 < nkt) store_tile(cur ^ 1);
+    __syncthreads();
+  };
+  using F = std::integral_constant<bool, false>;
+  using L = std::integral_constant<bool, true>;
+  const int nsteady = nkt - ((T % 64) != 0 ? 1 : 0);
+  if (nsteady == 0) {
+    tile_step(0, 0, L{}, L{});
+  } else {
+    tile_step(0, 0, L{}, F{});
+    for (int kt = 1; kt < nsteady; ++kt) tile_step(kt, kt & 1, F{}, F{});
+    if (nsteady < nkt) tile_step(nsteady, nsteady & 1, F{}, L{});
+  }
+  #pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    float l = l_run[qb];
+    const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(l), __float_as_uint(l), false, false);
+    l = __uint_as_float(t32[0]) + __uint_as_float(t32[1]);
+    const int qi = q0 + 32 * qb;
+    if (qi < T) {
+      const float inv = 1.0f / l;
+      bf16* orow = (bf16*)a.out + (row0 + qi) * H + h * AT_HD;
+      #pragma unroll
+      for (int db = 0; db < 2; ++db)
+        #pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const f32x4 x = {o[qb][db][4 * c] * inv, o[qb][db][4 * c + 1] * inv, o[qb][db][4 * c + 2] * inv,
+                           o[qb][db][4 * c + 3] * inv};
+          *(uint2*)(orow + 32 * db + 8 * c + 4 * hw) = pack_h4<false>(x);
+        }
+    }
+  }
+}
+
+int launch_attention_f8(const AttnArgs& a, int B, hipStream_t s) {
+  if (a.H != a.nh * AT_HD || !a.q_log2 || a.tlen || !a.qk8 || !a.qks || !a.v16 || !a.vamax || a.T <= 0) return -3;
+  if ((long long)a.T * 2 * a.H >= (1LL << 31)) return -3;   // 32-bit buffer offsets
+  hipLaunchKernelGGL(attention_f8_kernel, dim3((a.T + 255) / 256, a.nh, B), dim3(256), 0, s, a);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 // Short-sequence bf16 attention (T <= 160, WavLM 3 s clips: T = 149): block = (clip, hpb heads),
 // one wave per 16-query block, the whole padded key row (NKB x 16 keys) of one head in LDS.
 // K and V go HBM -> LDS by LDS-DMA (buffer_load ... lds, 16 B per lane, XOR-swizzled 16-B chunks

@@ -35,7 +35,7 @@ static int g_opt[OPT_COUNT] = {0};
 static const char* const g_opt_name[OPT_COUNT] = {"gemm_cfg", "gemm_nonpersist", "gelu_exact", "conv0_valu",
                                                    "posconv_gemm", "no_lnfold", "gemm_mx_staged", "no_split",
                                                    "logmel_v1", "ln_x3_v1", "attn_x3_f32", "ln_rows_v1", "posconv_2cl",
-                                                   "attn_short", "attn_long"};
+                                                   "attn_short", "attn_long", "fp8_attn_bf16"};
 int sse_opt(int id) { return __atomic_load_n(&g_opt[id], __ATOMIC_RELAXED); }
 
 namespace {
@@ -686,6 +686,7 @@ WavlmWs wavlm_plan(const sse_model* m, int B, int L, Plan& p) {
 
 struct WhisperWs {
   size_t zero, lm, mel, h1, x, xb, qkv, ctx, ff, xf;
+  size_t vam;      // fp8 attention: per-(clip, column) max |V| (float bits), [B][D]
   size_t p1, p2;   // folded pre-LN: per-256-column (mean, M2) partials of the residual stream's rows
   size_t dx, dxb, dv, dq, dctx, dff, dxf;   // decoder rows [B][*]
 };
@@ -707,6 +708,7 @@ WhisperWs whisper_plan(const sse_model* m, int B, Plan& p) {
   w.ctx = p.add(M * D * ex);
   w.ff = p.add(M * (size_t)c.ffn * ex);
   w.xf = p.add(M * D * 4);
+  w.vam = m->mx() ? p.add((size_t)B * D * 4) : 0;
   w.p1 = w.p2 = 0;
   if (m->ln_fold) {
     w.p1 = p.add(M * (D / 256) * 8);
@@ -1335,6 +1337,13 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
   unsigned char* xq_s = xq + (size_t)M * D;
   unsigned char* fq = (unsigned char*)(ws + w.ff);
   unsigned char* fq_s = fq + (size_t)M * F;
+  // fp8 attention (default on the MX path): Q | K e4m3 [M][2D] | V bf16 [M][D] | Q | K scales [M][2D / 32] in
+  // the QKV space ([M][3D] bf16 = 6D bytes per row)
+  const bool f8attn = mx && !sse_opt(OPT_FP8_ATTN_BF16);
+  unsigned char* qk8 = (unsigned char*)qkv;
+  bf16* v16 = (bf16*)(qk8 + (size_t)M * 2 * D);
+  unsigned char* qks = qk8 + (size_t)M * 4 * D;
+  unsigned* vam = mx ? (unsigned*)(ws + w.vam) : nullptr;
   auto mx_gemm = [&](const char* tag, const unsigned char* A, const unsigned char* As, size_t wq, size_t wsc, size_t bo,
                      int N, int K, bool res, void* Ct, unsigned char* Cs, int act) {
     GemmArgs g{};
@@ -1363,7 +1372,21 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
     const LayerW& Lw = m->layers[l];
     if (mx) {
       RC(launch_layernorm_mx<R>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, D, eps, xq, xq_s, s));
-      RC(mx_gemm("gemm_mx:qkv", xq, xq_s, Lw.qkv_q, Lw.qkv_s, Lw.qkv_b, 3 * D, D, false, qkv, nullptr, ACT_NONE));
+      if (f8attn) {
+        // one GEMM over the packed [3D][D] weights: Q | K columns as MX-fp8 with row-major scales (the attention
+        // reads them per row), V columns bf16 plus their per-(clip, column) amax (gemm8_kernel<MXE = 6>)
+        RC(hipMemsetAsync(vam, 0, (size_t)B * D * 4, s) == hipSuccess ? 0 : SSE_ERR_HIP);
+        GemmArgs g{};
+        g.A = xq; g.a_scale = xq_s; g.B = m->ptr(Lw.qkv_q); g.b_scale = m->ptr<unsigned char>(Lw.qkv_s);
+        g.M = M; g.N = 3 * D; g.K = D; g.rows_per_seg = M; g.lda = D; g.bias = m->ptr<float>(Lw.qkv_b); g.zero = zero;
+        g.Ct = qk8; g.c_scale = qks; g.c_scale_rm = 1; g.ldc = 2 * D; g.n_split = 2 * D;
+        g.ct2 = v16; g.ldc2 = D; g.vamax = vam; g.vamax_rows = Tq;
+        RC(prof(m, s, "gemm_mx:qkv", gflops(g),
+                (double)M * D + 3.0 * D * D + (M + 3.0 * D) * D / 32.0 + M * 2.0 * D * (1 + 1.0 / 32) + M * 2.0 * D,
+                [&] { return launch_gemm8_mx(g, s); }));
+      } else {
+        RC(mx_gemm("gemm_mx:qkv", xq, xq_s, Lw.qkv_q, Lw.qkv_s, Lw.qkv_b, 3 * D, D, false, qkv, nullptr, ACT_NONE));
+      }
     } else {
       GemmArgs g{};
       g.A = xb; g.B = m->ptr(Lw.qkv_w); g.M = M; g.N = 3 * D; g.K = D; g.rows_per_seg = M; g.lda = D;
@@ -1382,8 +1405,14 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
     a.qkv = qkv; a.out = ctx; a.T = Tq; a.H = D; a.nh = nh; a.ldq = m->ldq;
     a.q_log2 = m->bf();
     a.scale = a.q_log2 ? 0.6931471805599453f : 1.0f;
-    RC(prof(m, s, "attn", 4.0 * B * (double)Tq * Tq * D, (double)B * Tq * 4.0 * D * sizeof(T),
-            [&] { return launch_attention<T>(a, B, s); }));
+    if (f8attn) {
+      a.qkv = nullptr; a.qk8 = qk8; a.qks = qks; a.v16 = v16; a.vamax = vam;
+      RC(prof(m, s, "attn_f8", 4.0 * B * (double)Tq * Tq * D, (double)B * Tq * (2.0 * D * (1 + 1.0 / 32) + 4.0 * D),
+              [&] { return launch_attention_f8(a, B, s); }));
+    } else {
+      RC(prof(m, s, "attn", 4.0 * B * (double)Tq * Tq * D, (double)B * Tq * 4.0 * D * sizeof(T),
+              [&] { return launch_attention<T>(a, B, s); }));
+    }
     g = GemmArgs{};
     g.A = ctx; g.B = m->ptr(Lw.o_w); g.M = M; g.N = D; g.K = D; g.rows_per_seg = M; g.lda = D;
     g.bias = m->ptr<float>(Lw.o_b); set_resid(g); g.ldc = D; g.zero = zero;
@@ -1989,6 +2018,17 @@ int sse_attention(const void* d_qkv, void* d_out, int B, int T, int H, int nh, i
   return launch_attention<bf16>(a, B, (hipStream_t)stream) ? SSE_ERR_HIP : SSE_OK;
 }
 
+int sse_attention_f8(const uint8_t* d_qk, const uint8_t* d_qk_scale, const void* d_v, const uint32_t* d_vamax,
+                     void* d_out, int B, int T, int H, int nh, void* stream) {
+  if (!d_qk || !d_qk_scale || !d_v || !d_vamax || !d_out || B <= 0 || T <= 0 || nh <= 0 || H != nh * 64)
+    return SSE_ERR_INVALID;
+  AttnArgs a{};
+  a.out = d_out; a.T = T; a.H = H; a.nh = nh; a.ldq = 2 * H; a.scale = 0.6931471805599453f; a.q_log2 = 1;
+  a.qk8 = d_qk; a.qks = d_qk_scale; a.v16 = d_v; a.vamax = d_vamax;
+  const int rc = launch_attention_f8(a, B, (hipStream_t)stream);
+  return rc == -3 ? SSE_ERR_INVALID : (rc ? SSE_ERR_HIP : SSE_OK);
+}
+
 int sse_gemm(int dtype, const void* d_a, const void* d_b, const float* d_bias, const float* d_resid, float* d_cf,
              void* d_ct, int M, int N, int K, int act, const void* d_zero, void* stream) {
   if (!d_a || !d_b || !d_zero || M <= 0 || N <= 0 || K <= 0 || (!d_cf && !d_ct)) return SSE_ERR_INVALID;
@@ -2000,17 +2040,21 @@ int sse_gemm(int dtype, const void* d_a, const void* d_b, const float* d_bias, c
 }
 
 int sse_gemm_ex(const sse_gemm_desc* d, void* stream) {
-  if (!d || !d->a || !d->b || !d->zero || d->M <= 0 || d->N <= 0 || d->K <= 0 || d->ldc < d->N || (!d->cf && !d->ct))
+  if (!d || !d->a || !d->b || !d->zero || d->M <= 0 || d->N <= 0 || d->K <= 0 || (!d->cf && !d->ct) ||
+      d->ldc < (d->n_split ? d->n_split : d->N))
     return SSE_ERR_INVALID;
   if (d->dtype != SSE_DTYPE_BF16 && d->dtype != SSE_DTYPE_FP16 && d->dtype != SSE_DTYPE_F32 && d->dtype != SSE_DTYPE_FP8)
     return SSE_ERR_INVALID;
   if (d->dtype == SSE_DTYPE_FP8) {
-    if (!d->a_scale || !d->b_scale || d->ldc != d->N || d->apart || d->rpart || d->opart) return SSE_ERR_INVALID;
+    if (!d->a_scale || !d->b_scale || d->ldc != (d->n_split ? d->n_split : d->N) || d->apart || d->rpart || d->opart)
+      return SSE_ERR_INVALID;
     if (d->N % 256 || d->K % 128) return SSE_ERR_UNSUPPORTED;
     GemmArgs g{};
     g.A = d->a; g.a_scale = d->a_scale; g.B = d->b; g.b_scale = d->b_scale; g.M = d->M; g.N = d->N; g.K = d->K;
     g.rows_per_seg = d->M; g.lda = d->K; g.bias = d->bias; g.resid = d->resid; g.resid_t = (const bf16*)d->resid_t;
-    g.Cf = d->cf; g.Ct = d->ct; g.ldc = d->N; g.act = d->act; g.zero = d->zero;
+    g.Cf = d->cf; g.Ct = d->ct; g.ldc = d->ldc; g.act = d->act; g.zero = d->zero;
+    g.c_scale = d->c_scale; g.c_scale_rm = d->c_scale_rm; g.vamax = d->vamax; g.vamax_rows = d->vamax_rows;
+    g.ct2 = d->ct2; g.n_split = d->n_split; g.ldc2 = d->ldc2;
     const int rc = launch_gemm8_mx(g, (hipStream_t)stream);
     return rc == -3 ? SSE_ERR_INVALID : (rc ? SSE_ERR_HIP : SSE_OK);
   }

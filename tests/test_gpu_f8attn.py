@@ -1,0 +1,250 @@
+"""The fp8 Whisper attention (round 5) and the two MX GEMM epilogues that produce its operands.
+
+The SSE_DTYPE_FP8 encoder (REF/whisper_embeddings_large.py:250-254, HF WhisperAttention) runs its attention on
+the block-scaled fp8 MFMA: the Q|K GEMM writes MX-fp8 with ROW-MAJOR scales (c_scale_rm), the V GEMM bf16 plus
+a per-(clip, column) max |V| (vamax), and attention_f8_kernel (C-ABI hook sse_attention_f8) computes both
+products in e4m3 -- P in e4m3, V in e4m3 with one power-of-two scale per (clip, head).
+
+  * GEMM forms: exact checks against the GEMM's own outputs -- the row-major scales equal the tiled-layout run's
+    bytes (same codes), vamax equals max |ct| per segment bit for bit (segments crossing row tiles, a partial last
+    tile), and both leave guard rows untouched.
+  * attention: a torch fp32 reference over the DEQUANTISED q, k and the kernel's own e4m3 rounding of v (oracle/mx.py
+    scale rule), exact base-2 softmax.  The kernel's remaining roundings are P in e4m3 (3 mantissa bits, against
+    the running max) and fp32 sums, so the bar is the format's own error: rel-L2 <= 1.5 x that of the reference
+    with P rounded to e4m3 against the exact max (+2e-3), max |out - ref| <= 0.1 max |ref|.  (Random scores over
+    1500 keys average P's rounding noise against an output of the same small size: ~2.5e-2 rel-L2 there.)  The
+    adversarial score patterns of test_gpu_flash.py drive the rescale path (the 448 row-sum trigger, 3-unit slack).
+    Clips are independent: clip i alone equals clip i in the batch bit for bit.
+"""
+import ctypes
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+LOG2E = 1.0 / math.log(2.0)
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm()).item()
+
+
+def _e4m3(x):
+    return x.to(torch.float8_e4m3fn).float()
+
+
+def _operands(B, T, H, kind, seed):
+    """q (scaled into log2 units), k, v [B*T, H] fp32 on the device, with the adversarial patterns."""
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    q, k, v = (torch.randn((B, T, H), device="cuda", generator=g) for _ in range(3))
+    if kind == "climb":
+        u = torch.randn((H,), device="cuda", generator=g)
+        u = u / u.norm()
+        q = q * 0.1 + u * 4.0
+        ramp = torch.linspace(0, 1, T, device="cuda")[None, :, None]
+        k = k * 0.1 + u * (ramp * 300.0)
+    elif kind == "spike":
+        k[:, max(T - 7, 0)] *= 12.0
+    elif kind == "tail":
+        k[:, -(T % 64 or 64):] *= 6.0
+    elif kind == "vscale":   # V columns of very different magnitude per head (the per-head scale's worst case)
+        v = v * torch.logspace(-2, 2, H, device="cuda")[None, None, :]
+    q = q * (0.125 * LOG2E)
+    return q.reshape(B * T, H), k.reshape(B * T, H), v.reshape(B * T, H)
+
+
+def _quantize_qk(q, k):
+    """MX-fp8 of [q | k] per 32 columns: (codes uint8 [R][2H], row-major exponents uint8 [R][2H/32],
+    dequantised fp32)."""
+    from oracle import mx
+    x = torch.cat([q, k], dim=1).cpu().numpy().astype(np.float32)
+    codes, _, eb = mx.quantize(x, 0)
+    deq = torch.from_numpy(mx.dequantize(codes, eb).astype(np.float32)).cuda()
+    return torch.from_numpy(codes).cuda(), torch.from_numpy(np.ascontiguousarray(eb)).cuda(), deq
+
+
+def _vamax(v16, B, T, H):
+    return v16.float().abs().view(B, T, H).amax(dim=1).contiguous().view(torch.int32)
+
+
+def _run(qk8, qks, v16, vam, B, T, H, nh):
+    from ssr_amd import _lib
+    out = torch.full((B * T + 64, H), float("nan"), dtype=torch.bfloat16, device="cuda")
+    rc = _lib.lib().sse_attention_f8(qk8.data_ptr(), qks.data_ptr(), v16.data_ptr(), vam.data_ptr(), out.data_ptr(),
+                                     B, T, H, nh, _stream())
+    _lib.check(rc, "sse_attention_f8")
+    torch.cuda.synchronize()
+    assert bool(torch.isnan(out[B * T:].float()).all()), "store past the output"
+    return out[:B * T]
+
+
+def _reference(deq, v16, B, T, H, nh, p8=False):
+    """exact base-2 softmax over the dequantised q.k, times v rounded as the kernel stages it; p8: the
+    probabilities rounded to e4m3 against the exact row max (the format's own error, for the bar)."""
+    from oracle import mx
+    x = deq.view(B, T, 2 * H)
+    q = x[..., :H].reshape(B, T, nh, 64).transpose(1, 2)
+    k = x[..., H:].reshape(B, T, nh, 64).transpose(1, 2)
+    v = v16.float().view(B, T, nh, 64).transpose(1, 2)                      # [B, nh, T, 64]
+    amax = v.abs().amax(dim=(2, 3)).cpu().numpy().astype(np.float32)        # per (clip, head)
+    E = torch.from_numpy(mx.scale_exp(amax).astype(np.float32) - 127.0).cuda()[:, :, None, None]
+    vq = _e4m3(v * torch.exp2(-E)) * torch.exp2(E)
+    s = q @ k.transpose(-1, -2)
+    p = torch.exp2(s - s.amax(-1, keepdim=True))
+    o = ((_e4m3(p) if p8 else p) @ vq) / p.sum(-1, keepdim=True)
+    return o.transpose(1, 2).reshape(B * T, H)
+
+
+@pytest.mark.parametrize("T", [1500, 300, 161, 65, 1])
+@pytest.mark.parametrize("kind", ["random", "climb", "spike", "tail", "vscale"])
+def test_attention_f8_vs_fp32_reference(T, kind):
+    B, nh = 2, 4
+    H = 64 * nh
+    q, k, v = _operands(B, T, H, kind, seed=T * 11 + len(kind))
+    qk8, qks, deq = _quantize_qk(q, k)
+    v16 = v.to(torch.bfloat16)
+    vam = _vamax(v16, B, T, H)
+    out = _run(qk8, qks, v16, vam, B, T, H, nh)
+    assert torch.isfinite(out.float()).all(), (kind, T)
+    ref = _reference(deq, v16, B, T, H, nh)
+    fmt = _rel(_reference(deq, v16, B, T, H, nh, p8=True), ref)
+    err = (out.float() - ref).abs().max().item()
+    top = ref.abs().max().item()
+    rel = _rel(out, ref)
+    print(f"f8 attention {kind:6s} T={T:5d}: max err {err:.3e} of {top:.3f}, rel-L2 {rel:.3e} "
+          f"(e4m3 P against the exact max: {fmt:.3e})")
+    assert rel <= 1.5 * fmt + 2e-3 and err <= 0.1 * top, (kind, T, err, top, rel, fmt)
+
+
+def test_attention_f8_clips_independent():
+    """Clip 1 of a 3-clip batch equals the same clip alone, bit for bit (no cross-clip state: the V scale
+    is per clip)."""
+    B, T, nh = 3, 1500, 4
+    H = 64 * nh
+    q, k, v = _operands(B, T, H, "random", seed=5)
+    v[T:2 * T] *= 40.0   # a louder middle clip: its V scale differs from its neighbours'
+    qk8, qks, _ = _quantize_qk(q, k)
+    v16 = v.to(torch.bfloat16)
+    full = _run(qk8, qks, v16, _vamax(v16, B, T, H), B, T, H, nh)
+    sl = slice(T, 2 * T)
+    one = _run(qk8[sl].contiguous(), qks[sl].contiguous(), v16[sl].contiguous(), _vamax(v16[sl], 1, T, H), 1, T, H, nh)
+    assert torch.equal(full[sl], one)
+
+
+def test_attention_f8_large_v2_shape():
+    """The bench shape's head layout (H = 1280, 20 heads) at B = 2, against the reference."""
+    B, T, nh = 2, 1500, 20
+    H = 64 * nh
+    q, k, v = _operands(B, T, H, "random", seed=77)
+    qk8, qks, deq = _quantize_qk(q, k)
+    v16 = v.to(torch.bfloat16)
+    out = _run(qk8, qks, v16, _vamax(v16, B, T, H), B, T, H, nh)
+    ref = _reference(deq, v16, B, T, H, nh)
+    assert _rel(out, ref) <= 1.5 * _rel(_reference(deq, v16, B, T, H, nh, p8=True), ref) + 2e-3
+
+
+def _gemm_mx(qa, sa, qb, sb, bias, M, N, K, **kw):
+    from ssr_amd import _lib
+    d = _lib.sse_gemm_desc()
+    d.dtype, d.M, d.N, d.K, d.ldc = _lib.SSE_DTYPE_FP8, M, N, K, kw.pop("ldc", N)
+    zero = torch.zeros(64, dtype=torch.float32, device="cuda")
+    d.a, d.b, d.zero, d.a_scale, d.b_scale, d.bias = (qa.data_ptr(), qb.data_ptr(), zero.data_ptr(), sa.data_ptr(),
+                                                      sb.data_ptr(), bias.data_ptr())
+    for key, val in kw.items():
+        setattr(d, key, val if isinstance(val, int) else val.data_ptr())
+    rc = _lib.lib().sse_gemm_ex(ctypes.byref(d), _stream())
+    _lib.check(rc, "sse_gemm_ex")
+    torch.cuda.synchronize()
+
+
+def _mx_operands(M, N, K, seed):
+    from oracle import mx
+    rng = np.random.default_rng(seed)
+    a = rng.standard_normal((M, K)).astype(np.float32)
+    bw = (rng.standard_normal((N, K)) / np.sqrt(K)).astype(np.float32)
+    qa, sa, _ = mx.quantize(a, 0)
+    qb, sb, _ = mx.quantize(bw, 1)
+    dev = lambda x: torch.from_numpy(x).cuda()
+    bias = dev(rng.standard_normal(N).astype(np.float32))
+    return dev(qa), dev(sa), dev(qb), dev(sb), bias
+
+
+@pytest.mark.parametrize("M", [300, 1500, 3001])
+def test_gemm_mx_rowmajor_scales(M):
+    """The Q|K GEMM form (gemm8_kernel<MXE = 4>): the same e4m3 codes as the tiled-scale form, its scales
+    row-major (c_scale[m][n / 32]) equal to the tiled bytes; nothing past row M written."""
+    from oracle import mx
+    from ssr_amd.model import mx_scale_bytes
+    N, K = 512, 256
+    qa, sa, qb, sb, bias = _mx_operands(M, N, K, M)
+    pat = 0xA5
+    ct0 = torch.full((M + 64, N), pat, dtype=torch.uint8, device="cuda")
+    cs0 = torch.full((mx_scale_bytes(M, N),), pat, dtype=torch.uint8, device="cuda")
+    _gemm_mx(qa, sa, qb, sb, bias, M, N, K, ct=ct0, c_scale=cs0)
+    ct1 = torch.full((M + 64, N), pat, dtype=torch.uint8, device="cuda")
+    cs1 = torch.full((M * (N // 32) + 256,), pat, dtype=torch.uint8, device="cuda")
+    _gemm_mx(qa, sa, qb, sb, bias, M, N, K, ct=ct1, c_scale=cs1, c_scale_rm=1)
+    assert torch.equal(ct0[:M], ct1[:M])
+    assert bool((ct1[M:] == pat).all()) and bool((cs1[M * (N // 32):] == pat).all())
+    r, bl = np.meshgrid(np.arange(M), np.arange(N // 32), indexing="ij")
+    tiled = cs0.cpu().numpy()[mx.a_scale_off(r, bl, N // 128)]
+    assert np.array_equal(cs1[:M * (N // 32)].cpu().numpy().reshape(M, N // 32), tiled)
+
+
+@pytest.mark.parametrize("M,R", [(900, 300), (3000, 1500), (1000, 64), (4500, 1500)])
+def test_gemm_mx_vamax(M, R):
+    """The V GEMM form (gemm8_kernel<MXE = 5>): bf16 output identical to the plain bf16 form, and vamax[s][n]
+    == the float bits of max |ct| over the rows of segment s (segments crossing 256-row tiles and the two
+    64-row halves of a wave, partial last tile), by one atomicMax per lane."""
+    N, K = 512, 256
+    qa, sa, qb, sb, bias = _mx_operands(M, N, K, M + R)
+    c0 = torch.empty((M, N), dtype=torch.bfloat16, device="cuda")
+    _gemm_mx(qa, sa, qb, sb, bias, M, N, K, ct=c0)
+    nseg = (M + R - 1) // R
+    vam = torch.zeros((nseg + 1, N), dtype=torch.int32, device="cuda")
+    c1 = torch.full((M + 64, N), float("nan"), dtype=torch.bfloat16, device="cuda")
+    _gemm_mx(qa, sa, qb, sb, bias, M, N, K, ct=c1, vamax=vam, vamax_rows=R)
+    assert torch.equal(c0, c1[:M])
+    assert bool(torch.isnan(c1[M:].float()).all())
+    ref = torch.stack([c0[s * R:min((s + 1) * R, M)].float().abs().amax(dim=0) for s in range(nseg)])
+    assert torch.equal(vam[:nseg].view(torch.float32), ref)
+    assert bool((vam[nseg] == 0).all())
+
+
+@pytest.mark.parametrize("M,R", [(3000, 1500), (1000, 300)])
+def test_gemm_mx_fused_qkv(M, R):
+    """The encoder's fused QKV form (gemm8_kernel<MXE = 6>, one launch over N = 3H): per 256-column tile either
+    the Q|K epilogue (MX-fp8, row-major scales) or the V one (bf16 + vamax).  Its outputs equal the two
+    separate forms' bit for bit: codes and scales of columns [0, 2H), bf16 V and vamax of columns [2H, 3H)."""
+    H = 256
+    N, K = 3 * H, 256
+    qa, sa, qb, sb, bias = _mx_operands(M, N, K, M + 3)
+    pat = 0xA5
+    # separate: Q|K over the first 2H weight rows, V over the last H (the packed B-scale tiles split at 256 rows)
+    from ssr_amd.model import mx_scale_bytes
+    cut = mx_scale_bytes(2 * H, K)
+    ct0 = torch.full((M, 2 * H), pat, dtype=torch.uint8, device="cuda")
+    cs0 = torch.full((M * (2 * H // 32),), pat, dtype=torch.uint8, device="cuda")
+    _gemm_mx(qa, sa, qb[:2 * H], sb[:cut], bias[:2 * H].contiguous(), M, 2 * H, K, ct=ct0, c_scale=cs0, c_scale_rm=1)
+    nseg = (M + R - 1) // R
+    v0 = torch.empty((M, H), dtype=torch.bfloat16, device="cuda")
+    vm0 = torch.zeros((nseg, H), dtype=torch.int32, device="cuda")
+    _gemm_mx(qa, sa, qb[2 * H:].contiguous(), sb[cut:].contiguous(), bias[2 * H:].contiguous(), M, H, K, ct=v0,
+             vamax=vm0, vamax_rows=R)
+    ct1 = torch.full((M + 64, 2 * H), pat, dtype=torch.uint8, device="cuda")
+    cs1 = torch.full((M * (2 * H // 32) + 256,), pat, dtype=torch.uint8, device="cuda")
+    v1 = torch.full((M + 64, H), float("nan"), dtype=torch.bfloat16, device="cuda")
+    vm1 = torch.zeros((nseg, H), dtype=torch.int32, device="cuda")
+    _gemm_mx(qa, sa, qb, sb, bias, M, N, K, ldc=2 * H, ct=ct1, c_scale=cs1, c_scale_rm=1, ct2=v1, ldc2=H,
+             n_split=2 * H, vamax=vm1, vamax_rows=R)
+    assert torch.equal(ct0, ct1[:M]) and bool((ct1[M:] == pat).all())
+    assert torch.equal(cs0, cs1[:M * (2 * H // 32)]) and bool((cs1[M * (2 * H // 32):] == pat).all())
+    assert torch.equal(v0, v1[:M]) and bool(torch.isnan(v1[M:].float()).all())
+    assert torch.equal(vm0, vm1)

@@ -12,7 +12,7 @@ from conftest import ROOT
 
 def _header_symbols():
     txt = open(os.path.join(ROOT, "include", "sse.h")).read()
-    return sorted(set(re.findall(r"\b(sse_[a-z_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(sse_[a-z0-9_]+)\s*\(", txt)))
 
 
 def test_library_exports_every_header_symbol():
@@ -83,7 +83,7 @@ def test_options_are_explicit_only():
     from ssr_amd import _lib
     L = _lib.lib()
     for name in (b"gemm_cfg", b"gemm_nonpersist", b"gelu_exact", b"conv0_valu", b"posconv_gemm", b"no_lnfold",
-                 b"gemm_mx_staged"):
+                 b"gemm_mx_staged", b"fp8_attn_bf16"):
         assert L.sse_get_option(name) == 0
         with _lib.option(name.decode(), 1):
             assert L.sse_get_option(name) == 1

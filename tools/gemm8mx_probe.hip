@@ -31,15 +31,20 @@ __global__ void fill_u8(unsigned char* p, long long n, unsigned seed, int scale_
 
 typedef void (*kfn)(GemmArgs);
 
-struct Shape { const char* name; int M, N, K; int mode = 0; };   // mode 1: fc1 (GELU, MX-fp8 out); 2: fc2 (bf16 residual)
+// mode 1: fc1 (GELU, MX-fp8 out); 2: fc2 (bf16 residual); round 5, the fp8 attention's operands: 4: MX-fp8 out with
+// row-major scales (MXE 4), 5: bf16 out + per-clip column amax (MXE 5), 6: the fused Q|K (4) | V (5) form (MXE 6)
+struct Shape { const char* name; int M, N, K; int mode = 0; };
 
-int main() {
+int main(int argc, char** argv) {
+  const bool f8 = argc > 1 && argv[1][0] == 'f';   // "f8": only the fp8-attention QKV forms
   int cus = 256;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const Shape shapes[] = {
       {"qkv", 192000, 3840, 1280}, {"ffn1", 192000, 5120, 1280}, {"ffn2", 192000, 1280, 5120},
       {"k640", 192000, 1280, 640}, {"k1280", 192000, 1280, 1280}, {"k2560", 192000, 1280, 2560},
       {"fc1_q8", 192000, 5120, 1280, 1}, {"fc2_res", 192000, 1280, 5120, 2},
+      {"qkv", 192000, 3840, 1280, 0}, {"qkv_q8", 192000, 3840, 1280, 4}, {"qk_q8", 192000, 2560, 1280, 4},
+      {"v_amax", 192000, 1280, 1280, 5}, {"v_bf16", 192000, 1280, 1280, 0}, {"qkv_fus", 192000, 3840, 1280, 6},
   };
   const long long maxA = 192000LL * 5120, maxB = 5120LL * 5120, maxC = 192000LL * 5120;
   unsigned char *a, *b, *sa, *sb, *cs;
@@ -50,6 +55,10 @@ int main() {
   CK(hipMalloc(&sa, maxA / 32 + 4096)); CK(hipMalloc(&sb, maxB / 32 + 4096));
   CK(hipMalloc(&zero, 256)); CK(hipMemset(zero, 0, 256));
   CK(hipMalloc(&cs, maxC / 32 + 4096)); CK(hipMalloc(&bias, 5120 * 4)); CK(hipMemset(bias, 0, 5120 * 4));
+  unsigned* vam;
+  bf16* c2;
+  CK(hipMalloc(&vam, 128 * 5120 * 4)); CK(hipMemset(vam, 0, 128 * 5120 * 4));
+  CK(hipMalloc(&c2, 192000LL * 1280 * 2));
   hipLaunchKernelGGL(fill_u8, dim3(2048), dim3(256), 0, 0, a, maxA, 17u, 0);
   hipLaunchKernelGGL(fill_u8, dim3(2048), dim3(256), 0, 0, b, maxB, 91u, 0);
   hipLaunchKernelGGL(fill_u8, dim3(2048), dim3(256), 0, 0, sa, maxA / 32 + 4096, 5u, 1);
@@ -58,12 +67,19 @@ int main() {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const int ROUNDS = 3, IT = 10;
+  int si = -1;
   for (const Shape& s : shapes) {
+    ++si;
+    if (f8 != (si >= 8)) continue;
     GemmArgs g{};
     g.A = a; g.B = b; g.M = s.M; g.N = s.N; g.K = s.K; g.rows_per_seg = s.M; g.lda = s.K;
     g.Ct = c; g.ldc = s.N; g.act = ACT_NONE; g.zero = zero; g.a_scale = sa; g.b_scale = sb; g.bias = bias;
     if (s.mode == 1) { g.act = ACT_GELU_FAST; g.c_scale = cs; g.bias = bias; }
     if (s.mode == 2) { g.resid_t = c; g.bias = bias; }
+    if (s.mode == 4) { g.c_scale = cs; g.c_scale_rm = 1; }
+    if (s.mode == 5) { g.vamax = vam; g.vamax_rows = 1500; }
+    if (s.mode == 6) { g.c_scale = cs; g.c_scale_rm = 1; g.ldc = 2560; g.n_split = 2560; g.ct2 = c2; g.ldc2 = 1280;
+                       g.vamax = vam; g.vamax_rows = 1500; }
     const int n_tiles = ((s.M + 255) / 256) * (s.N / 256);
     const double tf = 2.0 * s.M * s.N * s.K / 1e12;
     double best[2] = {1e30, 1e30};
@@ -71,7 +87,11 @@ int main() {
       for (int dbg = 0; dbg < 2; ++dbg) {
         kfn k = dbg ? gemm8_kernel<1, true, false, true>
                     : (s.mode == 2 ? gemm8_kernel<0, true, false, true, 2>
-                                   : (s.mode == 1 ? gemm8_kernel<0, true, false, true, 1> : gemm8_kernel<0, true, false, true, 3>));
+                                   : (s.mode == 1 ? gemm8_kernel<0, true, false, true, 1>
+                                                  : (s.mode == 4 ? gemm8_kernel<0, true, false, true, 4>
+                                                                 : (s.mode == 5 ? gemm8_kernel<0, true, false, true, 5>
+                                                                                : (s.mode == 6 ? gemm8_kernel<0, true, false, true, 6>
+                                                                                               : gemm8_kernel<0, true, false, true, 3>)))));
         for (int w = 0; w < 2; ++w) hipLaunchKernelGGL(k, dim3(n_tiles), dim3(512), 0, 0, g);
         CK(hipEventRecord(e0, 0));
         for (int i = 0; i < IT; ++i) hipLaunchKernelGGL(k, dim3(n_tiles), dim3(512), 0, 0, g);
