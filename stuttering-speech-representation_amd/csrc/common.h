@@ -418,14 +418,14 @@ __host__ __device__ inline long long mx_scale_bytes(long long R, int K) { return
 
 // E8M0 exponent of a 32-element block with max |x| = amax: the smallest E with amax <= 448 * 2^E
 // (448 = e4m3 max), clamped to [-127, 127]; returns the biased byte E + 127.
+// For amax >= 0 (bits u): be - 127 - (mantissa <= 0x600000 ? 8 : 7) biased by 127 is ((u + 0x1FFFFF) >> 23) - 8
+// (the mantissa test folded into the carry), clamped below at 0 (zero / denormal blocks: 2^-127); the upper
+// clamp is never reached (be <= 255 gives <= 248).  Three integer ops instead of nine.
 __host__ __device__ inline int mx_scale_exp(float amax) {
   union { float f; unsigned u; } v;
   v.f = amax;
-  const int be = (int)((v.u >> 23) & 255);
-  if (be == 0) return 0;                       // zero / denormal block: 2^-127
-  int E = be - 127 - ((v.u & 0x7FFFFF) <= 0x600000 ? 8 : 7);
-  E = E < -127 ? -127 : (E > 127 ? 127 : E);
-  return E + 127;
+  const int e = (int)((v.u + 0x1FFFFFu) >> 23) - 8;
+  return e > 0 ? e : 0;
 }
 // max over the 8 lanes (lane & ~7) .. (lane | 7): DPP quad_perm xor 1, xor 2, then row_half_mirror
 // (lane i <-> 7 - i within each 8-lane half-row swaps the two quads) -- VALU only, no LDS

@@ -782,13 +782,17 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
       #pragma unroll
       for (int ni = 0; ni < 2; ++ni) {
         const f32x4 o0 = acc[mi][ni][i][0], o1 = acc[mi][ni][i][1];
-        float a = fmaxf(fmaxf(fmaxf(fabsf(o0[0]), fabsf(o0[1])), fmaxf(fabsf(o0[2]), fabsf(o0[3]))),
-                        fmaxf(fmaxf(fabsf(o1[0]), fabsf(o1[1])), fmaxf(fabsf(o1[2]), fabsf(o1[3]))));
+        // (IEEE maximum: the MFMA outputs go in as they are -- fmaxf's maxnum would canonicalise every operand first)
+        float a = __builtin_elementwise_maximum(
+            __builtin_elementwise_maximum(__builtin_elementwise_maximum(fabsf(o0[0]), fabsf(o0[1])),
+                                          __builtin_elementwise_maximum(fabsf(o0[2]), fabsf(o0[3]))),
+            __builtin_elementwise_maximum(__builtin_elementwise_maximum(fabsf(o1[0]), fabsf(o1[1])),
+                                          __builtin_elementwise_maximum(fabsf(o1[2]), fabsf(o1[3]))));
         {   // the row's four q lanes: max over q ^ 1 then q ^ 2 by lane-group swaps (VALU, no LDS round trip)
           const auto t16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(a), false, false);
-          a = fmaxf(__uint_as_float(t16[0]), __uint_as_float(t16[1]));
+          a = __builtin_elementwise_maximum(__uint_as_float(t16[0]), __uint_as_float(t16[1]));
           const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(a), false, false);
-          a = fmaxf(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
+          a = __builtin_elementwise_maximum(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
         }
         const int e = mx_scale_exp(a);
         // e4m3 = RNE(x / 2^(e - 127)) by the scaled conversion (the scale's exponent field only: tools/probe_cvt.hip

@@ -1548,6 +1548,7 @@ constexpr int SPLIT_MIN = 128;
 // parts of a split call: 2 (three or four streams measured slower in rounds 3 and 4)
 int split_parts(int) { return 2; }
 bool split_applies(const sse_model* m, int B, const Sink* sink) {
+  // (Whisper-large-v2 fp8 B = 128 as two streams measured 184.8 vs 178.4 ms/step, round 5: not applied)
   return m->cfg.kind == SSE_KIND_WAVLM && B >= SPLIT_MIN && !sse_opt(OPT_NO_SPLIT) && (!sink || !sink->hs);
 }
 // clips of part i of P (the first B % P parts one more)

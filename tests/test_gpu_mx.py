@@ -178,3 +178,4 @@ def test_whisper_large_v2_fp8_vs_reference_fixture():
     rel, cos = _rel(got, g["emb"][0]).max(), _cos(got, g["emb"][0]).min()
     print("fp8 whisper-large-v2 rel-L2", rel, "cos", cos)
     assert rel <= 0.08 and cos >= 0.995
+
