@@ -428,11 +428,12 @@ __host__ __device__ inline int mx_scale_exp(float amax) {
   return e > 0 ? e : 0;
 }
 // max over the 8 lanes (lane & ~7) .. (lane | 7): DPP quad_perm xor 1, xor 2, then row_half_mirror
-// (lane i <-> 7 - i within each 8-lane half-row swaps the two quads) -- VALU only, no LDS
+// (lane i <-> 7 - i within each 8-lane half-row swaps the two quads) -- VALU only, no LDS; IEEE maximum
+// (fmaxf's maxnum would first canonicalise the DPP-moved operand: one more v_max per step)
 SSE_DEV float max8_dpp(float v) {
-  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true)));   // [1,0,3,2]
-  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true)));   // [2,3,0,1]
-  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, true)));  // half mirror
+  v = __builtin_elementwise_maximum(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true)));
+  v = __builtin_elementwise_maximum(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true)));
+  v = __builtin_elementwise_maximum(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, true)));
   return v;
 }
 

@@ -562,7 +562,8 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
         }
         if (MX && g.c_scale) {
           // MX-fp8 out: the wave holds one row's 256 columns, 8 lanes = one 32-column block
-          const float a = max8_dpp(fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
+          const float a = max8_dpp(__builtin_elementwise_maximum(__builtin_elementwise_maximum(fabsf(o[0]), fabsf(o[1])),
+                                                               __builtin_elementwise_maximum(fabsf(o[2]), fabsf(o[3]))));
           const int e = mx_scale_exp(a);
           const float inv = mx_inv_scale(e);
           int x = __builtin_amdgcn_cvt_pk_fp8_f32(o[0] * inv, o[1] * inv, 0, false);

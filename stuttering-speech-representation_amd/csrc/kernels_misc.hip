@@ -563,7 +563,8 @@ SSE_DEV f32x4 load4_x3(const f16* p, int H) {
 // whose 7 neighbours (lane ^ 1, 2, 4) hold the rest of the 32-column block: amax, E8M0 exponent
 // (mx_scale_exp), e4m3 = RNE(x * 2^-E), one dword store; lane % 8 == 0 stores the scale byte.
 SSE_DEV void mx_quant4(f32x4 o, unsigned char* dst, unsigned char* scale, long long row, int c, int K, int lane) {
-  const float a = max8_dpp(fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
+  const float a = max8_dpp(__builtin_elementwise_maximum(__builtin_elementwise_maximum(fabsf(o[0]), fabsf(o[1])),
+                                                               __builtin_elementwise_maximum(fabsf(o[2]), fabsf(o[3]))));
   const int e = mx_scale_exp(a);
   const float inv = mx_inv_scale(e);
   int x = __builtin_amdgcn_cvt_pk_fp8_f32(o[0] * inv, o[1] * inv, 0, false);
@@ -946,7 +947,8 @@ __global__ __launch_bounds__(256) void layernorm_mx_kernel(const TI* __restrict_
         f32x4 o;
         #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = fmaf((cur[i][e] - mean) * rstd, wv[e], bv[e]);   // = ln_apply4
-        const float a = max8_dpp(fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
+        const float a = max8_dpp(__builtin_elementwise_maximum(__builtin_elementwise_maximum(fabsf(o[0]), fabsf(o[1])),
+                                                               __builtin_elementwise_maximum(fabsf(o[2]), fabsf(o[3]))));
         const int e8 = mx_scale_exp(a);
         const float inv = mx_inv_scale(e8);
         int xq = __builtin_amdgcn_cvt_pk_fp8_f32(o[0] * inv, o[1] * inv, 0, false);
@@ -973,8 +975,8 @@ __global__ __launch_bounds__(256) void layernorm_mx_kernel(const TI* __restrict_
 // bf16 input: 8 elements (one 16-B load) per lane per 512-element chunk, so a row of 1280 is 3 load
 // instructions per lane instead of 5; an MX block of 32 is 4 lanes (DPP quad max); 8-byte fp8 stores.
 SSE_DEV float max4_dpp(float v) {
-  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true)));   // [1,0,3,2]
-  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true)));   // [2,3,0,1]
+  v = __builtin_elementwise_maximum(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true)));
+  v = __builtin_elementwise_maximum(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true)));
   return v;
 }
 template <int NC>
@@ -1041,7 +1043,7 @@ __global__ __launch_bounds__(256) void layernorm_mx8_kernel(const bf16* __restri
       }
       float m = 0.f;
       #pragma unroll
-      for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(o[e]));
+      for (int e = 0; e < 8; ++e) m = __builtin_elementwise_maximum(m, fabsf(o[e]));
       const float a = max4_dpp(m);
       const int e8 = mx_scale_exp(a);
       const float inv = mx_inv_scale(e8);
@@ -1125,7 +1127,8 @@ __global__ __launch_bounds__(256) void mx_quantize_kernel(const float* __restric
   if (role == 0) {
     mx_quant4(o, q + row * K + c, scale, row, c, K, lane);
   } else {
-    const float a = max8_dpp(fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
+    const float a = max8_dpp(__builtin_elementwise_maximum(__builtin_elementwise_maximum(fabsf(o[0]), fabsf(o[1])),
+                                                               __builtin_elementwise_maximum(fabsf(o[2]), fabsf(o[3]))));
     const int e = mx_scale_exp(a);
     const float inv = mx_inv_scale(e);
     int v = __builtin_amdgcn_cvt_pk_fp8_f32(o[0] * inv, o[1] * inv, 0, false);
@@ -1554,11 +1557,11 @@ __global__ __launch_bounds__(256) void attention_kernel(AttnArgs a) {
         if (BIAS) v = fmaf(gate[wave * 16 + r16], rb[key - qi + (Tk - 1)], v);
         v = key < T ? v : -INFINITY;
         s[kb][r] = v;
-        tmax = fmaxf(tmax, v);
+        tmax = __builtin_elementwise_maximum(tmax, v);
       }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float m_new = fmaxf(m_run, tmax);
+    tmax = __builtin_elementwise_maximum(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = __builtin_elementwise_maximum(tmax, __shfl_xor(tmax, 32, 64));
+    const float m_new = __builtin_elementwise_maximum(m_run, tmax);
     const float alpha = exp2f((m_run - m_new) * LOG2E);
     m_run = m_new;
     l_run *= alpha;
@@ -1816,14 +1819,14 @@ __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
           }
         float tmax;
         {
-          tmax = fmaxf(fmaxf(s2[0].x, s2[0].y), s2[1].x);
-          tmax = fmaxf(fmaxf(tmax, s2[1].y), s2[2].x);
+          tmax = __builtin_elementwise_maximum(__builtin_elementwise_maximum(s2[0].x, s2[0].y), s2[1].x);
+          tmax = __builtin_elementwise_maximum(__builtin_elementwise_maximum(tmax, s2[1].y), s2[2].x);
           #pragma unroll
-          for (int e = 2; e < 8; ++e) tmax = e == 2 ? fmaxf(tmax, s2[2].y) : fmaxf(fmaxf(tmax, s2[e].x), s2[e].y);
+          for (int e = 2; e < 8; ++e) tmax = e == 2 ? __builtin_elementwise_maximum(tmax, s2[2].y) : __builtin_elementwise_maximum(__builtin_elementwise_maximum(tmax, s2[e].x), s2[e].y);
           const auto t16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
-          tmax = fmaxf(__uint_as_float(t16[0]), __uint_as_float(t16[1]));
+          tmax = __builtin_elementwise_maximum(__uint_as_float(t16[0]), __uint_as_float(t16[1]));
           const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
-          tmax = fmaxf(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
+          tmax = __builtin_elementwise_maximum(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
         }
         const float tm = tmax * sl2;
         // finite floor: a row with every key so far masked keeps fma(-inf, ., -m) = -inf, never NaN
@@ -1868,17 +1871,17 @@ __global__ __launch_bounds__(256, 3) void attention_flash2_kernel(AttnArgs a) {
           }
           v2[kb * 2 + hh] = v;
         }
-      float tmax = fmaxf(fmaxf(v2[0].x, v2[0].y), v2[1].x);
-      tmax = fmaxf(fmaxf(tmax, v2[1].y), v2[2].x);
+      float tmax = __builtin_elementwise_maximum(__builtin_elementwise_maximum(v2[0].x, v2[0].y), v2[1].x);
+      tmax = __builtin_elementwise_maximum(__builtin_elementwise_maximum(tmax, v2[1].y), v2[2].x);
       #pragma unroll
-      for (int e = 2; e < 8; ++e) tmax = e == 2 ? fmaxf(tmax, v2[2].y) : fmaxf(fmaxf(tmax, v2[e].x), v2[e].y);
+      for (int e = 2; e < 8; ++e) tmax = e == 2 ? __builtin_elementwise_maximum(tmax, v2[2].y) : __builtin_elementwise_maximum(__builtin_elementwise_maximum(tmax, v2[e].x), v2[e].y);
       {
         const auto t16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
-        tmax = fmaxf(__uint_as_float(t16[0]), __uint_as_float(t16[1]));
+        tmax = __builtin_elementwise_maximum(__uint_as_float(t16[0]), __uint_as_float(t16[1]));
         const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
-        tmax = fmaxf(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
+        tmax = __builtin_elementwise_maximum(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
       }
-      const float m_new = fmaxf(m_run[qq], tmax);
+      const float m_new = __builtin_elementwise_maximum(m_run[qq], tmax);
       // rescale only when some row's max grew (alpha == 1 exactly otherwise: skipping is exact)
       if (__any(m_new > m_run[qq])) {
         const float alpha = __builtin_amdgcn_exp2f(m_run[qq] - m_new);
@@ -2601,14 +2604,14 @@ __global__ __launch_bounds__(32 * NKB, 3) void attention_full_kernel(AttnArgs a,
         s[kb][2 * hf] = v.x;
         s[kb][2 * hf + 1] = v.y;
       }
-    float mx = fmaxf(s[0][0], s[0][1]);
+    float mx = __builtin_elementwise_maximum(s[0][0], s[0][1]);
     #pragma unroll
-    for (int kb = 0; kb < NKB; ++kb) mx = fmaxf(fmaxf(mx, fmaxf(s[kb][0], s[kb][1])), fmaxf(s[kb][2], s[kb][3]));
+    for (int kb = 0; kb < NKB; ++kb) mx = __builtin_elementwise_maximum(__builtin_elementwise_maximum(mx, __builtin_elementwise_maximum(s[kb][0], s[kb][1])), __builtin_elementwise_maximum(s[kb][2], s[kb][3]));
     {
       const auto t16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      mx = fmaxf(__uint_as_float(t16[0]), __uint_as_float(t16[1]));
+      mx = __builtin_elementwise_maximum(__uint_as_float(t16[0]), __uint_as_float(t16[1]));
       const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      mx = fmaxf(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
+      mx = __builtin_elementwise_maximum(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
     }
     f32x2 l2 = {0.f, 0.f};
     const f32x2 mm = {-mx, -mx};

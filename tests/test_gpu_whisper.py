@@ -275,9 +275,12 @@ def test_whisper_flash3_matches_flash2(dtype, tol):
     for q, c in enumerate(_clips(None, [3.0, 12.0])):
         w[q] = 0.0
         w[q, :c.shape[0]] = torch.from_numpy(c)
-    a = m.whisper_embed(w, idx, [])[0]
-    with _lib.option("attn_long", 1):
-        b = m.whisper_embed(w, idx, [])[0]
+    # the fp8 model runs the fp8 attention by default (test_gpu_f8attn.py); its bf16-attention form
+    # (fp8_attn_bf16 = 1) is the one that takes flash3 / flash2
+    with _lib.option("fp8_attn_bf16", 1 if dtype == "fp8" else 0):
+        a = m.whisper_embed(w, idx, [])[0]
+        with _lib.option("attn_long", 1):
+            b = m.whisper_embed(w, idx, [])[0]
     assert torch.isfinite(a).all()
     d = _rel(a.cpu().numpy(), b.cpu().numpy()).max()
     print(dtype, "flash3 vs flash2 rel-L2", d)
@@ -286,6 +289,15 @@ def test_whisper_flash3_matches_flash2(dtype, tol):
         rel = _rel(a[q].cpu().numpy(), g["emb"][q]).max()
         print(dtype, "flash3 whisper-small rel-L2", q, rel)
         assert rel <= tol
+    if dtype == "fp8":   # the default fp8 attention on the same clips: at the bar, and close to the bf16 one
+        f = m.whisper_embed(w, idx, [])[0]
+        for q in range(2):
+            rel = _rel(f[q].cpu().numpy(), g["emb"][q]).max()
+            print("fp8 attention whisper-small rel-L2", q, rel)
+            assert rel <= tol
+        d8 = _rel(f.cpu().numpy(), a.cpu().numpy()).max()
+        print("fp8 attention vs bf16 attention rel-L2", d8)
+        assert d8 <= 0.05
 
 
 def test_whisper_small_folded_vs_materialised_layernorm():
