@@ -2216,7 +2216,8 @@ typedef __attribute__((address_space(3))) i32x2 lds_i32x2;
 typedef short v2i16f8 __attribute__((ext_vector_type(2)));
 typedef __bf16 v2bf16f8 __attribute__((ext_vector_type(2)));
 
-__global__ __launch_bounds__(256, 2) void attention_f8_kernel(AttnArgs a) {
+template <int QB>   // query blocks of 32 per wave (2: 256 queries per block)
+__global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attention_f8_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * F8_BUF];
   int qc, h, b;
   attn_block_xcd(qc, h, b);
@@ -2231,11 +2232,11 @@ __global__ __launch_bounds__(256, 2) void attention_f8_kernel(AttnArgs a) {
   const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.qks + row0 * LS), (short)0, T * LS, 0x00020000);
   const auto rv = __builtin_amdgcn_make_buffer_rsrc((void*)((const bf16*)a.v16 + row0 * H), (short)0, T * H * 2,
                                                     0x00020000);
-  const int q0 = qc * 256 + wave * 64 + j;   // this lane's query in block qb: q0 + 32 qb
-  i32x8f8 qf[2];
-  int qsc[2];
+  const int q0 = qc * (128 * QB) + wave * (32 * QB) + j;   // this lane's query in block qb: q0 + 32 qb
+  i32x8f8 qf[QB];
+  int qsc[QB];
   #pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
+  for (int qb = 0; qb < QB; ++qb) {
     const int qo = (q0 + 32 * qb) * L8 + 64 * h + 16 * hw;
     const u32x4f8 lo = __builtin_bit_cast(u32x4f8, __builtin_amdgcn_raw_buffer_load_b128(rq, qo, 0, 0));
     const u32x4f8 hi = __builtin_bit_cast(u32x4f8, __builtin_amdgcn_raw_buffer_load_b128(rq, qo + 32, 0, 0));
@@ -2309,17 +2310,17 @@ __global__ __launch_bounds__(256, 2) void attention_f8_kernel(AttnArgs a) {
         voff[db][r1] = row * 64 + 16 * ((2 * db + g16) ^ ((row >> 3) & 3)) + 8 * hh;
       }
   }
-  f32x16 o[2][2];
+  f32x16 o[QB][2];
   #pragma unroll
-  for (int qb = 0; qb < 2; ++qb)
+  for (int qb = 0; qb < QB; ++qb)
     #pragma unroll
     for (int e = 0; e < 16; ++e) o[qb][0][e] = o[qb][1][e] = 0.f;
   // the running max enters S^T as a bf16 k-step (flash3): A (key side) = 1 at k = 0..2, B = -m in 3 terms
-  bf16x8 aext, bext[2];
+  bf16x8 aext, bext[QB];
   #pragma unroll
   for (int e = 0; e < 8; ++e) aext[e] = (bf16)0.0f;
   #pragma unroll
-  for (int qb = 0; qb < 2; ++qb)
+  for (int qb = 0; qb < QB; ++qb)
     #pragma unroll
     for (int e = 0; e < 8; ++e) bext[qb][e] = (bf16)0.0f;
   if (hw == 0) aext[0] = aext[1] = aext[2] = (bf16)1.0f;
@@ -2333,7 +2334,9 @@ __global__ __launch_bounds__(256, 2) void attention_f8_kernel(AttnArgs a) {
     bext[qb][1] = hw == 0 ? t1 : (bf16)0.0f;
     bext[qb][2] = hw == 0 ? t2 : (bf16)0.0f;
   };
-  float m_run[2], l_run[2] = {0.f, 0.f};
+  float m_run[QB], l_run[QB];
+  #pragma unroll
+  for (int qb = 0; qb < QB; ++qb) l_run[qb] = 0.f;
   constexpr float lmax = 448.f;
   load_tile(0);
   store_tile(0);
@@ -2345,14 +2348,14 @@ __global__ __launch_bounds__(256, 2) void attention_f8_kernel(AttnArgs a) {
     const char* Ks = smem + cur * F8_BUF;
     const char* Vs = Ks + F8_KV;
     const int kbase = kt * 64;
-    f32x16 st[2][2];
+    f32x16 st[QB][2];
     #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
       const u32x4f8 lo = *(const u32x4f8*)(Ks + 2048 * kb + koff0);
       const u32x4f8 hi = *(const u32x4f8*)(Ks + 2048 * kb + koff1);
       const i32x8f8 kf = {(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
       #pragma unroll
-      for (int qb = 0; qb < 2; ++qb) {
+      for (int qb = 0; qb < QB; ++qb) {
         #pragma unroll
         for (int e = 0; e < 16; ++e) st[qb][kb][e] = 0.f;
         if (!first) st[qb][kb] = mfma32_h<false>(aext, bext[qb], st[qb][kb]);
@@ -2362,16 +2365,16 @@ __global__ __launch_bounds__(256, 2) void attention_f8_kernel(AttnArgs a) {
     }
     if (last) {   // element e of key block kb is key 32 kb + 8 (e / 4) + 4 hw + e % 4
       #pragma unroll
-      for (int qb = 0; qb < 2; ++qb)
+      for (int qb = 0; qb < QB; ++qb)
         #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
           #pragma unroll
           for (int e = 0; e < 16; ++e)
             if (kbase + 32 * kb + 8 * (e >> 2) + 4 * hw + (e & 3) >= T) st[qb][kb][e] = -INFINITY;
     }
-    i32x8f8 pf[2];
+    i32x8f8 pf[QB];
     #pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
+    for (int qb = 0; qb < QB; ++qb) {
       auto row_max = [&]() {
         float ta = __builtin_elementwise_maximum(st[qb][0][0], st[qb][0][1]);
         float tb = __builtin_elementwise_maximum(st[qb][1][0], st[qb][1][1]);
@@ -2435,7 +2438,7 @@ __global__ __launch_bounds__(256, 2) void attention_f8_kernel(AttnArgs a) {
         vf[2 * rho + 1] = r[1];
       }
       #pragma unroll
-      for (int qb = 0; qb < 2; ++qb)
+      for (int qb = 0; qb < QB; ++qb)
         o[qb][db] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf[qb], o[qb][db], 0, 0, 0, vsc, 0, 0x7F);
     }
     if (kt + 1 < nkt) store_tile(cur ^ 1);
@@ -2452,7 +2455,7 @@ __global__ __launch_bounds__(256, 2) void attention_f8_kernel(AttnArgs a) {
     if (nsteady < nkt) tile_step(nsteady, nsteady & 1, F{}, L{});
   }
   #pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
+  for (int qb = 0; qb < QB; ++qb) {
     float l = l_run[qb];
     const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(l), __float_as_uint(l), false, false);
     l = __uint_as_float(t32[0]) + __uint_as_float(t32[1]);
@@ -2475,7 +2478,8 @@ __global__ __launch_bounds__(256, 2) void attention_f8_kernel(AttnArgs a) {
 int launch_attention_f8(const AttnArgs& a, int B, hipStream_t s) {
   if (a.H != a.nh * AT_HD || !a.q_log2 || a.tlen || !a.qk8 || !a.qks || !a.v16 || !a.vamax || a.T <= 0) return -3;
   if ((long long)a.T * 2 * a.H >= (1LL << 31)) return -3;   // 32-bit buffer offsets
-  hipLaunchKernelGGL(attention_f8_kernel, dim3((a.T + 255) / 256, a.nh, B), dim3(256), 0, s, a);
+  // (one query block per wave, 168 VGPRs at three blocks per CU, measured 1.4 % slower per step: not kept)
+  hipLaunchKernelGGL(attention_f8_kernel<2>, dim3((a.T + 255) / 256, a.nh, B), dim3(256), 0, s, a);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
