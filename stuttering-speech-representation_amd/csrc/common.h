@@ -383,7 +383,9 @@ SSE_DEV float2 ln_part_combine(const float2 (&v)[NT], float eps) {
     const float d = v[t].x - mean;
     m2 += v[t].y + 256.f * d * d;
   }
-  return make_float2(mean, 1.0f / sqrtf(m2 * (1.0f / (256 * NT)) + eps));
+  // v_rsq_f32 (1 ulp) instead of the correctly rounded 1 / sqrtf (a ~20-instruction refinement sequence): the
+  // folded epilogues take this per row and per lane (8 rows per lane per tile)
+  return make_float2(mean, __builtin_amdgcn_rsqf(m2 * (1.0f / (256 * NT)) + eps));
 }
 template <int NT>
 SSE_DEV float2 ln_part_stats_n(const float2* __restrict__ part, long long m, float eps) {
