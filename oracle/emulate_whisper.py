@@ -102,7 +102,25 @@ def _attn(q, k, v, attn):
     return (pq @ vq) / l
 
 
-def hidden_states(spec, p, mel, gemm="mx8", attn="bf16", stream="bf16"):
+def _gelu_poly(x, c, coef):
+    """the kernels' clamped odd-polynomial GELU (common.h gelu_fp8out2 form): x (1/2 + xc R(xc^2))"""
+    xc = x.clamp(-c, c)
+    s = xc * xc
+    pp = torch.full_like(x, coef[0])
+    for a in coef[1:]:
+        pp = pp * s + a
+    return x * (xc * pp + 0.5)
+
+
+GELU_FP8 = {   # tools/fit_gelu.py fits: (clamp, coefficients highest degree first)
+    "deg5": (3.5, (-3.503167250e-07, 2.229058919e-05, -5.630472442e-04, 7.574830670e-03, -6.208017841e-02,
+                   3.963519037e-01)),
+    "deg3": (3.0, (-0.00015428909682668746, 0.004529666155576706, -0.05285683274269104, 0.38795197010040283)),
+    "deg2": (3.0, (0.0018274825997650623, -0.03881775215268135, 0.3680003583431244)),
+}
+
+
+def hidden_states(spec, p, mel, gemm="mx8", attn="bf16", stream="bf16", gelu_fc1="exact"):
     eps, nh, hd = spec.ln_eps, spec.heads, spec.head_dim
     rnd = _bf if stream == "bf16" else (lambda t: t)
     cf = "bf16" if gemm != "fp32" else "fp32"
@@ -123,7 +141,8 @@ def hidden_states(spec, p, mel, gemm="mx8", attn="bf16", stream="bf16"):
         ctx = rnd(_attn(qh, kh, vh, attn).transpose(0, 1).reshape(T, nh * hd))
         x = rnd(x + _lin(ctx, p[f"{s_}.out_proj.weight"], cf) + p[f"{s_}.out_proj.bias"])
         h = _ln(x, p[f"{a}.final_layer_norm.weight"], p[f"{a}.final_layer_norm.bias"], eps)
-        h = _gelu(_lin(h, p[f"{a}.fc1.weight"], gemm) + p[f"{a}.fc1.bias"])
+        h = _lin(h, p[f"{a}.fc1.weight"], gemm) + p[f"{a}.fc1.bias"]
+        h = _gelu(h) if gelu_fc1 == "exact" else _gelu_poly(h, *GELU_FP8[gelu_fc1])
         x = rnd(x + _lin(h, p[f"{a}.fc2.weight"], gemm) + p[f"{a}.fc2.bias"])
         hs.append(x)
     hs[-1] = _ln(x, p["encoder.layer_norm.weight"], p["encoder.layer_norm.bias"], eps)
@@ -134,6 +153,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--attn", default="bf16,qk8,qk8pv8t,qk8pv8")
     ap.add_argument("--gemm", default="mx8")
+    ap.add_argument("--gelu", default="exact", help="fc1 GELU: exact | deg5 | deg3 | deg2 (the fp8-out polynomials)")
     ap.add_argument("--threads", type=int, default=os.cpu_count())
     ap.add_argument("--out", default="")
     a = ap.parse_args()
@@ -148,12 +168,12 @@ def main() -> None:
     res = {}
     with torch.no_grad():
         for attn in a.attn.split(","):
-            hs = hidden_states(spec, p, mel, a.gemm, attn)
+            hs = hidden_states(spec, p, mel, a.gemm, attn, gelu_fc1=a.gelu)
             got = np.stack([hs[i].mean(0).numpy() for i in idx])
             rel = np.linalg.norm(got - ref, axis=-1) / np.linalg.norm(ref, axis=-1)
             cos = (got * ref).sum(-1) / (np.linalg.norm(got, axis=-1) * np.linalg.norm(ref, axis=-1))
-            res[f"{a.gemm}/{attn}"] = {"rel_l2_max": float(rel.max()), "cos_min": float(cos.min())}
-            print(a.gemm, attn, json.dumps(res[f"{a.gemm}/{attn}"]), flush=True)
+            res[f"{a.gemm}/{attn}/{a.gelu}"] = {"rel_l2_max": float(rel.max()), "cos_min": float(cos.min())}
+            print(a.gemm, attn, a.gelu, json.dumps(res[f"{a.gemm}/{attn}/{a.gelu}"]), flush=True)
     if a.out:
         with open(a.out, "w") as f:
             json.dump(res, f, indent=1)
