@@ -15,6 +15,7 @@
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef int i32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8b __attribute__((ext_vector_type(8)));
 
@@ -77,6 +78,28 @@ __global__ void rate(long long* out, float* sink) {
       c1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, a, c1, 0, 0, 0, 0x7F7F7F7F, 0, 0x7F7F7F7F);
       c2 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, a, c2, 0, 0, 0, 0x7F7F7F7F, 0, 0x7F7F7F7F);
       c3 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, a, c3, 0, 0, 0, 0x7F7F7F7F, 0, 0x7F7F7F7F);
+    } else if constexpr (KIND == 2) {   // 16x16x128 scaled: the MX GEMM's instruction (4 accumulators of 4)
+      f32x4 d0 = {c0[0], c0[1], c0[2], c0[3]}, d1 = {c1[0], c1[1], c1[2], c1[3]}, d2 = {c2[0], c2[1], c2[2], c2[3]},
+            d3 = {c3[0], c3[1], c3[2], c3[3]};
+      d0 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, a, d0, 0, 0, 0, 0x7F7F7F7F, 0, 0x7F7F7F7F);
+      d1 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, a, d1, 0, 0, 0, 0x7F7F7F7F, 0, 0x7F7F7F7F);
+      d2 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, a, d2, 0, 0, 0, 0x7F7F7F7F, 0, 0x7F7F7F7F);
+      d3 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, a, d3, 0, 0, 0, 0x7F7F7F7F, 0, 0x7F7F7F7F);
+      c0[0] = d0[0]; c0[1] = d0[1]; c0[2] = d0[2]; c0[3] = d0[3];
+      c1[0] = d1[0]; c1[1] = d1[1]; c1[2] = d1[2]; c1[3] = d1[3];
+      c2[0] = d2[0]; c2[1] = d2[1]; c2[2] = d2[2]; c2[3] = d2[3];
+      c3[0] = d3[0]; c3[1] = d3[1]; c3[2] = d3[2]; c3[3] = d3[3];
+    } else if constexpr (KIND == 3) {   // 16x16x32 bf16: the bf16 GEMM's instruction
+      f32x4 d0 = {c0[0], c0[1], c0[2], c0[3]}, d1 = {c1[0], c1[1], c1[2], c1[3]}, d2 = {c2[0], c2[1], c2[2], c2[3]},
+            d3 = {c3[0], c3[1], c3[2], c3[3]};
+      d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xb, xb, d0, 0, 0, 0);
+      d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xb, xb, d1, 0, 0, 0);
+      d2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xb, xb, d2, 0, 0, 0);
+      d3 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xb, xb, d3, 0, 0, 0);
+      c0[0] = d0[0]; c0[1] = d0[1]; c0[2] = d0[2]; c0[3] = d0[3];
+      c1[0] = d1[0]; c1[1] = d1[1]; c1[2] = d1[2]; c1[3] = d1[3];
+      c2[0] = d2[0]; c2[1] = d2[1]; c2[2] = d2[2]; c2[3] = d2[3];
+      c3[0] = d3[0]; c3[1] = d3[1]; c3[2] = d3[2]; c3[3] = d3[3];
     } else {
       c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xb, xb, c0, 0, 0, 0);
       c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xb, xb, c1, 0, 0, 0);
@@ -167,5 +190,13 @@ int main() {
   hipLaunchKernelGGL(rate<1>, 1, 64, 0, 0, dt, sink);
   hipMemcpy(&t, dt, 8, hipMemcpyDeviceToHost);
   printf("== rate: 32x32x16 bf16 %.1f cycles per MFMA (clock64)\n", t / 1024.0);
+  hipLaunchKernelGGL(rate<2>, 1, 64, 0, 0, dt, sink);
+  hipLaunchKernelGGL(rate<2>, 1, 64, 0, 0, dt, sink);
+  hipMemcpy(&t, dt, 8, hipMemcpyDeviceToHost);
+  printf("== rate: 16x16x128 f8f6f4 (scaled) %.1f cycles per MFMA (clock64)\n", t / 1024.0);
+  hipLaunchKernelGGL(rate<3>, 1, 64, 0, 0, dt, sink);
+  hipLaunchKernelGGL(rate<3>, 1, 64, 0, 0, dt, sink);
+  hipMemcpy(&t, dt, 8, hipMemcpyDeviceToHost);
+  printf("== rate: 16x16x32 bf16 %.1f cycles per MFMA (clock64)\n", t / 1024.0);
   return 0;
 }
