@@ -331,7 +331,13 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
-    if constexpr (MX) {
+    if constexpr (MX && DBG == 4) {   // probe: no MFMA (the fragment and scale reads kept live)
+      #pragma unroll
+      for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(afx[i]));
+      #pragma unroll
+      for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(bx[j]));
+      asm volatile("" ::"v"(sa), "v"(sb));
+    } else if constexpr (MX) {
       g8_sfor<0, 4>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
         g8_sfor<0, 2>([&](auto jc) {
@@ -372,7 +378,7 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
     auto issue_wait = [&](auto p_c) {
       constexpr int P = decltype(p_c)::value;
       if constexpr (MODE == 1) {
-        issue_steady(t, p_c);
+        if constexpr (DBG != 5) issue_steady(t, p_c);   // probe 5: no steady-loop DMA
         if constexpr (MX) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       } else {
@@ -415,7 +421,7 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
   for (; t < nk; ++t) run_tile(t, std::integral_constant<int, 0>{});
   if (wm == 0) g8_barrier();   // balance group 1's extra barrier
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if constexpr (DBG == 1) {
+  if constexpr (DBG == 1 || DBG == 4 || DBG == 5) {   // (probes: no epilogue)
     float cs = 0.f;
     #pragma unroll
     for (int a = 0; a < 2; ++a)

@@ -82,10 +82,12 @@ int main(int argc, char** argv) {
                        g.vamax = vam; g.vamax_rows = 1500; }
     const int n_tiles = ((s.M + 255) / 256) * (s.N / 256);
     const double tf = 2.0 * s.M * s.N * s.K / 1e12;
-    double best[2] = {1e30, 1e30};
+    double best[4] = {1e30, 1e30, 1e30, 1e30};
+    const int ND = f8 ? 2 : 4;   // 2: no MFMA, 3: no steady-loop DMA (both without the epilogue)
     for (int r = 0; r < ROUNDS; ++r)
-      for (int dbg = 0; dbg < 2; ++dbg) {
-        kfn k = dbg ? gemm8_kernel<1, true, false, true>
+      for (int dbg = 0; dbg < ND; ++dbg) {
+        kfn k = dbg == 2 ? gemm8_kernel<4, true, false, true> : dbg == 3 ? gemm8_kernel<5, true, false, true>
+              : dbg ? gemm8_kernel<1, true, false, true>
                     : (s.mode == 2 ? gemm8_kernel<0, true, false, true, 2>
                                    : (s.mode == 1 ? gemm8_kernel<0, true, false, true, 1>
                                                   : (s.mode == 4 ? gemm8_kernel<0, true, false, true, 4>
@@ -104,8 +106,8 @@ int main(int argc, char** argv) {
       }
     const double rounds = (double)n_tiles / cus;
     printf("%-6s M=%d N=%d K=%d tiles=%d (%.2f rounds of %d CUs)\n", s.name, s.M, s.N, s.K, n_tiles, rounds, cus);
-    const char* nm[2] = {"full", "no-epilogue"};
-    for (int d = 0; d < 2; ++d)
+    const char* nm[4] = {"full", "no-epilogue", "no-ep,no-mfma", "no-ep,no-dma"};
+    for (int d = 0; d < ND; ++d)
       printf("   %-12s %9.1f us  %7.1f TF/s  per tile-round %.2f us  per K-tile %.3f us\n", nm[d], best[d] * 1e3,
              tf / (best[d] * 1e-3), best[d] * 1e3 / rounds, best[d] * 1e3 / rounds / (s.K / 128));
     fflush(stdout);
