@@ -328,7 +328,7 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
   };
   auto mma = [&](f32x4 (&c)[4][2], const bf16x8 (&bf)[2][2], const i32x8 (&bx)[2], auto ni_c) {
     constexpr int NI = decltype(ni_c)::value;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (compiler-placed per-operand waits instead: neutral, round 5)
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
     if constexpr (MX && DBG == 4) {   // probe: no MFMA (the fragment and scale reads kept live)
