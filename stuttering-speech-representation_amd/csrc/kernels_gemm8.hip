@@ -156,9 +156,9 @@ SSE_DEV i32x8 g8_cat(bf16x8 lo, bf16x8 hi) {
 }
 
 // DBG = 1 (timing experiments only, not launched by the library): no epilogue, a checksum keeps the MFMAs live.
-template <bool RES, bool Q8 = false, bool RB = false, int FX = 0, bool RSC = false, bool VAM = false>
+template <bool RES, bool Q8 = false, bool RB = false, int FX = 0, bool RSC = false, bool VAM = false, bool RBL = false>
 SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, int n0, int wm, int wn,
-                                int q, int r16);
+                                int q, int r16, const char* rl0 = nullptr, const char* rl1 = nullptr);
 
 // TR = true: the MFMAs compute C^T blocks (the B fragment is the MFMA's A operand), so every
 // lane ends up holding 4 consecutive output columns of one row and the epilogue stores straight
@@ -249,6 +249,26 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, LPTR(dst + wave * 1024), 16, b_voff[half - 2][0], soff, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, LPTR(dst + (wave + 8) * 1024), 16, b_voff[half - 2][1], soff, 0,
                                                0);
+    }
+  };
+
+  // fc2 (MXE 2): the bf16 residual rows of the tile go to LDS by DMA -- half 0 during the last K-tile into the
+  // buffer K-tile nk - 2 used, half 1 after the main loop into the last K-tile's (gemm8r_kernel<RB>'s scheme):
+  // 64 pieces of 1 KiB per half, rows of 512 B, 16-B chunk c at c ^ (row & 15); rows >= M read as zeros
+  constexpr bool RBP = MX && TR && MXE == 2 && DBG == 0;
+  auto res_dma = [&](int mi, int buf) {
+    if constexpr (RBP) {
+      const long long r0 = (long long)m0 + mi * 128, rows = (long long)M - r0;
+      const long long nrec = rows > 0 ? (rows * g.ldc - n0) * 2 : 0;
+      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(g.resid_t + (rows > 0 ? r0 * g.ldc + n0 : 0)), (short)0, (int)min(nrec, (long long)0x7FFFFFF0),
+          0x00020000);
+      #pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int u = wave * 8 + e, row = 2 * u + (lane >> 5), c = (lane & 31) ^ (row & 15);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, LPTR(smem + buf * G8_BUF + u * 1024), 16,
+                                                 (unsigned)((row * g.ldc + c * 8) * 2), 0u, 0, 0);
+      }
     }
   };
 
@@ -375,6 +395,9 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
     constexpr int MODE = decltype(mode_c)::value;
     const char* buf = smem + (t & 1) * G8_BUF;
     const int k = 4 * t;
+    // RBP, last K-tile: half 0's residual rows go out before phase 0 (the tail waits leave those 8 in flight)
+    const int xr = (RBP && MODE == 0 && t == nk - 1) ? 8 : 0;
+    if (xr) res_dma(0, nk & 1);
     auto issue_wait = [&](auto p_c) {
       constexpr int P = decltype(p_c)::value;
       if constexpr (MODE == 1) {
@@ -383,7 +406,8 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
         else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       } else {
         issue(k + P);
-        g8_wait<MX>(k + P, nk);
+        if constexpr (RBP) g8_vmcnt_dyn<MX>(g8_count<MX>(k + P, nk) + xr);
+        else g8_wait<MX>(k + P, nk);
       }
     };
     const std::integral_constant<int, 0> ni0;
@@ -419,8 +443,14 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
   int t = 0;
   for (; t + 2 < nk; ++t) run_tile(t, std::integral_constant<int, 1>{});
   for (; t < nk; ++t) run_tile(t, std::integral_constant<int, 0>{});
-  if (wm == 0) g8_barrier();   // balance group 1's extra barrier
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (wm == 0) g8_barrier();   // balance group 1's extra barrier: every wave's LDS reads are done
+  if constexpr (RBP) {
+    res_dma(1, (nk - 1) & 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // half 0 landed; half 1's 8 pieces in flight
+    __syncthreads();
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   if constexpr (DBG == 1 || DBG == 4 || DBG == 5) {   // (probes: no epilogue)
     float cs = 0.f;
     #pragma unroll
@@ -438,7 +468,9 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
   if constexpr (TR) {
     if constexpr (MX) {   // fp8 (Q8) or bf16 / fp32 out; the bf16 residual stream in place (fc2, RB)
       if constexpr (MXE == 1) g8_epilogue_direct<false, true, false, 1>(g, acc, m0, n0, wm, wn, q, r16);
-      else if constexpr (MXE == 2) g8_epilogue_direct<true, false, true, 2>(g, acc, m0, n0, wm, wn, q, r16);
+      else if constexpr (MXE == 2)
+        g8_epilogue_direct<true, false, true, 2, false, false, true>(g, acc, m0, n0, wm, wn, q, r16,
+                                                                      smem + (nk & 1) * G8_BUF, smem + ((nk - 1) & 1) * G8_BUF);
       else if constexpr (MXE == 3) g8_epilogue_direct<false, false, false, 2>(g, acc, m0, n0, wm, wn, q, r16);
       else if constexpr (MXE == 4) g8_epilogue_direct<false, true, false, 2, true>(g, acc, m0, n0, wm, wn, q, r16);
       else if constexpr (MXE == 5) g8_epilogue_direct<false, false, false, 2, false, true>(g, acc, m0, n0, wm, wn, q, r16);
@@ -635,9 +667,11 @@ SSE_DEV int g8p_tile(int b, int r, int G, int n_tiles) {
 // compile time: the caller guarantees g agrees)
 // RSC (with Q8): the scales row-major, c_scale[m * (N / 32) + n / 32] (GemmArgs::c_scale_rm).
 // VAM (bf16 out): the per-segment column amax of GemmArgs::vamax (see vamax_half below).
-template <bool RES, bool Q8, bool RB, int FX, bool RSC, bool VAM>
+// RBL (with RB): the residual rows are in LDS (gemm8_kernel<MXE = 2> DMAs half 0 to rl0 during the last K-tile and
+// half 1 to rl1 after the main loop; rows of 512 B, 16-B chunk c at c ^ (row & 15)); the caller has waited for half 0
+template <bool RES, bool Q8, bool RB, int FX, bool RSC, bool VAM, bool RBL>
 SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, int n0, int wm, int wn,
-                                int q, int r16) {
+                                int q, int r16, const char* rl0, const char* rl1) {
   const bool has_bias = FX ? true : g.bias != nullptr;
   const bool has_res = RES && (FX ? true : (RB ? g.resid_t != nullptr : g.resid != nullptr));
   const bool ln = RES && !FX && (g.rstats != nullptr || g.rpart != nullptr);
@@ -657,6 +691,12 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
   float2 st[4];
   auto load_half = [&](int mi) {
     if (!has_res) return;
+    if constexpr (RBL) {
+      if (mi) {   // half 1's residual DMA (the only memory op still in flight) landed for every wave
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+    }
     #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = m0 + mi * 128 + wm * 64 + i * 16 + r16;
@@ -664,7 +704,10 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
       const long long rrow = g.resid_rows ? (long long)(mc % g.resid_rows) * g.ldc : (long long)mc * g.ldc;
       #pragma unroll
       for (int ni = 0; ni < 2; ++ni) {
-        if constexpr (RB) {
+        if constexpr (RB && RBL) {
+          const int row = wm * 64 + i * 16 + r16, c = ni * 16 + wn * 4 + (q & 1) * 2 + (q >> 1);
+          rvb[i][ni] = *(const uint4*)((mi ? rl1 : rl0) + row * 512 + ((c ^ r16) << 4));
+        } else if constexpr (RB) {
           rvb[i][ni] = *(const uint4*)(g.resid_t + rrow + n0 + ni * 128 + wn * 32 + (q & 1) * 16 + (q >> 1) * 8);
         } else {
           #pragma unroll
