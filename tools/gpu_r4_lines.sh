@@ -1,5 +1,5 @@
 # Round-4 bench lines (one box): each line to gpurun_out/<tag>_<name>.json.  Usage: bash tools/gpu_r4_lines.sh <tag> [names...]
-# names: base fp16x3 large_fp16x3 large_bf16 wlv2_bf16 wlv2_fp8 wlv2_fp16x3 small_bf16 small_fp8 small_fp16x3 logmel
+# names: base fp16 fp16x3 large_fp16x3 large_bf16 wlv2_bf16 wlv2_fp8 wlv2_fp16x3 small_bf16 small_fp8 small_fp16x3 logmel
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -14,6 +14,7 @@ run() {   # name, args...
 for n in "$@"; do
   case $n in
     base) run base --steps 20 --warmup 5 ;;
+    fp16) run fp16 --dtype fp16 --steps 20 --warmup 5 ;;
     fp16x3) run fp16x3 --dtype fp16x3 --steps 10 ;;
     large_fp16x3) run large_fp16x3 --model wavlm-large --dtype fp16x3 --steps 5 ;;
     large_bf16) run large_bf16 --model wavlm-large --steps 10 ;;
