@@ -350,7 +350,8 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
     constexpr int NI = decltype(ni_c)::value;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (compiler-placed per-operand waits instead: neutral, round 5)
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
+    // (MX: no raised priority -- fc2 1.152 -> 1.139 ms, the other MX shapes level: r5_gemm8mx_probe_setprio.txt)
+    if constexpr (!MX) __builtin_amdgcn_s_setprio(1);
     if constexpr (MX && DBG == 4) {   // probe: no MFMA (the fragment and scale reads kept live)
       #pragma unroll
       for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(afx[i]));
@@ -376,7 +377,7 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
             c[i][j] = TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][ks], af[i][ks], c[i][j], 0, 0, 0)
                          : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bf[j][ks], c[i][j], 0, 0, 0);
     }
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (!MX) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   };
 
