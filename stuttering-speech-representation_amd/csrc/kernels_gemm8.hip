@@ -350,8 +350,8 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
     constexpr int NI = decltype(ni_c)::value;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (compiler-placed per-operand waits instead: neutral, round 5)
     __builtin_amdgcn_sched_barrier(0);
-    // (MX: no raised priority -- fc2 1.152 -> 1.139 ms, the other MX shapes level: r5_gemm8mx_probe_setprio.txt)
-    if constexpr (!MX) __builtin_amdgcn_s_setprio(1);
+    // (no raised wave priority around the MFMAs, here or in gemm8p / gemm8r: removing it took fp8 Whisper
+    // 184.3 -> 183.1 and WavLM-base 11.71 -> 11.65 ms/step, r5_ab_mx_setprio.txt / r5_ab_bf16_setprio.txt)
     if constexpr (MX && DBG == 4) {   // probe: no MFMA (the fragment and scale reads kept live)
       #pragma unroll
       for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(afx[i]));
@@ -377,7 +377,6 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
             c[i][j] = TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][ks], af[i][ks], c[i][j], 0, 0, 0)
                          : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bf[j][ks], c[i][j], 0, 0, 0);
     }
-    if constexpr (!MX) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   };
 
@@ -1299,7 +1298,6 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
   auto mma = [&](f32x4 (&c)[4][2], const bf16x8 (&bf)[2][2]) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
     if constexpr (DBG == 4) {   // probe: no MFMA (the fragment reads kept live)
       #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
@@ -1316,7 +1314,6 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
           #pragma unroll
           for (int j = 0; j < 2; ++j) c[i][j] = g8_mfma<F16>(bf[j][ks], af[i][ks], c[i][j]);
     }
-    __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   };
 
@@ -1676,14 +1673,12 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
   auto mma = [&](f32x4 (&c)[4][2], const bf16x8 (&bf)[2][2]) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
     #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
       #pragma unroll
       for (int i = 0; i < 4; ++i)
         #pragma unroll
         for (int j = 0; j < 2; ++j) c[i][j] = g8_mfma<F16>(bf[j][ks], af[i][ks], c[i][j]);
-    __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   };
   const bool has_bias = g.bias != nullptr;
