@@ -473,6 +473,11 @@ def main():
     # value: an unperturbed timed region (per-launch event records add ~0.5 ms/step of launch
     # gaps); roofline: a second timed region of the same K steps with the events (single-stream)
     elapsed, _ = timed(False)
+    # N > 1: the last step's gathered [world*B, 4, H] slot checked against every rank's own rows (rank-tagged
+    # clips), and the world size RCCL itself reports -- outside the timed region
+    gather_check = pipe.verify() if dist is not None else None
+    if gather_check is not None and gather_check["rccl_world"] != world:
+        raise RuntimeError(f"RCCL world {gather_check['rccl_world']} != WORLD_SIZE {world}")
     records, prof_elapsed = [], None
     if not a.no_profile:
         prof_elapsed, records = timed(True)
@@ -497,6 +502,9 @@ def main():
                        "model": spec.name, "global_batch": world * B, "clip_samples": L,
                        "layers_pooled": idx, "parallelism": f"clip-sharded dp{world}"},
         }
+        if gather_check is not None:
+            res["rccl_world"] = gather_check["rccl_world"]
+            res["gather_check"] = gather_check
         if records:
             rf = roofline(records, a.dtype)
             rf["device_ms_per_step_sum"] = round(sum(r[1] for r in records) / a.steps, 3)
@@ -507,6 +515,8 @@ def main():
                 rf["traffic_source"] = src + " (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE, bytes per launch)"
             res["roofline"] = rf
         res["model_flops_frac"] = round(value / world * FLOP_PER_CLIP[a.model] / 1e12 / PEAK_TFLOPS[a.dtype], 4)
+        if a.dtype == "fp16x3":   # the same logical FLOPs against the dense fp16 MFMA peak (3 products per term)
+            res["logical_flops_frac_dense_fp16"] = round(value / world * FLOP_PER_CLIP[a.model] / 1e12 / PEAK_TFLOPS["fp16"], 4)
         ncpu = a.cpu_sample if a.cpu_sample is not None else (256 if wavlm else 2)   # ~10-30 s of CPU work
         if world == 1 and ncpu > 0:
             res["cpu_baseline"] = cpu_baseline(a.model, ncpu, secs)

@@ -331,7 +331,8 @@ const char* sse_version(void);
  *   "attn_long"         Whisper bf16 / fp8 encoder attention: 0 = the 32x32 swapped-product kernel with two
  *                       32-query blocks per wave (production), 2 = the same with one (identical outputs),
  *                       1 = the 16x16 flash kernel (same bar, not bit-identical)
- * sse_set_option returns the previous value (>= 0) or SSE_ERR_INVALID for an unknown name. */
+ * sse_set_option returns the previous value (>= 0), or SSE_ERR_INVALID for an unknown name or a value outside
+ * the switch's range (0..1; gemm_cfg 0..3, attn_long 0..2) -- nothing is changed then. */
 int sse_set_option(const char* name, int value);
 int sse_get_option(const char* name);
 

@@ -298,3 +298,45 @@ class StepGather:
             if self.pending[i] is not None:
                 self.pending[i].wait()
                 self.pending[i] = None
+
+    def verify(self) -> dict:
+        """After ``drain()``: check that the last step's gathered slot is what every rank produced, in rank
+        order, and report the world size the collective backend itself saw (bench.py's line carries it, so
+        a multi-GPU record proves "RCCL saw N ranks" on its own).  Raises RuntimeError on any disagreement:
+
+          * this rank's own rows sit at block ``rank`` of the gathered slot, bit for bit;
+          * block r's checksum (fp64 sum, and sum weighted by position) equals the checksum rank r computed
+            over its own rows (one tiny all_gather of [world, 2] checksums), so every block came from its
+            rank and from that rank's LAST step (not a stale slot);
+          * the per-rank checksums are pairwise distinct when ``distinct`` data is expected (bench clips are
+            rank-tagged: rank r embeds clips r*B .. r*B + B - 1), so no rank's rows were replicated.
+
+        Returns {"rccl_world": W, "backend": ..., "blocks_checked": W}."""
+        if self.dist is None or self.steps == 0:
+            return {"rccl_world": 1, "backend": None, "blocks_checked": 0}
+        world = self.dist.get_world_size(self.group)
+        rank = self.dist.get_rank(self.group)
+        slot = (self.steps - 1) % 2
+        own = self.outs[slot]
+        B = own.shape[0]
+        if self.gathered[slot].shape[0] != world * B:
+            raise RuntimeError(f"gathered slot holds {self.gathered[slot].shape[0]} rows for world {world} x {B}")
+        blocks = self.gathered[slot].view(world, B, -1)
+        if not torch.equal(blocks[rank], own.view(B, -1)):
+            raise RuntimeError(f"rank {rank}: its own rows are not at block {rank} of the gathered slot")
+
+        def checksum(x):
+            x = x.reshape(-1).double()
+            w = torch.arange(1, x.numel() + 1, dtype=torch.float64, device=x.device)
+            return torch.stack([x.sum(), (x * w).sum()])
+        mine = checksum(own)
+        flat = torch.empty((world * 2,), dtype=torch.float64, device=own.device)
+        self.dist.all_gather_into_tensor(flat, mine, group=self.group)
+        allsums = flat.view(world, 2)
+        got = torch.stack([checksum(blocks[r]) for r in range(world)])
+        if not torch.equal(got, allsums):
+            bad = [r for r in range(world) if not torch.equal(got[r], allsums[r])]
+            raise RuntimeError(f"rank {rank}: gathered blocks {bad} differ from their ranks' own rows")
+        if len({tuple(v) for v in allsums.cpu().tolist()}) != world:
+            raise RuntimeError(f"rank {rank}: two ranks contributed identical rows (expected rank-distinct clips)")
+        return {"rccl_world": world, "backend": str(self.dist.get_backend(self.group)), "blocks_checked": world}

@@ -420,13 +420,14 @@ __host__ __device__ inline long long mx_scale_bytes(long long R, int K) { return
 
 // E8M0 exponent of a 32-element block with max |x| = amax: the smallest E with amax <= 448 * 2^E
 // (448 = e4m3 max), clamped to [-127, 127]; returns the biased byte E + 127.
-// For amax >= 0 (bits u): be - 127 - (mantissa <= 0x600000 ? 8 : 7) biased by 127 is ((u + 0x1FFFFF) >> 23) - 8
-// (the mantissa test folded into the carry), clamped below at 0 (zero / denormal blocks: 2^-127); the upper
-// clamp is never reached (be <= 255 gives <= 248).  Three integer ops instead of nine.
+// For |amax| (bits u, sign masked off): be - 127 - (mantissa <= 0x600000 ? 8 : 7) biased by 127 is
+// ((u + 0x1FFFFF) >> 23) - 8 (the mantissa test folded into the carry), clamped below at 0 (zero / denormal
+// blocks: 2^-127); the upper clamp is never reached (be <= 255 gives <= 248).  The sign mask makes -0.0 or a
+// negative input give the exponent of its magnitude instead of a byte past 255.  Four integer ops instead of nine.
 __host__ __device__ inline int mx_scale_exp(float amax) {
   union { float f; unsigned u; } v;
   v.f = amax;
-  const int e = (int)((v.u + 0x1FFFFFu) >> 23) - 8;
+  const int e = (int)(((v.u & 0x7FFFFFFFu) + 0x1FFFFFu) >> 23) - 8;
   return e > 0 ? e : 0;
 }
 // max over the 8 lanes (lane & ~7) .. (lane | 7): DPP quad_perm xor 1, xor 2, then row_half_mirror

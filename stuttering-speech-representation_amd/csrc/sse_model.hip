@@ -36,6 +36,8 @@ static const char* const g_opt_name[OPT_COUNT] = {"gemm_cfg", "gemm_nonpersist",
                                                    "posconv_gemm", "no_lnfold", "gemm_mx_staged", "no_split",
                                                    "logmel_v1", "ln_x3_v1", "attn_x3_f32", "ln_rows_v1", "posconv_2cl",
                                                    "attn_short", "attn_long", "fp8_attn_bf16"};
+// the largest value each switch takes (0 .. max; anything else is SSE_ERR_INVALID, not a silent default)
+static const int g_opt_max[OPT_COUNT] = {3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 1};
 int sse_opt(int id) { return __atomic_load_n(&g_opt[id], __ATOMIC_RELAXED); }
 
 namespace {
@@ -1676,7 +1678,8 @@ const char* sse_version(void) { return SSE_VERSION; }
 
 int sse_set_option(const char* name, int value) {
   for (int i = 0; name && i < OPT_COUNT; ++i)
-    if (!std::strcmp(name, g_opt_name[i])) return __atomic_exchange_n(&g_opt[i], value, __ATOMIC_RELAXED);
+    if (!std::strcmp(name, g_opt_name[i]))
+      return value < 0 || value > g_opt_max[i] ? SSE_ERR_INVALID : __atomic_exchange_n(&g_opt[i], value, __ATOMIC_RELAXED);
   return SSE_ERR_INVALID;
 }
 

@@ -56,6 +56,15 @@ def _operands(B, T, H, kind, seed):
         k[:, -(T % 64 or 64):] *= 6.0
     elif kind == "vscale":   # V columns of very different magnitude per head (the per-head scale's worst case)
         v = v * torch.logspace(-2, 2, H, device="cuda")[None, None, :]
+    elif kind == "sink":     # one key ~11 log2 units above a flat tail that still holds ~40 % of the
+        # probability mass (each tail p ~ 2^-11 of the spike's, below e4m3's smallest subnormal relative to the max),
+        # and V correlated (all ~1) so a dropped tail shows as a bias instead of averaging out
+        u = torch.randn((H,), device="cuda", generator=g)
+        u = u / u.norm() * math.sqrt(H / 64)      # unit norm per 64-dim head
+        q = q * 0.02 + u * 4.0
+        k = k * 0.02
+        k[:, 0] = u * (11.0 / (4.0 * 0.125 * LOG2E))
+        v = 1.0 + 0.1 * v
     q = q * (0.125 * LOG2E)
     return q.reshape(B * T, H), k.reshape(B * T, H), v.reshape(B * T, H)
 
@@ -103,7 +112,7 @@ def _reference(deq, v16, B, T, H, nh, p8=False):
 
 
 @pytest.mark.parametrize("T", [1500, 300, 161, 65, 1])
-@pytest.mark.parametrize("kind", ["random", "climb", "spike", "tail", "vscale"])
+@pytest.mark.parametrize("kind", ["random", "climb", "spike", "tail", "vscale", "sink"])
 def test_attention_f8_vs_fp32_reference(T, kind):
     B, nh = 2, 4
     H = 64 * nh

@@ -342,12 +342,15 @@ def test_embed_output_and_workspace_guard_bands(wavlm_sd, dtype):
 
 
 @pytest.mark.parametrize("M", [257, 511, 3000])
-def test_gemm_mx_bf16_residual_in_place(M):
+@pytest.mark.parametrize("form", ["fc2", "no_bias", "gelu"])
+def test_gemm_mx_bf16_residual_in_place(M, form):
     """The Whisper fp8 fc2 form: MX-fp8 operands, the bf16 residual stream read and rewritten in place
     (resid_t == ct).  Round 5 moved it from the LDS-staged epilogue to the register-direct one
     (gemm8_kernel<.., MX, RBE>): the same fp32 expression (acc + bias, + residual, rounded once), so the
     result equals the staged kernel's (option gemm_mx_staged = 1) bit for bit; guard rows stay untouched
-    and the values match the dequantised product."""
+    and the values match the dequantised product.  Forms other than fc2's (no bias, an activation: ADVICE r5)
+    must not reach the compile-time fc2 epilogue, which assumes a bias and no activation: they take the staged
+    kernel on both settings of the option."""
     from oracle import mx
     from ssr_amd import _lib
     N, K = 512, 384
@@ -360,13 +363,19 @@ def test_gemm_mx_bf16_residual_in_place(M):
     qa_, sa_, qb_, sb_ = dev(qa), dev(sa), dev(qb), dev(sb)
     bias = torch.from_numpy(rng.standard_normal(N).astype(np.float32)).cuda()
     res0 = torch.from_numpy(rng.standard_normal((M, N)).astype(np.float32)).cuda().to(torch.bfloat16)
-    ref = torch.from_numpy(mx.dequantize(qa, ea) @ mx.dequantize(qb, eb).T).cuda() + bias + res0.float()
+    prod = torch.from_numpy(mx.dequantize(qa, ea) @ mx.dequantize(qb, eb).T).cuda()
+    act = 1 if form == "gelu" else 0   # ACT_GELU (erf)
+    if form == "no_bias":
+        bias = None
+    pre = prod + (bias if bias is not None else 0.0)
+    ref = (torch.nn.functional.gelu(pre) if act else pre) + res0.float()
     outs = []
     for staged in (0, 1):
         c = Guarded(M, N, N, torch.bfloat16)
         c.out.copy_(res0)
         with _lib.option("gemm_mx_staged", staged):
-            _gemm_ex(2, qa_, qb_, M, N, K, N, bias=bias, resid_t=c.ptr(), ct=c.ptr(), a_scale=sa_, b_scale=sb_)
+            _gemm_ex(2, qa_, qb_, M, N, K, N, bias=bias, act=act, resid_t=c.ptr(), ct=c.ptr(), a_scale=sa_,
+                     b_scale=sb_)
         c.check(f"mx resid staged={staged}")
         outs.append(c.out.clone())
     assert torch.equal(outs[0], outs[1])

@@ -91,6 +91,20 @@ def test_options_are_explicit_only():
     assert L.sse_set_option(b"no_such_switch", 1) < 0
 
 
+def test_option_values_out_of_range_are_rejected():
+    """A value outside a switch's range is an error, not a silent fallback (attn_short = 2 used to be
+    accepted and run the production kernel); the switch keeps its value."""
+    from ssr_amd import _lib
+    L = _lib.lib()
+    for name, top in ((b"attn_short", 1), (b"attn_long", 2), (b"gemm_cfg", 3), (b"no_split", 1)):
+        assert L.sse_get_option(name) == 0
+        assert L.sse_set_option(name, top + 1) < 0
+        assert L.sse_set_option(name, -1) < 0
+        assert L.sse_get_option(name) == 0
+        assert L.sse_set_option(name, top) == 0
+        assert L.sse_set_option(name, 0) == top
+
+
 def test_attention_hook_rejects_q_log2_with_other_scale():
     """sse_attention validates before any device work: q_log2 = 1 requires scale = ln 2 (the 32x32 flash
     kernel reads log2-domain logits and never applies a scale; the short-T kernels would)."""

@@ -62,7 +62,29 @@ static kfr pick_r(int dbg) {   // the folded post-LN residual GEMM (oproj / ffn2
 
 struct Shape { const char* name; int M, N, K, act, ep; int rps = 0; long long seg = 0, lda = 0; };   // rps > 0: conv addressing
 
-int main() {
+// round 6: gemm8h_kernel (two co-resident 256x128 workgroups per CU) against gemm8p_kernel on the K = 768 shapes
+typedef void (*kfh)(GemmArgs);
+template <int ACT, int EP>
+static kfh pick_h(int dbg) {
+  switch (dbg) {
+    case 2: return gemm8h_kernel<ACT, EP, 2>;
+    case 4: return gemm8h_kernel<ACT, EP, 4>;
+    case 5: return gemm8h_kernel<ACT, EP, 5>;
+    default: return gemm8h_kernel<ACT, EP, 0>;
+  }
+}
+
+__global__ void count_diff(const unsigned short* a, const unsigned short* b, long long n, unsigned long long* out) {
+  unsigned long long c = 0;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    c += a[i] != b[i];
+  if (c) atomicAdd(out, c);
+}
+
+static int half_tiles(int argc, char** argv);
+
+int main(int argc, char** argv) {
+  if (argc > 1 && argv[1][0] == 'h') return half_tiles(argc, argv);
   int cus = 256;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const Shape shapes[] = {
@@ -164,6 +186,100 @@ int main() {
     for (int d = 0; d < 8; ++d)
       printf("   %-14s %8.1f us  %7.1f TF/s  per-round %.2f us\n", nm[d], best[d] * 1e3, tf / (best[d] * 1e-3),
              best[d] * 1e3 / __builtin_ceil(rounds));
+    fflush(stdout);
+  }
+  return 0;
+}
+
+// h [rounds]: per shape, gemm8p (the library's persistent 256x256 kernel) vs gemm8h (256x128, two workgroups per
+// CU) in interleaved rounds: full launch, gemm8h without epilogue / MFMA / DMA; outputs compared bit for bit.
+static int half_tiles(int argc, char** argv) {
+  const int ROUNDS = argc > 2 ? atoi(argv[2]) : 3, IT = 20;
+  int cus = 256;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  int occ = 0;
+  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, gemm8h_kernel<ACT_NONE, 1, 0>, 256, 0));
+  printf("gemm8h: %d workgroups per CU (occupancy API), %d CUs\n", occ, cus);
+  struct S { const char* name; int M, N, K, act, ep; };
+  const S shapes[] = {{"qkv", 38144, 2560, 768, ACT_NONE, 1},          {"qkv_fold", 38144, 2560, 768, ACT_NONE, 3},
+                      {"ffn1", 38144, 3072, 768, ACT_GELU_FAST, 1},    {"ffn1_fold", 38144, 3072, 768, ACT_GELU_FAST, 3},
+                      {"proj", 38144, 768, 512, ACT_NONE, 1},          {"k3072", 38144, 2560, 3072, ACT_NONE, 1},
+                      {"m4099", 4099, 768, 768, ACT_GELU_FAST, 3}};
+  const long long maxA = 38144LL * 3072, maxB = 3072LL * 3072, maxC = 38144LL * 3072;
+  bf16 *a, *b, *c0, *c1;
+  float *bias, *acol;
+  float2* apart;
+  void* zero;
+  unsigned long long* nd;
+  CK(hipMalloc(&a, maxA * 2)); CK(hipMalloc(&b, maxB * 2)); CK(hipMalloc(&c0, maxC * 2)); CK(hipMalloc(&c1, maxC * 2));
+  CK(hipMalloc(&bias, 4096 * 4)); CK(hipMalloc(&acol, 4096 * 4)); CK(hipMalloc(&apart, 38144LL * 3 * 8));
+  CK(hipMalloc(&zero, 256)); CK(hipMemset(zero, 0, 256)); CK(hipMalloc(&nd, 8));
+  hipLaunchKernelGGL(fill_bf16, dim3(2048), dim3(256), 0, 0, a, maxA, 17u, 1.0f);
+  hipLaunchKernelGGL(fill_bf16, dim3(2048), dim3(256), 0, 0, b, maxB, 91u, 0.036f);
+  {
+    std::vector<float> h(4096);
+    for (int i = 0; i < 4096; ++i) h[i] = 0.01f * (float)((i * 37) % 101 - 50);
+    CK(hipMemcpy(bias, h.data(), 4096 * 4, hipMemcpyHostToDevice));
+    for (int i = 0; i < 4096; ++i) h[i] = 0.5f + 0.001f * (float)((i * 53) % 97);
+    CK(hipMemcpy(acol, h.data(), 4096 * 4, hipMemcpyHostToDevice));
+    std::vector<float2> p(38144 * 3);
+    for (size_t i = 0; i < p.size(); ++i) p[i] = make_float2(0.01f * (float)((i * 29) % 61 - 30), 200.f + (float)(i % 113));
+    CK(hipMemcpy(apart, p.data(), p.size() * 8, hipMemcpyHostToDevice));
+  }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (const S& s : shapes) {
+    GemmArgs g{};
+    g.A = a; g.B = b; g.M = s.M; g.N = s.N; g.K = s.K; g.rows_per_seg = s.M; g.lda = s.K;
+    g.bias = (s.ep & 1) ? bias : nullptr; g.ldc = s.N; g.act = s.act; g.zero = zero;
+    if (s.ep & 2) { g.apart = apart; g.apart_nt = 3; g.acol = acol; g.ln_eps = 1e-5f; }
+    const int n_tiles = ((s.M + 255) / 256) * (s.N / 256), h_tiles = ((s.M + 255) / 256) * (s.N / 128);
+    const int G = n_tiles < cus ? n_tiles : cus;
+    kfn kp;
+    kfh kh[4];
+    const int hd[4] = {0, 2, 4, 5};
+    if (s.act == ACT_GELU_FAST) {
+      kp = s.ep == 3 ? pick<ACT_GELU_FAST, 3>(0) : pick<ACT_GELU_FAST, 1>(0);
+      for (int d = 0; d < 4; ++d) kh[d] = s.ep == 3 ? pick_h<ACT_GELU_FAST, 3>(hd[d]) : pick_h<ACT_GELU_FAST, 1>(hd[d]);
+    } else {
+      kp = s.ep == 3 ? pick<ACT_NONE, 3>(0) : pick<ACT_NONE, 1>(0);
+      for (int d = 0; d < 4; ++d) kh[d] = s.ep == 3 ? pick_h<ACT_NONE, 3>(hd[d]) : pick_h<ACT_NONE, 1>(hd[d]);
+    }
+    // bit identity of the two library forms
+    CK(hipMemset(c0, 0xFF, (size_t)s.M * s.N * 2)); CK(hipMemset(c1, 0xEE, (size_t)s.M * s.N * 2));
+    g.Ct = c0;
+    hipLaunchKernelGGL(kp, dim3(G), dim3(512), 0, 0, g, n_tiles);
+    g.Ct = c1;
+    hipLaunchKernelGGL(kh[0], dim3(h_tiles), dim3(256), 0, 0, g);
+    CK(hipMemset(nd, 0, 8));
+    hipLaunchKernelGGL(count_diff, dim3(1024), dim3(256), 0, 0, (const unsigned short*)c0, (const unsigned short*)c1,
+                       (long long)s.M * s.N, nd);
+    unsigned long long ndh = 0;
+    CK(hipMemcpy(&ndh, nd, 8, hipMemcpyDeviceToHost));
+    g.Ct = c1;
+    double best[5] = {1e30, 1e30, 1e30, 1e30, 1e30};
+    for (int r = 0; r < ROUNDS; ++r)
+      for (int v = 0; v < 5; ++v) {
+        auto go = [&] {
+          if (v == 0) hipLaunchKernelGGL(kp, dim3(G), dim3(512), 0, 0, g, n_tiles);
+          else hipLaunchKernelGGL(kh[v - 1], dim3(h_tiles), dim3(256), 0, 0, g);
+        };
+        for (int w = 0; w < 3; ++w) go();
+        CK(hipEventRecord(e0, 0));
+        for (int i = 0; i < IT; ++i) go();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        ms /= IT;
+        if (ms < best[v]) best[v] = ms;
+      }
+    const double tf = 2.0 * s.M * s.N * s.K / 1e12;
+    printf("%-10s M=%d N=%d K=%d  256x256 tiles %d (%.2f rounds), 256x128 tiles %d; differing outputs %llu\n", s.name, s.M,
+           s.N, s.K, n_tiles, (double)n_tiles / cus, h_tiles, ndh);
+    const char* nm[5] = {"gemm8p (lib)", "gemm8h full", "gemm8h no-epi", "gemm8h no-mfma", "gemm8h no-dma"};
+    for (int v = 0; v < 5; ++v)
+      printf("   %-16s %8.1f us  %7.1f TF/s\n", nm[v], best[v] * 1e3, tf / (best[v] * 1e-3));
     fflush(stdout);
   }
   return 0;
