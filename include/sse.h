@@ -326,13 +326,15 @@ const char* sse_version(void);
  *   "no_split"          1 = WavLM batches run as one stream (no two-stream half-batch split)
  *   "logmel_v1"         1 = the one-frame-per-wave log-mel kernel
  *   "ln_x3_v1", "attn_x3_f32", "ln_rows_v1", "posconv_2cl"   earlier kernels kept for A/B and bit-identity tests
- *   "attn_short"        short-T (<= 160 frames) attention: 0 = head-pipelined (production), 1 = one head
- *                       at a time (bit-identical; the reference of tests/test_gpu_attention_pipe.py)
+ *   "attn_short"        short-T (<= 160 frames) attention: 0 = head-pipelined, double-buffered, one block per CU
+ *                       (production), 1 = one head at a time (bit-identical; the reference of
+ *                       tests/test_gpu_attention_pipe.py), 2 = two blocks per CU with single-buffered refills
+ *                       (round 6; bit-identical, slower)
  *   "attn_long"         Whisper bf16 / fp8 encoder attention: 0 = the 32x32 swapped-product kernel with two
  *                       32-query blocks per wave (production), 2 = the same with one (identical outputs),
  *                       1 = the 16x16 flash kernel (same bar, not bit-identical)
  * sse_set_option returns the previous value (>= 0), or SSE_ERR_INVALID for an unknown name or a value outside
- * the switch's range (0..1; gemm_cfg 0..3, attn_long 0..2) -- nothing is changed then. */
+ * the switch's range (0..1; gemm_cfg 0..3, attn_short 0..2, attn_long 0..2) -- nothing is changed then. */
 int sse_set_option(const char* name, int value);
 int sse_get_option(const char* name);
 

@@ -2725,10 +2725,16 @@ typedef unsigned int u32x4a __attribute__((ext_vector_type(4)));
 // and the 4 output stores (exactly 4 buffer stores: the pipelined kernels' counted vmcnt relies on it).
 // Used by attention_pipe_kernel, instruction for instruction the per-query-
 // block body of attention_full_kernel (bit-identical results).
-template <bool BIAS, int NKB, bool RAG, bool H16>
+// Hooks (attention_pipe2_kernel): mid() runs once the head's K / Q / gate-row reads are consumed (after the S
+// MFMAs and the gate read), end() once its V^T reads are (after the P.V MFMAs, before the stores); the other
+// kernels pass no-ops, so their code is unchanged.
+struct AttnNoHook {
+  SSE_DEV void operator()() const {}
+};
+template <bool BIAS, int NKB, bool RAG, bool H16, typename Mid = AttnNoHook, typename End = AttnNoHook>
 SSE_DEV void attn_head_body(const char* Ks, const char* Vs, const char* grow, const bf16x8 (&qf)[2], const float2* rbp,
                             float gcon, int T, int qi, int g, int koff0, int koff1, const int (&voffs)[4], float sl2,
-                            __amdgpu_buffer_rsrc_t orsrc, unsigned obase) {
+                            __amdgpu_buffer_rsrc_t orsrc, unsigned obase, Mid&& mid = Mid{}, End&& end = End{}) {
   constexpr int TP = NKB * 16;
   const float LOG2E = 1.4426950408889634f;
   // all K fragments first, then the 2 x NKB MFMAs as NKB independent chains (the per-kb read ->
@@ -2746,6 +2752,7 @@ SSE_DEV void attn_head_body(const char* Ks, const char* Vs, const char* grow, co
   for (int kb = 0; kb < NKB; ++kb) s[kb] = mfma_h<H16>(kf[kb][1], qf[1], s[kb]);
   float gq2 = 0.f;
   if (BIAS) gq2 = wavlm_gate_pair<H16>(*(const bf16x8*)grow, gcon, g) * LOG2E;
+  mid();
   // this lane's bias pairs start at d0 = 4 g - qi + TP - 1 (d = d0 + 16 kb + 2 hf): its LDS address in a
   // register the compiler cannot fold (the table sits past 64 KB, beyond a ds_read's 16-bit offset, and a
   // folded constant base costs a v_add per read), the key-block offsets as immediates
@@ -2822,6 +2829,7 @@ SSE_DEV void attn_head_body(const char* Ks, const char* Vs, const char* grow, co
       o[db] = mfma_h<H16>(vf, pf, o[db]);
     }
   }
+  end();
   const float inv = 1.0f / l;
   #pragma unroll
   for (int db = 0; db < 4; ++db) {
@@ -2939,6 +2947,171 @@ __global__ __launch_bounds__(64 * NKB, 1) void attention_pipe_kernel(AttnArgs a,
   }
 }
 
+// Two blocks per CU (round 6; option attn_short = 2 -- measured slower, not the default).  attention_pipe_kernel's double-buffered images (2 x 63 KB)
+// allow one block of 10 waves per CU: 2.5 waves per SIMD, and its SQ counters (profiles/r6_pmc_sq_attention_pipe
+// .json) show a latency-bound kernel -- 45 % of wave cycles waiting, VALU 14 % and MFMA 10 % busy, no LDS bank
+// conflicts.  Here a block keeps ONE image (K | V | Q | gate rows, 63 KB) and refills it in two parts while it
+// computes, so two blocks fit on a CU (<= 80 KB each with the bias pairs of up to 6 heads: 5 waves per SIMD at
+// the kernel's 96 VGPRs):
+//   head h:  wait K|Q|gate(h), barrier 1 -> K / Q / gate reads, S MFMAs (attn_head_body part 1) -> wait V(h),
+//            barrier 2 (every wave is done with K|Q|gate(h)) -> issue K|Q|gate(h + 1) -> softmax, V^T reads,
+//            P.V -> barrier 3 (every wave is done with V(h)) -> issue V(h + 1) -> the 4 output stores.
+// Vector-memory ops of a wave in issue order: K|Q|gate(h+1) [4 or 5], V(h+1) [2], stores(h) [4]; so the wait at
+// the top of head h+1 is vmcnt(2 + 4) and the V wait at barrier 2 vmcnt(4) (head 0: vmcnt(2) / vmcnt(0)).
+// Per wave the arithmetic is attn_head_body's, so the outputs are bit-identical to the other short-T kernels.
+template <bool BIAS, int NKB, bool RAG, bool H16 = false>
+__global__ __launch_bounds__(64 * NKB, 5) void attention_pipe2_kernel(AttnArgs a, int hpb) {
+  constexpr int TP = NKB * 16;
+  constexpr int NW = NKB;
+  constexpr int KS = TP * 128;
+  constexpr int NGP = (TP + 63) / 64;
+  constexpr int BUF = 3 * KS + NGP * 1024;     // K | V | Q | gate rows
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float2* rb2 = (float2*)(smem + BUF);
+  float* gcs = (float*)(rb2 + hpb * 2 * TP);
+
+  const int h0 = blockIdx.x * hpb, b = blockIdx.y;
+  const int TS = a.T, T = a.tlen ? a.tlen[b] : a.T, H = a.H, H3 = a.ldq;
+  if (T > TP) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  const bf16* qkv = (const bf16*)a.qkv + (long long)b * TS * H3;
+  const float LOG2E = 1.4426950408889634f;
+  const __amdgpu_buffer_rsrc_t orsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)((bf16*)a.out + (long long)b * TS * H), (short)0, T * H * 2, 0x00020000);
+  const int swk = (r16 >> 1) & 7;
+  const int koff0 = r16 * 128 + ((g ^ swk) << 4), koff1 = r16 * 128 + (((g + 4) ^ swk) << 4);
+  const int rowv = 4 * g + (r16 >> 2), swv = ((rowv >> 1) & 3) << 1;
+  int voffs[4];
+  #pragma unroll
+  for (int db = 0; db < 4; ++db) voffs[db] = rowv * 128 + (((2 * db + ((r16 & 3) >> 1)) ^ swv) << 4) + 8 * (r16 & 1);
+  // (inline-asm LDS-DMA as in attention_pipe_kernel: the builtin would put a vmcnt(0) before every transpose read)
+  const u32x4a crs = {(unsigned)(size_t)qkv, (unsigned)((size_t)qkv >> 32) & 0xffffu, (unsigned)(T * H3 * 2), 0x00020000u};
+  const unsigned sbase = (unsigned)(size_t)LPTR(smem);
+  auto dma = [&](unsigned lds, unsigned voff) {
+    asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(crs), "{m0}"(lds) : "memory");
+  };
+  // the DMA lane offsets are recomputed from an opaque lane id at every issue: these issues sit inside the head
+  // body (S scores / O accumulators live), where 7 loop-invariant offsets held across the loop spilled
+  auto issue_kqg = [&](int hh) {   // K and Q (2 pieces each per wave), the gate rows (waves < NGP: one more)
+    const int h = h0 + hh;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    #pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int p = wave + NW * u;
+      const int row = 8 * p + (ln >> 3);
+      const unsigned rbase = (unsigned)(row * H3 * 2);
+      const unsigned kch = (unsigned)(((ln & 7) ^ ((row >> 1) & 7)) << 4);
+      dma(sbase + p * 1024, rbase + kch + (unsigned)((H + h * AT_HD) * 2));
+      dma(sbase + 2 * KS + p * 1024, rbase + kch + (unsigned)(h * AT_HD * 2));
+    }
+    if (BIAS && wave < NGP) dma(sbase + 3 * KS + wave * 1024, (unsigned)((64 * wave + ln) * H3 * 2 + (3 * H + 8 * h) * 2));
+  };
+  auto issue_v = [&](int hh) {     // V (2 pieces per wave)
+    const int h = h0 + hh;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    #pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int p = wave + NW * u;
+      const int row = 8 * p + (ln >> 3);
+      const unsigned rbase = (unsigned)(row * H3 * 2);
+      const unsigned vch = (unsigned)(((ln & 7) ^ (((row >> 1) & 3) << 1)) << 4);
+      dma(sbase + KS + p * 1024, rbase + vch + (unsigned)((2 * H + h * AT_HD) * 2));
+    }
+  };
+  issue_kqg(0);
+  issue_v(0);
+  if (BIAS) {
+    for (int i = tid; i < hpb * 2 * TP; i += 64 * NW) {
+      const int hh = i / (2 * TP), j = i - hh * 2 * TP;
+      const float* rh = a.relb + (long long)(h0 + hh) * (2 * a.maxd + 1) + a.maxd;
+      float v[2];
+      #pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        v[e] = 0.f;
+        if (j + e < 2 * TP - 1) {
+          int d = j + e - (TP - 1);
+          d = d < -a.maxd ? -a.maxd : (d > a.maxd ? a.maxd : d);
+          v[e] = rh[d];
+        }
+      }
+      rb2[i] = make_float2(v[0], v[1]);
+    }
+    if (tid < hpb) gcs[tid] = a.gconst[h0 + tid];
+  }
+  const int qb = wave, qi = qb * 16 + r16;
+  const float sl2 = a.scale * LOG2E;
+  const char* Ks = smem;
+  const char* Vs = smem + KS;
+  const char* Qs = smem + 2 * KS + qb * 2048;
+  for (int hh = 0; hh < hpb; ++hh) {
+    const int h = h0 + hh;
+    const bool more = hh + 1 < hpb;
+    // K|Q|gate(hh) landed for this wave (younger: V(hh) and head hh - 1's 4 stores)
+    if (hh == 0) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    attn_barrier();
+    bf16x8 qf[2];
+    qf[0] = *(const bf16x8*)(Qs + koff0);
+    qf[1] = *(const bf16x8*)(Qs + koff1);
+    int Th = T;
+    if constexpr (RAG) asm volatile("" : "+s"(Th));
+    auto mid = [&]() {
+      // every K / Q / gate read of this wave retired; V(hh) landed (younger: head hh - 1's stores)
+      if (hh == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+      attn_barrier();
+      if (more) issue_kqg(hh + 1);
+    };
+    auto end = [&]() {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      attn_barrier();
+      if (more) issue_v(hh + 1);
+    };
+    attn_head_body<BIAS, NKB, RAG, H16>(Ks, Vs, smem + 3 * KS + qi * 16, qf, rb2 + hh * 2 * TP, BIAS ? gcs[hh] : 0.f, Th,
+                                        qi, g, koff0, koff1, voffs, sl2, orsrc, (unsigned)((qi * H + h * AT_HD) * 2), mid,
+                                        end);
+  }
+}
+
+template <bool BIAS, int NKB, bool RAG, bool H16>
+int launch_attention_pipe2(const AttnArgs& a, int B, hipStream_t s) {
+  constexpr int TP = NKB * 16;
+  constexpr int IMG = 3 * TP * 128 + ((TP + 63) / 64) * 1024;
+  const auto kern = attention_pipe2_kernel<BIAS, NKB, RAG, H16>;
+  constexpr int NT = 64 * NKB;
+  static int per_cu[64][13] = {{0}}, cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || a.nh > 12 * 64) return -2;
+  if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -2;
+  // heads per block: blocks of one round, fewest heads per block (each block's first head load is exposed)
+  int hpb = 1;
+  double best = 1e30;
+  for (int c = 1; c <= a.nh && c <= 12; ++c) {
+    if (a.nh % c) continue;
+    const size_t lds = (size_t)IMG + (BIAS ? (size_t)c * (2 * TP * 8 + 4) : 0);
+    if (lds > 160 * 1024) continue;
+    int& pc = per_cu[dev][c];
+    if (!pc) {
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kern, NT, lds) != hipSuccess) return -2;
+      if (pc < 1) pc = -1;
+    }
+    if (pc < 1) continue;
+    const long long slots = (long long)cus[dev] * pc;
+    const long long nb = (long long)(a.nh / c) * B;
+    const long long rounds = (nb + slots - 1) / slots;
+    const double cost = (double)rounds * (c + 1);
+    if (cost < best) best = cost, hpb = c;
+  }
+  if (best >= 1e30) return -3;
+  const size_t lds = (size_t)IMG + (BIAS ? (size_t)hpb * (2 * TP * 8 + 4) : 0);
+  hipLaunchKernelGGL(kern, dim3(a.nh / hpb, B), dim3(NT), lds, s, a, hpb);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 template <bool BIAS, int NKB, bool RAG, bool H16, int DBG = 0>
 int launch_attention_pipe(const AttnArgs& a, int B, hipStream_t s) {
   constexpr int TP = NKB * 16;
@@ -2979,8 +3152,13 @@ int launch_attention_pipe(const AttnArgs& a, int B, hipStream_t s) {
 
 template <bool BIAS, int NKB, bool RAG, bool H16>
 int launch_attention_short(const AttnArgs& a, int B, hipStream_t s) {
-  const int o = sse_opt(OPT_ATTN_SHORT);   // 0 (default): pipelined; 1: one head at a time (the bit-identity reference)
-  return o == 1 ? launch_attention_full<BIAS, NKB, RAG, H16>(a, B, s) : launch_attention_pipe<BIAS, NKB, RAG, H16>(a, B, s);
+  // 0 (default): the double-buffered head pipeline, one block per CU (attention_pipe_kernel); 1: one head at a time
+  // (the bit-identity reference); 2: two blocks per CU with single-buffered refills (attention_pipe2_kernel, round 6:
+  // bit-identical and slower -- B = 128 39.3 vs 32.0 us, profiles/r6_attn_probe.txt)
+  const int o = sse_opt(OPT_ATTN_SHORT);
+  if (o == 1) return launch_attention_full<BIAS, NKB, RAG, H16>(a, B, s);
+  if (o == 2) return launch_attention_pipe2<BIAS, NKB, RAG, H16>(a, B, s);
+  return launch_attention_pipe<BIAS, NKB, RAG, H16>(a, B, s);
 }
 
 template <bool BIAS, bool RAG, bool H16>

@@ -1,6 +1,6 @@
-"""The head-pipelined short-T attention kernel (attention_pipe_kernel, kernels_misc.hip; option
-attn_short = 0, the default) against the one-head-at-a-time kernel it replaced
-(attention_full_kernel, attn_short = 1): per wave the
+"""The head-pipelined short-T attention kernels (kernels_misc.hip: attention_pipe_kernel, double-buffered, one block
+per CU, option attn_short = 0, the default; attention_pipe2_kernel, two blocks per CU, attn_short = 2, round 6) against
+the one-head-at-a-time kernel (attention_full_kernel, attn_short = 1): per wave the
 same fragments, the same softmax order and the same MFMA chain, so the embeddings must agree bit for
 bit -- at batch sizes that select 1, 3, 6 and 12 heads per block (the double-buffered head loop),
 at 49 and 149 frames (4 and 10 key blocks), on ragged batches (per-clip masks, long clips left to
@@ -32,7 +32,7 @@ def _both(m, w, idx, mode, **kw):
     return a, b
 
 
-@pytest.mark.parametrize("mode", [0])
+@pytest.mark.parametrize("mode", [0, 2])
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])
 @pytest.mark.parametrize("n_clips,samples", [(6, 48000), (48, 48000), (128, 48000), (256, 48000), (5, 16000),
                                              (40, 16000)])
@@ -50,7 +50,7 @@ def test_attention_pipe_bit_identical(wavlm_sd, mode, dtype, n_clips, samples):
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("mode", [0])
+@pytest.mark.parametrize("mode", [0, 2])
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])
 def test_attention_pipe_ragged(wavlm_sd, mode, dtype):
     from ssr_amd import config as C

@@ -96,7 +96,7 @@ def test_option_values_out_of_range_are_rejected():
     accepted and run the production kernel); the switch keeps its value."""
     from ssr_amd import _lib
     L = _lib.lib()
-    for name, top in ((b"attn_short", 1), (b"attn_long", 2), (b"gemm_cfg", 3), (b"no_split", 1)):
+    for name, top in ((b"attn_short", 2), (b"attn_long", 2), (b"gemm_cfg", 3), (b"no_split", 1)):
         assert L.sse_get_option(name) == 0
         assert L.sse_set_option(name, top + 1) < 0
         assert L.sse_set_option(name, -1) < 0

@@ -1,4 +1,5 @@
-// Short-T attention probe: attention_full_kernel vs attention_pipe_kernel (option attn_short 1 / 0) on the same
+// Short-T attention probe: attention_full_kernel vs attention_pipe_kernel vs attention_pipe2_kernel (option attn_short
+// 1 / 0 / 2) on the same
 // random WavLM-base-shaped q|k|v|gate rows -- bitwise comparison (first mismatches by clip / row / head /
 // column) and event timing of each at the bench's batch sizes.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -mllvm -amdgpu-mfma-vgpr-form \
@@ -12,8 +13,8 @@
 #include <vector>
 
 static int g_pipe = 0;
-// g_pipe: 0 full, 1 pipelined -> option attn_short 1, 0 (the round-4 three-deep ring was removed in round 5)
-int sse_opt(int id) { return id == OPT_ATTN_SHORT ? (g_pipe == 0 ? 1 : 0) : 0; }
+// g_pipe: 0 full, 1 pipelined (double-buffered, one block per CU), 2 two blocks per CU -> option attn_short 1, 0, 2
+int sse_opt(int id) { return id == OPT_ATTN_SHORT ? (g_pipe == 0 ? 1 : (g_pipe == 1 ? 0 : 2)) : 0; }
 
 #define CK(x)                                                                      \
   do {                                                                             \
@@ -41,13 +42,14 @@ static int run(int B, int T, bool h16, bool ragged, int reps) {
   for (auto& x : hr) x = rnd();
   std::vector<int> hl(B);
   for (int b = 0; b < B; ++b) hl[b] = ragged ? (b % 5 == 0 ? T : 1 + (int)((T - 1) * (0.5f + 0.5f * rnd()))) : T;
-  void *dq, *dout[2];
+  void *dq, *dout[3];
   float *dg, *dr;
   int* dl;
   const size_t ob = (size_t)B * T * H * 2;
   CK(hipMalloc(&dq, hq.size() * 2));
   CK(hipMalloc(&dout[0], ob));
   CK(hipMalloc(&dout[1], ob));
+  CK(hipMalloc(&dout[2], ob));
   CK(hipMalloc(&dg, nh * 4));
   CK(hipMalloc(&dr, hr.size() * 4));
   CK(hipMalloc(&dl, B * 4));
@@ -55,11 +57,11 @@ static int run(int B, int T, bool h16, bool ragged, int reps) {
   CK(hipMemcpy(dg, hg.data(), nh * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(dr, hr.data(), hr.size() * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(dl, hl.data(), B * 4, hipMemcpyHostToDevice));
-  float ms[2] = {0, 0};
+  float ms[3] = {0, 0, 0};
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < 3; ++k) {
     CK(hipMemset(dout[k], 0, ob));
     AttnArgs a{};
     a.qkv = dq;
@@ -107,8 +109,8 @@ static int run(int B, int T, bool h16, bool ragged, int reps) {
   }
   std::vector<uint16_t> o0(ob / 2), o1(ob / 2);
   CK(hipMemcpy(o0.data(), dout[0], ob, hipMemcpyDeviceToHost));
-  long long bad[2] = {0, 0};
-  for (int k = 1; k < 2; ++k) {
+  long long bad[3] = {0, 0, 0};
+  for (int k = 1; k < 3; ++k) {
     CK(hipMemcpy(o1.data(), dout[k], ob, hipMemcpyDeviceToHost));
     int shown = 0;
     for (int b = 0; b < B; ++b)
@@ -125,15 +127,16 @@ static int run(int B, int T, bool h16, bool ragged, int reps) {
           }
         }
   }
-  std::printf("B=%d T=%d %s%s: full %.2f us, pipe %.2f us, mismatches %lld\n", B, T, h16 ? "fp16" : "bf16",
-              ragged ? " ragged" : "", 1e3 * ms[0], 1e3 * ms[1], bad[1]);
+  std::printf("B=%d T=%d %s%s: full %.2f us, pipe %.2f us, pipe2 %.2f us, mismatches %lld / %lld\n", B, T,
+              h16 ? "fp16" : "bf16", ragged ? " ragged" : "", 1e3 * ms[0], 1e3 * ms[1], 1e3 * ms[2], bad[1], bad[2]);
   CK(hipFree(dq));
   CK(hipFree(dout[0]));
   CK(hipFree(dout[1]));
+  CK(hipFree(dout[2]));
   CK(hipFree(dg));
   CK(hipFree(dr));
   CK(hipFree(dl));
-  return bad[1] ? 1 : 0;
+  return bad[1] || bad[2] ? 1 : 0;
 }
 
 int main() {

@@ -7,6 +7,10 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 TAG=$1
+if [ -x pbin/gemm8_probe ]; then
+  timeout -k 10 300 pbin/gemm8_probe h 3 > gpurun_out/${TAG}_gemm8h_probe.txt 2>&1 || { tail -5 gpurun_out/${TAG}_gemm8h_probe.txt; exit 1; }
+  cat gpurun_out/${TAG}_gemm8h_probe.txt
+fi
 timeout -k 10 600 python -u -m pytest tests -m gpu -q -s --timeout 300 --timeout-method thread -k "f8attn or residual_in_place" > gpurun_out/${TAG}_sel.log 2>&1
 grep -E "f8 attention|passed|failed|FAILED" gpurun_out/${TAG}_sel.log | tail -45
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1
