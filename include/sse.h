@@ -295,6 +295,11 @@ size_t sse_mx_scale_bytes(int R, int K);
 /* byte offset of the scale of (row r, block b = k / 32) in the role's layout */
 long long sse_mx_scale_offset(int role, int r, int b, int K);
 int sse_mx_quantize(const float* d_x, int R, int K, int role, uint8_t* d_q, uint8_t* d_scale, void* stream);
+/* LayerNorm of bf16 rows d_x [R][H] (fp32 statistics, affine d_w / d_b) quantised to MX-fp8 in the A layout
+ * (the fp8 Whisper encoder's QKV / fc1 operand: REF/whisper_embeddings_large.py:250-254 -> HF WhisperEncoderLayer
+ * self_attn_layer_norm / final_layer_norm); H % 128 == 0, H <= 2048.  Test hook. */
+int sse_layernorm_mx(const void* d_x, const float* d_w, const float* d_b, int R, int H, float eps, uint8_t* d_q,
+                     uint8_t* d_scale, void* stream);
 /* C[M][N] = dequant(A)[M][K] . dequant(B)[N][K]^T (+bias) (GELU: act 1 erf, 2 bf16-path form)
  * (+resid fp32) -> d_cf fp32, or d_ct bf16, or (d_c_scale != NULL) d_ct MX-fp8 in the A layout of
  * a GEMM with K = N.  M > 0, N % 256 == 0, K % 128 == 0. */
@@ -324,6 +329,8 @@ const char* sse_version(void);
  *                       -large: read at sse_model_create, the folded model holds no plain QKV weights past layer 0)
  *   "gemm_mx_staged"    1 = LDS-staged epilogue for every MX-fp8 GEMM
  *   "no_split"          1 = WavLM batches run as one stream (no two-stream half-batch split)
+ *   "split_cumask"      two-stream half-batch split on CU-masked streams: 1 = CUs [0, n/2) | [n/2, n),
+ *                       2 = even | odd CUs (each half's grids sized to its CUs); 0 = both halves share every CU
  *   "logmel_v1"         1 = the one-frame-per-wave log-mel kernel
  *   "ln_x3_v1", "attn_x3_f32", "ln_rows_v1", "posconv_2cl"   earlier kernels kept for A/B and bit-identity tests
  *   "attn_short"        short-T (<= 160 frames) attention: 0 = head-pipelined, double-buffered, one block per CU
@@ -334,7 +341,7 @@ const char* sse_version(void);
  *                       32-query blocks per wave (production), 2 = the same with one (identical outputs),
  *                       1 = the 16x16 flash kernel (same bar, not bit-identical)
  * sse_set_option returns the previous value (>= 0), or SSE_ERR_INVALID for an unknown name or a value outside
- * the switch's range (0..1; gemm_cfg 0..3, attn_short 0..2, attn_long 0..2) -- nothing is changed then. */
+ * the switch's range (0..1; gemm_cfg 0..3, attn_short 0..2, attn_long 0..2, split_cumask 0..2) -- nothing is changed then. */
 int sse_set_option(const char* name, int value);
 int sse_get_option(const char* name);
 

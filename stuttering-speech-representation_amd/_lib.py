@@ -34,7 +34,7 @@ EXPORTED = ("sse_weight_floats", "sse_model_create", "sse_model_destroy", "sse_o
             "sse_resample", "sse_augment", "sse_mx_scale_bytes", "sse_mx_scale_offset", "sse_mx_quantize",
             "sse_mx_quantize_host", "sse_gemm_mx", "sse_pitch_shift_workspace_bytes", "sse_pitch_shift",
             "sse_set_option", "sse_get_option", "sse_embed_ragged", "sse_gemm_lnfold", "sse_check_range",
-            "sse_attention", "sse_gemm_ex", "sse_attention_f8")
+            "sse_attention", "sse_gemm_ex", "sse_attention_f8", "sse_layernorm_mx")
 
 
 class SSEError(RuntimeError):
@@ -196,6 +196,9 @@ def lib() -> ctypes.CDLL:
     L.sse_mx_quantize.restype = i32
     L.sse_mx_quantize_host.argtypes = [vp, i32, i32, i32, vp, vp]
     L.sse_mx_quantize_host.restype = i32
+    if hasattr(L, "sse_layernorm_mx"):   # (a round-5 build loaded for an A/B lacks this test hook)
+        L.sse_layernorm_mx.argtypes = [vp, vp, vp, i32, i32, ctypes.c_float, vp, vp, vp]
+        L.sse_layernorm_mx.restype = i32
     L.sse_gemm_mx.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp]
     L.sse_gemm_mx.restype = i32
     L.sse_strerror.argtypes = [i32]

@@ -284,9 +284,14 @@ enum {
   OPT_ATTN_LONG,        // no-bias (Whisper) flash attention: 0 32x32 swapped form, 2 query blocks per wave (default);
                         // 2 the same with one; 1 the 16x16 flash2 kernel
   OPT_FP8_ATTN_BF16,    // 1: the fp8 (MX) Whisper path keeps the bf16 QKV output and the bf16 flash attention
+  OPT_SPLIT_CUMASK,     // two-stream split on CU-masked streams: 1 = CUs [0, n/2) | [n/2, n), 2 = even | odd CUs
   OPT_COUNT
 };
 int sse_opt(int id);
+// CUs a kernel launched on stream s may use: the registered count of a CU-masked stream (split_forward,
+// OPT_SPLIT_CUMASK), else dev_cus.  Launchers that size a grid to the CU count (persistent GEMM, attention
+// heads per block, conv0) ask it, so a masked stream's grid matches its CUs.
+int sse_stream_cus(hipStream_t s, int dev_cus);
 inline bool gelu_exact_env() { return sse_opt(OPT_GELU_EXACT) != 0; }
 
 // ---------------------------------------------------------------------------------------

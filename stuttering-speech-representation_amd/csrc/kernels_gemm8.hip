@@ -788,7 +788,6 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
   };
   const unsigned lane_col = (unsigned)(wn * 32 + (q & 1) * 16 + (q >> 1) * 8);
   const unsigned lane_off2 = (unsigned)(((wm * 64 + r16) * g.ldc + lane_col) * 2);
-  const unsigned lane_off1 = (unsigned)((wm * 64 + r16) * g.ldc + lane_col);
   auto store_half = [&](int mi) {
     #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -822,13 +821,17 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
   // the same lane-pair exchange as the bf16 path (8 consecutive bytes per lane).  The four lanes of
   // a row hold the same exponents; lane q stores the scale dword (i = 0..3) of (mi, ni) = (q>>1, q&1).
   unsigned scw[2][2] = {{0u, 0u}, {0u, 0u}};
+  // Round 6: the two 128-column halves' 8-byte pieces of a row block are paired by one more lane-group swap
+  // (v_permlane32_swap: lanes q < 2 take half 0's 16 consecutive bytes, q >= 2 half 1's), so a row block goes out as
+  // ONE 16-B store per lane instead of two 8-B ones -- the per-CU store path costs per instruction, not per byte
+  //  -- and the row-major scales (RSC) as one byte store per half with every lane active (lane q
+  // stores row block i = q's exponent) instead of one per row block with a quarter of the lanes.
+  const unsigned lane_off16 = (unsigned)((wm * 64 + r16) * g.ldc + wn * 32 + (q & 1) * 16 + (q >> 1) * 128);
   auto store_half_q8 = [&](int mi) {
-    unsigned char* C8 = (unsigned char*)g.Ct;
+    int esel[2] = {0, 0};   // RSC: the exponents of row block i = q
     #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int m = m0 + mi * 128 + wm * 64 + i * 16 + r16;
-      const bool ok = m < g.M;
-      const long long row = (long long)(ok ? m : 0) * g.ldc;
+      u32x2 d[2];
       #pragma unroll
       for (int ni = 0; ni < 2; ++ni) {
         const f32x4 o0 = acc[mi][ni][i][0], o1 = acc[mi][ni][i][1];
@@ -856,12 +859,25 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
         w1 = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(w1, o1[2], o1[3], sc, true);
         const int x0 = __builtin_bit_cast(int, w0), x1 = __builtin_bit_cast(int, w1);
         const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)x0, (unsigned)x1, false, false);
-        __builtin_amdgcn_raw_buffer_store_b64(u32x2{sw[0], sw[1]}, ct_rsrc_of(mi, i, 1), lane_off1 + (unsigned)(ni * 128), 0u, 0);
-        if constexpr (RSC) {   // the row's four q lanes hold the same exponent: lane q == i stores it
-          if (q == i && ok) g.c_scale[(long long)m * (g.N >> 5) + ((n0 + ni * 128 + wn * 32) >> 5)] = (unsigned char)e;
+        d[ni] = u32x2{sw[0], sw[1]};   // 8 consecutive bytes: columns (q & 1) * 16 + (q >> 1) * 8 of block (ni, wn)
+        if constexpr (RSC) {   // the row's four q lanes hold the same exponent: lane q keeps row block i = q's
+          esel[ni] = q == i ? e : esel[ni];
         } else {
           scw[mi][ni] |= (unsigned)e << (8 * i);
         }
+      }
+      // v_permlane32_swap swaps lanes 32-63 of its first operand with lanes 0-31 of its second: lanes 0-31 (q < 2) end
+      // with their own half-0 piece | lane + 32's half-0 piece, lanes 32-63 with lane - 32's half-1 piece | their own
+      const auto t0 = __builtin_amdgcn_permlane32_swap(d[0][0], d[1][0], false, false);
+      const auto t1 = __builtin_amdgcn_permlane32_swap(d[0][1], d[1][1], false, false);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{t0[0], t1[0], t0[1], t1[1]}, ct_rsrc_of(mi, i, 1), lane_off16, 0u, 0);
+    }
+    if constexpr (RSC) {
+      const int m = m0 + mi * 128 + wm * 64 + q * 16 + r16;
+      if (m < g.M) {
+        #pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          g.c_scale[(long long)m * (g.N >> 5) + ((n0 + ni * 128 + wn * 32) >> 5)] = (unsigned char)esel[ni];
       }
     }
   };
@@ -2333,7 +2349,8 @@ int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
     if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       return -2;
     const int n_tiles = (int)grid.x;
-    const int G = n_tiles < cus[dev] ? n_tiles : cus[dev];
+    const int ncu = sse_stream_cus(s, cus[dev]);   // a CU-masked stream's own CUs
+    const int G = n_tiles < ncu ? n_tiles : ncu;
     const int ep = (a.bias ? 1 : 0) | (a.apart ? 2 : 0);
     auto go = [&](auto act, auto ct3, auto f16) {
       constexpr int AC = decltype(act)::value;

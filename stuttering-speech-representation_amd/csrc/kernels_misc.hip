@@ -455,7 +455,7 @@ int launch_conv0_gn(const float* x, int B, int L, const float* norm, const float
     if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       return -2;
     const int nchunk = (T0 + C0M_T - 1) / C0M_T;
-    int G = (3 * cus[dev] + B - 1) / B;
+    int G = (3 * sse_stream_cus(s, cus[dev]) + B - 1) / B;
     G = G < 1 ? 1 : (G > nchunk ? nchunk : G);
     hipLaunchKernelGGL(conv0_mfma_kernel<TO>, dim3(G, B), dim3(256), 0, s, x, L, norm, (const bf16x8*)wf, b0, T0,
                        (const float2*)ss, out);
@@ -973,7 +973,7 @@ __global__ __launch_bounds__(256) void layernorm_mx_kernel(const TI* __restrict_
 }
 
 // bf16 input: 8 elements (one 16-B load) per lane per 512-element chunk, so a row of 1280 is 3 load
-// instructions per lane instead of 5; an MX block of 32 is 4 lanes (DPP quad max); 8-byte fp8 stores.
+// instructions per lane instead of 5; an MX block of 32 is 4 lanes (DPP quad max); 16-byte fp8 stores (chunk pairs).
 SSE_DEV float max4_dpp(float v) {
   v = __builtin_elementwise_maximum(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true)));
   v = __builtin_elementwise_maximum(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true)));
@@ -1030,6 +1030,7 @@ __global__ __launch_bounds__(256) void layernorm_mx8_kernel(const bf16* __restri
           qs = fmaf(d, d, qs);
         }
     const float rstd = 1.0f / sqrtf(wave_sum_fast(qs) * inv_h + eps);
+    int xq[NC][2];   // this lane's 8 fp8 bytes of each chunk (stored below, chunk pairs as 16-B stores)
     #pragma unroll
     for (int i = 0; i < NC; ++i) {
       const int c = 512 * i + 8 * lane;
@@ -1051,10 +1052,27 @@ __global__ __launch_bounds__(256) void layernorm_mx8_kernel(const bf16* __restri
       x0 = __builtin_amdgcn_cvt_pk_fp8_f32(o[2] * inv, o[3] * inv, x0, true);
       int x1 = __builtin_amdgcn_cvt_pk_fp8_f32(o[4] * inv, o[5] * inv, 0, false);
       x1 = __builtin_amdgcn_cvt_pk_fp8_f32(o[6] * inv, o[7] * inv, x1, true);
-      if (ok) {
-        *(int2*)(q + (long long)row * H + c) = make_int2(x0, x1);
-        if ((lane & 3) == 0) sc[rr * LNMX_MAXB + (c >> 5)] = (unsigned char)e8;
-      }
+      xq[i][0] = x0;
+      xq[i][1] = x1;
+      if (ok && (lane & 3) == 0) sc[rr * LNMX_MAXB + (c >> 5)] = (unsigned char)e8;
+    }
+    // round 6: chunks 2p and 2p + 1 go out as 16-B stores (the per-CU store path costs per instruction): lane pairs
+    // (l, l ^ 1) swap pieces by DPP, the even lane stores columns 8l .. 8l + 15 of chunk 2p, the odd one columns
+    // 8(l - 1) .. of chunk 2p + 1; an unpaired last chunk keeps its 8-B stores
+    const bool odd = lane & 1;
+    unsigned char* qrow = q + (long long)row * H;
+    #pragma unroll
+    for (int i = 0; i + 1 < NC; i += 2) {
+      const int s0 = odd ? xq[i][0] : xq[i + 1][0], s1 = odd ? xq[i][1] : xq[i + 1][1];
+      const int r0v = __builtin_amdgcn_mov_dpp(s0, 0xB1, 0xF, 0xF, false);   // quad_perm [1, 0, 3, 2]
+      const int r1v = __builtin_amdgcn_mov_dpp(s1, 0xB1, 0xF, 0xF, false);
+      const int c = odd ? 512 * (i + 1) + 8 * (lane - 1) : 512 * i + 8 * lane;
+      const int4 v = odd ? make_int4(r0v, r1v, xq[i + 1][0], xq[i + 1][1]) : make_int4(xq[i][0], xq[i][1], r0v, r1v);
+      if (c < H) *(int4*)(qrow + c) = v;
+    }
+    if constexpr ((NC & 1) != 0) {
+      const int c = 512 * (NC - 1) + 8 * lane;
+      if (c < H) *(int2*)(qrow + c) = make_int2(xq[NC - 1][0], xq[NC - 1][1]);
     }
     #pragma unroll
     for (int i = 0; i < NC; ++i) cur[i] = nxt[i];
@@ -2684,7 +2702,7 @@ int launch_attention_full(const AttnArgs& a, int B, hipStream_t s) {
       return -2;
     if (per_cu[dev] < 1) per_cu[dev] = 1;
   }
-  const long long slots = (long long)cus[dev] * per_cu[dev];
+  const long long slots = (long long)sse_stream_cus(s, cus[dev]) * per_cu[dev];
   int hpb = 1;
   double best = 1e30;
   for (int c = 1; c <= a.nh; ++c) {   // fewest block rounds, then fewest blocks
@@ -3100,7 +3118,7 @@ int launch_attention_pipe2(const AttnArgs& a, int B, hipStream_t s) {
       if (pc < 1) pc = -1;
     }
     if (pc < 1) continue;
-    const long long slots = (long long)cus[dev] * pc;
+    const long long slots = (long long)sse_stream_cus(s, cus[dev]) * pc;
     const long long nb = (long long)(a.nh / c) * B;
     const long long rounds = (nb + slots - 1) / slots;
     const double cost = (double)rounds * (c + 1);
@@ -3138,7 +3156,7 @@ int launch_attention_pipe(const AttnArgs& a, int B, hipStream_t s) {
       if (pc < 1) pc = -1;
     }
     if (pc < 1) continue;
-    const long long slots = (long long)cus[dev] * pc;
+    const long long slots = (long long)sse_stream_cus(s, cus[dev]) * pc;
     const long long nb = (long long)(a.nh / c) * B;
     const long long rounds = (nb + slots - 1) / slots;
     const double cost = (double)rounds * (c + 1);

@@ -35,10 +35,34 @@ static int g_opt[OPT_COUNT] = {0};
 static const char* const g_opt_name[OPT_COUNT] = {"gemm_cfg", "gemm_nonpersist", "gelu_exact", "conv0_valu",
                                                    "posconv_gemm", "no_lnfold", "gemm_mx_staged", "no_split",
                                                    "logmel_v1", "ln_x3_v1", "attn_x3_f32", "ln_rows_v1", "posconv_2cl",
-                                                   "attn_short", "attn_long", "fp8_attn_bf16"};
+                                                   "attn_short", "attn_long", "fp8_attn_bf16", "split_cumask"};
 // the largest value each switch takes (0 .. max; anything else is SSE_ERR_INVALID, not a silent default)
-static const int g_opt_max[OPT_COUNT] = {3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 1};
+static const int g_opt_max[OPT_COUNT] = {3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 1, 2};
 int sse_opt(int id) { return __atomic_load_n(&g_opt[id], __ATOMIC_RELAXED); }
+
+// CU-masked streams (split_forward, OPT_SPLIT_CUMASK) and their CU counts; registered once, never removed
+// while the owning model lives (sse_model_destroy unregisters them)
+static std::mutex g_mask_mu;
+static std::vector<std::pair<hipStream_t, int>> g_mask_streams;
+int sse_stream_cus(hipStream_t s, int dev_cus) {
+  if (!s) return dev_cus;
+  std::lock_guard<std::mutex> lk(g_mask_mu);
+  for (const auto& e : g_mask_streams)
+    if (e.first == s) return e.second;
+  return dev_cus;
+}
+static void register_mask_stream(hipStream_t s, int cus) {
+  std::lock_guard<std::mutex> lk(g_mask_mu);
+  g_mask_streams.emplace_back(s, cus);
+}
+static void unregister_mask_stream(hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_mask_mu);
+  for (size_t i = 0; i < g_mask_streams.size(); ++i)
+    if (g_mask_streams[i].first == s) {
+      g_mask_streams.erase(g_mask_streams.begin() + i);
+      return;
+    }
+}
 
 namespace {
 
@@ -285,6 +309,10 @@ struct sse_model {
   static constexpr int MAX_PARTS = 4;
   hipStream_t aux[MAX_PARTS - 1] = {};
   hipEvent_t ev_fork = nullptr, ev_join[MAX_PARTS - 1] = {};
+  // OPT_SPLIT_CUMASK: both halves on CU-masked streams (mask kind 1 / 2), joined back to the caller's stream
+  hipStream_t mstream[2] = {};
+  hipEvent_t mjoin[2] = {};
+  int mkind = 0;
   std::mutex split_mu;
 
   template <typename X = void> const X* ptr(size_t off) const { return (const X*)(dmem + off); }
@@ -1582,13 +1610,48 @@ int split_forward(sse_model* m, const float* d_in, int B, int L, const Sink& sin
       }
     }
   }
+  // CU-masked halves (A/B option): each half-batch on its own half of the CUs, both forked from and joined to s
+  const int mk = P == 2 ? sse_opt(OPT_SPLIT_CUMASK) : 0;
+  if (mk && m->mkind != mk) {
+    for (int i = 0; i < 2; ++i) {
+      if (m->mstream[i]) {
+        unregister_mask_stream(m->mstream[i]);
+        (void)hipStreamDestroy(m->mstream[i]);
+        m->mstream[i] = nullptr;
+      }
+      if (!m->mjoin[i] && hipEventCreateWithFlags(&m->mjoin[i], hipEventDisableTiming) != hipSuccess) {
+        m->mjoin[i] = nullptr;
+        return SSE_ERR_HIP;
+      }
+    }
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, m->device) != hipSuccess || n <= 0 || n > 1024)
+      return SSE_ERR_HIP;
+    for (int i = 0; i < 2; ++i) {
+      std::vector<uint32_t> mask((n + 31) / 32, 0u);
+      int cnt = 0;
+      for (int c = 0; c < n; ++c) {
+        const bool mine = mk == 1 ? ((c < n / 2) == (i == 0)) : ((c & 1) == i);
+        if (mine) {
+          mask[c >> 5] |= 1u << (c & 31);
+          ++cnt;
+        }
+      }
+      if (hipExtStreamCreateWithCUMask(&m->mstream[i], (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+        m->mstream[i] = nullptr;
+        return SSE_ERR_HIP;
+      }
+      register_mask_stream(m->mstream[i], cnt);
+    }
+    m->mkind = mk;
+  }
   if (hipEventRecord(m->ev_fork, s) != hipSuccess) return SSE_ERR_HIP;
   int rc = 0, b0 = 0;
   size_t off = 0;
   for (int i = 0; i < P; ++i) {
     const int Bi = part_size(B, P, i);
-    hipStream_t si = i ? m->aux[i - 1] : s;
-    if (i && hipStreamWaitEvent(si, m->ev_fork, 0) != hipSuccess) return SSE_ERR_HIP;
+    hipStream_t si = mk ? m->mstream[i] : (i ? m->aux[i - 1] : s);
+    if ((i || mk) && hipStreamWaitEvent(si, m->ev_fork, 0) != hipSuccess) return SSE_ERR_HIP;
     Sink sk = sink;
     sk.B = Bi;
     sk.pooled = sink.pooled + (size_t)b0 * sink.n_ids * sink.H;
@@ -1599,6 +1662,12 @@ int split_forward(sse_model* m, const float* d_in, int B, int L, const Sink& sin
     b0 += Bi;
   }
   // the joins are recorded whatever happened, so the caller's stream never runs ahead of aux work
+  if (mk) {
+    for (int i = 0; i < 2; ++i)
+      if (hipEventRecord(m->mjoin[i], m->mstream[i]) != hipSuccess || hipStreamWaitEvent(s, m->mjoin[i], 0) != hipSuccess)
+        return SSE_ERR_HIP;
+    return rc;
+  }
   for (int i = 0; i < P - 1; ++i)
     if (hipEventRecord(m->ev_join[i], m->aux[i]) != hipSuccess || hipStreamWaitEvent(s, m->ev_join[i], 0) != hipSuccess)
       return SSE_ERR_HIP;
@@ -1791,6 +1860,13 @@ void sse_model_destroy(sse_model* m) {
   for (int i = 0; i < sse_model::MAX_PARTS - 1; ++i) {
     if (m->ev_join[i]) (void)hipEventDestroy(m->ev_join[i]);
     if (m->aux[i]) (void)hipStreamDestroy(m->aux[i]);
+  }
+  for (int i = 0; i < 2; ++i) {
+    if (m->mjoin[i]) (void)hipEventDestroy(m->mjoin[i]);
+    if (m->mstream[i]) {
+      unregister_mask_stream(m->mstream[i]);
+      (void)hipStreamDestroy(m->mstream[i]);
+    }
   }
   if (m->dmem) {
     int prev = -1;
@@ -2102,6 +2178,13 @@ long long sse_mx_scale_offset(int role, int r, int b, int K) {
 int sse_mx_quantize(const float* d_x, int R, int K, int role, uint8_t* d_q, uint8_t* d_scale, void* stream) {
   if (!d_x || !d_q || !d_scale || R <= 0 || K <= 0 || K % 128 || (role != 0 && role != 1)) return SSE_ERR_INVALID;
   return launch_mx_quantize(d_x, R, K, role, d_q, d_scale, (hipStream_t)stream) ? SSE_ERR_HIP : SSE_OK;
+}
+
+int sse_layernorm_mx(const void* d_x, const float* d_w, const float* d_b, int R, int H, float eps, uint8_t* d_q,
+                     uint8_t* d_scale, void* stream) {
+  if (!d_x || !d_w || !d_b || !d_q || !d_scale || R <= 0 || H <= 0 || H % 128 || H > 2048) return SSE_ERR_INVALID;
+  return launch_layernorm_mx<bf16>((const bf16*)d_x, d_w, d_b, R, H, eps, d_q, d_scale, (hipStream_t)stream) ? SSE_ERR_HIP
+                                                                                                            : SSE_OK;
 }
 
 int sse_mx_quantize_host(const float* x, int R, int K, int role, uint8_t* q, uint8_t* scale) {

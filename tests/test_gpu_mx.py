@@ -45,6 +45,41 @@ def test_gpu_quantiser_matches_restatement(role):
     assert np.array_equal(mx.exps_from_scales(sc.cpu().numpy(), R, K, role), mx.exps_from_scales(sch, R, K, role))
 
 
+@pytest.mark.parametrize("R,H", [(300, 1280), (257, 768), (64, 512), (131, 384)])
+def test_layernorm_mx_producer(R, H):
+    """The LN -> MX-fp8 producer of the fp8 encoder (layernorm_mx8_kernel via the sse_layernorm_mx hook): its codes
+    and scales against oracle/mx.py applied to an fp32 LayerNorm of the same bf16 rows.  The kernel's fp32 statistics
+    sum in a different order than numpy, so a value next to a rounding boundary may take the neighbouring code: >= 99.5 %
+    of codes equal, >= 99.9 % within one code, >= 99.5 % of scales equal.  Round 6 stores chunk pairs as 16-B stores (lane
+    pairs swap 8-B pieces): H = 1280 (3 chunks: a pair + a lone partial chunk), 768 (a pair with a partial chunk),
+    512 (a lone full chunk), 384 (a lone partial chunk) -- a misplaced piece would break whole 8-byte runs."""
+    import ctypes
+    from ssr_amd import _lib
+    from ssr_amd.model import mx_scale_bytes
+    rng = np.random.default_rng(R + H)
+    x = (rng.standard_normal((R, H)) * 2.0 + rng.standard_normal((R, 1)) * 3.0).astype(np.float32)
+    xb = torch.from_numpy(x).to(torch.bfloat16)
+    w = (1.0 + 0.2 * rng.standard_normal(H)).astype(np.float32)
+    b = (0.1 * rng.standard_normal(H)).astype(np.float32)
+    q = torch.full((R + 8, H), 0xA5, dtype=torch.uint8, device="cuda")
+    sc = torch.zeros(mx_scale_bytes(R, H), dtype=torch.uint8, device="cuda")
+    xd, wd, bd = xb.cuda(), torch.from_numpy(w).cuda(), torch.from_numpy(b).cuda()
+    rc = _lib.lib().sse_layernorm_mx(xd.data_ptr(), wd.data_ptr(), bd.data_ptr(), R, H, ctypes.c_float(1e-5),
+                                     q.data_ptr(), sc.data_ptr(), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    _lib.check(rc, "sse_layernorm_mx")
+    torch.cuda.synchronize()
+    assert bool((q[R:] == 0xA5).all()), "store past row R"
+    xf = xb.float().numpy().astype(np.float64)
+    mean = xf.mean(1, keepdims=True)
+    var = ((xf - mean) ** 2).mean(1, keepdims=True)
+    ln = (((xf - mean) / np.sqrt(var + 1e-5)) * w + b).astype(np.float32)
+    q0, _, e0 = mx.quantize(ln, 0)
+    qg = q[:R].cpu().numpy()
+    assert (qg == q0).mean() >= 0.995
+    assert (np.abs(qg.astype(np.int16) - q0.astype(np.int16)) <= 1).mean() >= 0.999   # sign-magnitude codes
+    assert (mx.exps_from_scales(sc.cpu().numpy(), R, H, 0) == e0).mean() >= 0.995
+
+
 def _operands(M, N, K, seed):
     rng = np.random.default_rng(seed)
     a = rng.standard_normal((M, K)).astype(np.float32)

@@ -15,6 +15,7 @@
 static int g_pipe = 0;
 // g_pipe: 0 full, 1 pipelined (double-buffered, one block per CU), 2 two blocks per CU -> option attn_short 1, 0, 2
 int sse_opt(int id) { return id == OPT_ATTN_SHORT ? (g_pipe == 0 ? 1 : (g_pipe == 1 ? 0 : 2)) : 0; }
+int sse_stream_cus(hipStream_t, int dev_cus) { return dev_cus; }
 
 #define CK(x)                                                                      \
   do {                                                                             \

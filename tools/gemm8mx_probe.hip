@@ -10,6 +10,7 @@
 #include <cstdlib>
 
 int sse_opt(int) { return 0; }
+int sse_stream_cus(hipStream_t, int dev_cus) { return dev_cus; }
 
 #define CK(x)                                                                              \
   do {                                                                                     \
