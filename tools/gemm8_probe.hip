@@ -10,6 +10,282 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off tools/gemm8_probe.hip -o tools/_build/gemm8_probe
 #include "../stuttering-speech-representation_amd/csrc/kernels_gemm8.hip"
 
+namespace {
+// ======================================================================================
+// Two co-resident 256x128 workgroups per CU (round 6, VERDICT r5 item 1: hide one tile's epilogue under
+// the other tile's main loop).  gemm8p_kernel holds a 256x256 fp32 accumulator tile = half of every SIMD's
+// 512-entry register file, so the next tile's MFMAs cannot run while a tile drains its epilogue; the per-CU
+// store path (~23 B/clk) leaves ~25 % of a K = 768 round exposed.  Here a workgroup is 4 waves
+// (one per SIMD) owning a 256-row x 128-column tile (128 accumulator registers per lane), two workgroups per
+// CU (launch bounds: <= 256 VGPRs; 80 KiB of LDS each), one tile per workgroup: while one workgroup runs its
+// epilogue or its prologue, the other one's MFMAs keep the SIMDs' matrix pipes busy, and the dispatcher
+// starts the next tile in the freed slot.  The price is operand traffic: per 64-deep K step 96 KiB per
+// 256 x 256 of output instead of 64 (A is read by both column halves).
+//   * K-tile = 32 (64 B per row), a 3-stage LDS ring of A 256 x 64 B | B 128 x 64 B (24 KiB per stage): the
+//     stage of K-tile t + 2 is issued right after the barrier of K-tile t (its buffer held K-tile t - 1, whose
+//     reads finished before that barrier), so every LDS-DMA has two K-tiles of MFMAs to land.
+//   * 16-B chunk c of row r holds logical chunk c ^ swz(r), swz = [0, 2, 3, 1][(r >> 2) & 3]: the MFMA
+//     fragment reads (lane (q, r16) reads chunk q of row r16) are conflict-free in ds_read_b128's 16-lane groups
+//     with 64-B rows (the 128-B-row swizzle of gemm8p does not apply).
+//   * wave (wm, wn) of the 2 x 2 grid owns rows wm*128 + [0, 128) and columns wn*64 + [0, 64): per K-tile 8 A
+//     and 4 B fragments (12 ds_read_b128), 32 MFMAs 16x16x32 computing C^T blocks (the same products in the
+//     same K order as gemm8p_kernel: outputs bit-identical to it, tests/test_gpu_kernels.py).
+//   * epilogue parameters (bias, folded-LN column sums, the rows' LayerNorm partials) go to LDS by DMA before
+//     the operand prologue and are retired by the first counted wait; the epilogue is g8p_epilogue's
+//     arithmetic on this tile's layout, stores through per-16-row-block buffer resources (rows >= M dropped).
+// (Probe-only since the measurement: the library keeps gemm8p_kernel)
+// LDS: 3 x 24 KiB operands | bias [0, 512) acol [1 K, 1.5 K) partials [2 K, 8 K) = 80 KiB per workgroup.
+constexpr int G8H_STAGE = 24 * 1024;
+constexpr int G8H_OPS = 3 * G8H_STAGE;
+constexpr int G8H_SMEM = G8H_OPS + 8 * 1024;
+
+// chunk swizzle of a 64-B row (see above): [0, 2, 3, 1] by (row >> 2) & 3
+SSE_DEV int g8h_swz(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
+
+// DBG (timing probes only, tools/gemm8_probe.hip; the library launches DBG = 0): 2 = no epilogue
+// (accumulators kept live), 4 = no epilogue and no MFMA (the fragment reads kept live), 5 = no epilogue and
+// no main-loop LDS-DMA.
+template <int ACT, int EP = 1, int DBG = 0, int FNT = 3>
+__global__ __launch_bounds__(256, 2) void gemm8h_kernel(GemmArgs g) {
+  static_assert(FNT == 3, "the parameter DMA stages 6 KiB of row partials (H = 768)");
+  __shared__ __attribute__((aligned(16))) char smem[G8H_SMEM];   // the ONLY shared object
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int q = lane >> 4, r16 = lane & 15;
+  const int M = g.M, K = g.K;
+  const int n_tiles_n = g.N / 128;
+  const int nk = K / 32;
+  constexpr bool has_bias = (EP & 1) != 0, fold = (EP & 2) != 0;
+  int bid = blockIdx.x;
+  {   // XCD-aware bijective remap: XCD x walks a contiguous range of row-major tiles
+    const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
+    bid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
+  }
+  const int m0 = (bid / n_tiles_n) * 256, n0 = (bid % n_tiles_n) * 128;
+  char* const ep = smem + G8H_OPS;
+
+  // ---- epilogue parameters into LDS first (2 DMAs per wave, retired by the first counted wait): waves 0-2 the
+  // row partials (2 KiB each), wave 3 the bias and the column sums (512 B each, the other half-piece reads zeros)
+  {
+    const void* zb = g.zero;
+    if (wave < 3) {
+      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(fold ? (const void*)g.apart : zb), (short)0, fold ? M * FNT * 8 : 0, 0x00020000);
+      #pragma unroll
+      for (int u = 0; u < 2; ++u)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, LPTR(ep + 2048 + (2 * wave + u) * 1024), 16, (unsigned)lane * 16u,
+                                                 (unsigned)(m0 * FNT * 8 + (2 * wave + u) * 1024), 0, 0);
+    } else {
+      const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(has_bias ? (const void*)(g.bias + n0) : zb), (short)0, has_bias ? 512 : 0, 0x00020000);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, LPTR(ep), 16, (unsigned)lane * 16u, 0u, 0, 0);
+      const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(fold ? (const void*)(g.acol + n0) : zb), (short)0, fold ? 512 : 0, 0x00020000);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, LPTR(ep + 1024), 16, (unsigned)lane * 16u, 0u, 0, 0);
+    }
+  }
+
+  // ---- LDS-DMA sources: one descriptor per operand based at the tile's first row, per-lane byte offsets fixed
+  // over K, the scalar offset advancing 64 B per K-tile.  Piece p (1 KiB) = rows 16p .. 16p + 15: lane l writes
+  // LDS chunk l & 3 of row 16p + (l >> 2), which holds logical chunk (l & 3) ^ swz(row).  A: pieces wave + 4u
+  // (u < 4), B: pieces wave + 4u (u < 2).
+  constexpr int NREC = 0x7FFFFFF0;
+  __amdgpu_buffer_rsrc_t a_rsrc, b_rsrc;
+  unsigned a_voff[4], b_voff[2];
+  {
+    const int mf = m0 < M ? m0 : M - 1;
+    const int seg0 = mf / g.rows_per_seg, rr0 = mf - seg0 * g.rows_per_seg;
+    const long long a_base = ((long long)seg0 * g.seg_stride + (long long)rr0 * g.lda) * 2;   // bytes
+    a_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)g.A + a_base), (short)0, NREC, 0x00020000);
+    b_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)g.B + (long long)n0 * K * 2), (short)0, NREC,
+                                               0x00020000);
+    #pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int row = (wave + 4 * u) * 16 + (lane >> 2);
+      const int ch = (lane & 3) ^ g8h_swz(row);
+      int m = m0 + row;
+      m = m < M ? m : M - 1;
+      const int seg = m / g.rows_per_seg, rr = m - seg * g.rows_per_seg;
+      const long long el = ((long long)seg * g.seg_stride + (long long)rr * g.lda) * 2 + ch * 16;
+      a_voff[u] = (unsigned)(el - a_base);
+      if (u < 2) b_voff[u] = (unsigned)((long long)row * K * 2 + ch * 16);
+    }
+  }
+  auto issue = [&](int t, int buf) {   // K-tile t into ring slot buf (6 LDS-DMA per wave)
+    char* dst = smem + buf * G8H_STAGE;
+    const unsigned soff = (unsigned)t * 64u;
+    #pragma unroll
+    for (int u = 0; u < 4; ++u)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, LPTR(dst + (wave + 4 * u) * 1024), 16, a_voff[u], soff, 0, 0);
+    #pragma unroll
+    for (int u = 0; u < 2; ++u)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, LPTR(dst + 16384 + (wave + 4 * u) * 1024), 16, b_voff[u], soff,
+                                               0, 0);
+  };
+
+  f32x4 acc[2][2][4][2];   // [mi][ni][i][j]: rows wm*128 + mi*64 + i*16 + r16, columns wn*64 + ni*32 + j*16 + 4q
+  #pragma unroll
+  for (int a = 0; a < 2; ++a)
+    #pragma unroll
+    for (int c = 0; c < 2; ++c)
+      #pragma unroll
+      for (int i = 0; i < 4; ++i)
+        #pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][c][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // this lane's fragment byte offset inside a 16-row block: row r16, logical chunk q (rows 16k + r16 share it)
+  const int frag = r16 * 64 + ((q ^ g8h_swz(r16)) << 4);
+  const int a_frag = (wm * 128) * 64 + frag, b_frag = 16384 + (wn * 64) * 64 + frag;
+  auto k_tile = [&](int buf) {
+    const char* s = smem + buf * G8H_STAGE;
+    bf16x8 af[8], bfr[4];
+    #pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = *(const bf16x8*)(s + b_frag + j * 1024);
+    #pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = *(const bf16x8*)(s + a_frag + i * 1024);
+    if constexpr (DBG == 4) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      #pragma unroll
+      for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(af[i]));
+      #pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(bfr[j]));
+      return;
+    }
+    #pragma unroll
+    for (int i = 0; i < 8; ++i)
+      #pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f32x4& c = acc[i >> 2][j >> 1][i & 3][j & 1];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], c, 0, 0, 0);
+      }
+  };
+
+  // ---- main loop: wait for K-tile t (this wave's 6 DMAs of t + 1 may stay in flight), barrier (every wave's
+  // DMAs of t landed; every wave's reads of t - 1 done), issue t + 2 into t - 1's slot, compute t
+  if constexpr (DBG != 5) {
+    issue(0, 0);
+    if (nk > 1) issue(1, 1);
+  }
+  int buf = 0;   // ring slot of K-tile t
+  int t = 0;
+  for (; t + 2 < nk; ++t) {
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    g8_barrier();
+    if constexpr (DBG != 5) issue(t + 2, buf == 0 ? 2 : buf - 1);
+    k_tile(buf);
+    buf = buf == 2 ? 0 : buf + 1;
+  }
+  for (; t < nk; ++t) {
+    if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    g8_barrier();
+    k_tile(buf);
+    buf = buf == 2 ? 0 : buf + 1;
+  }
+  if constexpr (DBG == 5) {   // (the parameter DMA is still to be waited for)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if constexpr (DBG == 2 || DBG == 4 || DBG == 5) {
+    #pragma unroll
+    for (int a = 0; a < 2; ++a)
+      #pragma unroll
+      for (int c = 0; c < 2; ++c)
+        #pragma unroll
+        for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(acc[a][c][i][0]), "v"(acc[a][c][i][1]));
+    return;
+  }
+
+  // ---- epilogue (g8p_epilogue's arithmetic): o = act(rstd_m acc + (bias[n] - rstd_m mean_m acol[n])), or
+  // act(acc + bias[n]) without the fold; bf16 pairs of lanes (q, q ^ 1) exchanged so each lane stores 8
+  // consecutive columns (one 16-B store per (mi, i, ni))
+  {   // lane-derived values from an opaque lane id (kept out of the main loop's registers)
+    int ln = (int)(threadIdx.x & 63);
+    asm volatile("" : "+v"(ln));
+    const int qq = ln >> 4, rr = ln & 15;
+    f32x4 bv[2][2], ac[2][2];
+    #pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+      #pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c = wn * 64 + ni * 32 + j * 16 + qq * 4;
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        const f32x4 b = *(const f32x4*)(ep + c * 4), a = *(const f32x4*)(ep + 1024 + c * 4);
+        bv[ni][j] = has_bias ? b : z;
+        ac[ni][j] = fold ? a : z;
+      }
+    auto finish_half = [&](int mi) {
+      asm volatile("" ::: "memory");
+      float2 ast[4];
+      #pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float2* p = (const float2*)(ep + 2048) + (wm * 128 + mi * 64 + i * 16 + rr) * FNT;
+        float2 v[FNT];
+        #pragma unroll
+        for (int u = 0; u < FNT; ++u) v[u] = p[u];
+        const float2 st = ln_part_combine<FNT>(v, g.ln_eps);
+        ast[i] = fold ? st : make_float2(0.f, 1.f);
+      }
+      #pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float rs = ast[i].y, nm = -ast[i].x * ast[i].y;
+        #pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          #pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            f32x4 o;
+            #pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = fmaf(acc[mi][ni][i][j][e], rs, fmaf(nm, ac[ni][j][e], bv[ni][j][e]));
+            if constexpr (ACT == ACT_GELU) {
+              const f32x2 lo = gelu_erf2(f32x2{o[0], o[1]}), hi = gelu_erf2(f32x2{o[2], o[3]});
+              o = f32x4{lo.x, lo.y, hi.x, hi.y};
+            }
+            acc[mi][ni][i][j] = o;
+          }
+        if constexpr (ACT == ACT_GELU_FAST) {
+          f32x2 o2[8];
+          #pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const f32x4 v = acc[mi][u >> 1][i][u & 1];
+            o2[2 * u] = f32x2{v[0], v[1]};
+            o2[2 * u + 1] = f32x2{v[2], v[3]};
+          }
+          gelu_out2_n<false, 8>(o2);
+          #pragma unroll
+          for (int u = 0; u < 4; ++u) acc[mi][u >> 1][i][u & 1] = f32x4{o2[2 * u].x, o2[2 * u].y, o2[2 * u + 1].x, o2[2 * u + 1].y};
+        }
+      }
+    };
+    const unsigned lane_off = (unsigned)((rr * g.ldc + wn * 64 + (qq & 1) * 16 + (qq >> 1) * 8) * 2);
+    auto store_half = [&](int mi) {
+      #pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const long long r0 = (long long)m0 + wm * 128 + mi * 64 + i * 16, rows = (long long)M - r0;
+        const long long nrec = rows > 0 ? (rows * g.ldc - n0) * 2 : 0;
+        const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)((bf16*)g.Ct + (rows > 0 ? r0 * g.ldc + n0 : 0)), (short)0, (int)min(nrec, (long long)0x7FFFFFF0),
+            0x00020000);
+        #pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          const f32x4 o0 = acc[mi][ni][i][0], o1 = acc[mi][ni][i][1];
+          const bf16x4 x0 = {(bf16)o0[0], (bf16)o0[1], (bf16)o0[2], (bf16)o0[3]};
+          const bf16x4 x1 = {(bf16)o1[0], (bf16)o1[1], (bf16)o1[2], (bf16)o1[3]};
+          const uint2 X = __builtin_bit_cast(uint2, x0), Y = __builtin_bit_cast(uint2, x1);
+          const auto s0 = __builtin_amdgcn_permlane16_swap(X.x, Y.x, false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(X.y, Y.y, false, false);
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{s0[0], s1[0], s0[1], s1[1]}, cr, lane_off + (unsigned)(ni * 64), 0u, 0);
+        }
+      }
+    };
+    finish_half(0);
+    store_half(0);
+    finish_half(1);
+    store_half(1);
+  }
+}
+
+}  // namespace
+
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
