@@ -291,6 +291,7 @@ struct sse_model {
   size_t dec_x0, dec_ln_w, dec_ln_b;   // decoder: embed_tokens[0] + embed_positions[0]; final LN
   std::vector<DecLayerW> dec;
   bool ln_fold = false;   // folded-LayerNorm weights present (bf16 post-LN WavLM, LayerW.qkv_wf / f1_wf)
+  bool pre_fold = false;  // bf16 stable-LN WavLM (large): each layer's attention LayerNorm folded into its QKV (l > 0)
   int ldq = 0;   // QKV GEMM width: 3H (+ 8*heads gate columns for WavLM, then zero pad to 256 so the
                 // 256x256 MFMA tile applies)
   std::vector<LayerW> layers;
@@ -419,6 +420,11 @@ int build_wavlm(sse_model* m, Blob& bl, Arena& ar) {
     m->relb = ar.put_f32(tab.data(), tab.size());
   }
   const bool fold = m->half() && !c.stable_layer_norm && H == 768;   // the GEMM epilogues combine 3 column-tile partials
+  // stable-LN (pre-LN, WavLM-large) in bf16: the QKV of layers l > 0 reads the bf16 residual stream itself with
+  // W' = W diag(ln1_w), the previous layer's ffn2 writing the rows' per-256-column partials (round 6); the GEMM
+  // epilogue's fold takes 3-5 partials per row on the plain bf16 kernel (H = 768..1280).  fc1 keeps its LayerNorm
+  // kernel (its GELU epilogue with 4-5 partials spills, as for Whisper-large-v2)
+  const bool prefold = m->dtype == SSE_DTYPE_BF16 && c.stable_layer_norm && H % 256 == 0 && H >= 768 && H <= 1280;
   const float *prev_l2w = nullptr, *prev_l2b = nullptr;
   for (int l = 0; l < c.layers; ++l) {
     const float *qw = bl.take((size_t)H * H), *qb = bl.take(H), *kw = bl.take((size_t)H * H), *kb = bl.take(H);
@@ -471,11 +477,13 @@ int build_wavlm(sse_model* m, Blob& bl, Arena& ar) {
         put_folded(ar, qkv.data(), qkvb.data(), ldq, H, prev_l2w, prev_l2b, &L.qkv_wf, &L.qkv_c, &L.qkv_bf, m->h16());
       put_folded(ar, f1w, f1b, F, H, l1w, l1b, &L.f1_wf, &L.f1_c, &L.f1_bf, m->h16());
     }
+    if (prefold && l > 0) put_folded(ar, qkv.data(), qkvb.data(), ldq, H, l1w, l1b, &L.qkv_wf, &L.qkv_c, &L.qkv_bf, false);
     prev_l2w = l2w;
     prev_l2b = l2b;
     m->layers.push_back(L);
   }
   m->ln_fold = fold;
+  m->pre_fold = prefold;
   return bl.ok ? SSE_OK : SSE_ERR_WEIGHTS;
 }
 
@@ -951,13 +959,17 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
   float2* p1 = (float2*)(ws + w.p1);
   float2* p2 = (float2*)(ws + w.p2);
   T* xs = xt;   // bf16 residual sum after the attention (xt, the projection output, is free by now)
+  // bf16 stable-LN (WavLM-large, round 6): layer l > 0's attention LayerNorm folded into its QKV (the previous ffn2
+  // writes the partials p2 of the bf16 stream); layer 0 and fc1 keep their LayerNorm kernels
+  const bool prefold = pre16 && m->pre_fold && !sse_opt(OPT_NO_LNFOLD);
   for (int l = 0; l < c.layers; ++l) {
     const LayerW& Lw = m->layers[l];
     const LayerW* Lp = l > 0 ? &m->layers[l - 1] : nullptr;
-    if (pre16)
-      RC((launch_layernorm<T, T>(x16, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, ACT_NONE,
-                                 nullptr, xb, s)));
-    else if (c.stable_layer_norm)
+    if (pre16) {
+      if (!(prefold && l > 0))
+        RC((launch_layernorm<T, T>(x16, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, ACT_NONE,
+                                   nullptr, xb, s)));
+    } else if (c.stable_layer_norm)
       RC((launch_layernorm<float, T>(x, m->ptr<float>(Lw.ln1_w), m->ptr<float>(Lw.ln1_b), M, H, eps, ACT_NONE,
                                      nullptr, xb, s)));
     GemmArgs g{};
@@ -965,6 +977,10 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     g.rows_per_seg = M; g.lda = H; g.bias = m->ptr<float>(Lw.qkv_b); g.Ct = qkv; g.ldc = m->ldq; g.zero = zero;
     if (lnfold && l > 0) {   // xb = bf16 of the previous layer's un-normalised sum: its final LN folded
       g.B = m->ptr(Lw.qkv_wf); g.bias = m->ptr<float>(Lw.qkv_bf); g.acol = m->ptr<float>(Lw.qkv_c);
+      g.apart = p2; g.apart_nt = nt; g.ln_eps = eps;
+    }
+    if (prefold && l > 0) {   // the bf16 stream itself, this layer's attention LN folded (partials from ffn2)
+      g.A = x16; g.B = m->ptr(Lw.qkv_wf); g.bias = m->ptr<float>(Lw.qkv_bf); g.acol = m->ptr<float>(Lw.qkv_c);
       g.apart = p2; g.apart_nt = nt; g.ln_eps = eps;
     }
     // algorithmic FLOPs count the 3H + 8*heads useful columns, not the zero pad to ldq
@@ -1019,6 +1035,7 @@ int wavlm_forward(sse_model* m, const float* wave, int B, int L, const Sink& sin
     }
     if (pre16) {
       g.resid = nullptr; g.Cf = nullptr; g.resid_t = (const bf16*)x16; g.Ct = x16;
+      if (prefold && l + 1 < c.layers) g.opart = p2;   // the next QKV's LayerNorm statistics
     }
     RC(prof(m, s, "gemm:ffn2", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
     if (pre16) {

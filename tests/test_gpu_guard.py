@@ -142,19 +142,19 @@ TDT = {1: torch.bfloat16, 4: torch.float16, 0: torch.float32}
 
 
 @pytest.mark.parametrize("M", [4097, 4113, 4351, 38161])
-@pytest.mark.parametrize("form", ["ep0", "ep1_gelu", "fold_ep3", "fold_ep3_gelu", "fold_fnt5", "h16_ep1_gelu",
+@pytest.mark.parametrize("form", ["ep0", "ep1_gelu", "fold_ep3", "fold_ep3_gelu", "fold_fnt4", "fold_fnt5", "h16_ep1_gelu",
                                   "staged_cf_ct"])
 def test_gemm_nonresidual_guard_bands(M, form):
     """gemm8p_kernel's register-direct epilogue (one buffer resource per 16-row block; bug A: each column
     tile's stores based at its own column, caught by the window check; bug B: rows >= M of the partial
     last row tile, caught by the guard rows) for EP 0 (no bias), 1 (bias, GELU), 3 (folded LayerNorm,
-    FNT 3 and 5), fp16 operands; and the LDS-staged 8-phase kernel (GELU with fp32 + bf16 outputs).
+    FNT 3, 4 (WavLM-large's QKV) and 5), fp16 operands; and the LDS-staged 8-phase kernel (GELU with fp32 + bf16 outputs).
     M = 38161 (149 full row tiles + 17 rows) x N = 1536 is 900 tiles: every persistent block walks 3-4
     tiles (the epilogue's stores stay in flight under the next tile's first K-tile)."""
     dt = torch.float16 if form.startswith("h16") else torch.bfloat16
     code = 4 if dt == torch.float16 else 1
-    K = {"fold_ep3": 768, "fold_ep3_gelu": 768, "fold_fnt5": 1280}.get(form, 192)
-    N = 512 if form != "fold_fnt5" else 768
+    K = {"fold_ep3": 768, "fold_ep3_gelu": 768, "fold_fnt4": 1024, "fold_fnt5": 1280}.get(form, 192)
+    N = 768 if form in ("fold_fnt4", "fold_fnt5") else 512
     if M > 30000:
         N *= 3
     ldc = N + 64

@@ -173,6 +173,29 @@ def test_bf16_lnfold_matches_materialised(wavlm_sd):
     assert _rel(a[:2], pooled_hs).max() <= 1e-5
 
 
+def test_large_bf16_qkv_fold_matches_materialised():
+    """WavLM-large (stable-LN) in bf16: layers l > 0 run no attention LayerNorm kernel -- the previous
+    ffn2 writes per-256-column partials of the rounded bf16 stream and the QKV GEMM applies the
+    LayerNorm through folded weights (FNT = 4 partials per row, H = 1024).  Against the materialised
+    flow (no_lnfold=1) by tolerance and by the distance of each to the fp32 path."""
+    from ssr_amd import _lib, config as C, synth
+    from ssr_amd.model import SSEModel
+    sd = synth.synth_wavlm_state_dict(C.WAVLM_LARGE, seed=9)
+    m = SSEModel(C.WAVLM_LARGE, sd, device="cuda:0", dtype="bf16", do_normalize=True)
+    w = torch.from_numpy(synth.synth_clips(5, 48000, seed=23)).cuda()
+    idx = [24, 18, 12, 6, 1]
+    a = m.embed(w, idx).cpu().numpy()
+    with _lib.option("no_lnfold", 1):
+        b = m.embed(w, idx).cpu().numpy()
+    del m
+    m32 = SSEModel(C.WAVLM_LARGE, sd, device="cuda:0", dtype="fp32", do_normalize=True)
+    r = m32.embed(w, idx).cpu().numpy()
+    e_a, e_b = _rel(a, r).max(), _rel(b, r).max()
+    print("large folded vs materialised", _rel(a, b).max(), "| vs fp32: folded", e_a, "materialised", e_b)
+    assert _rel(a, b).max() <= 2e-2
+    assert e_a <= 1.25 * e_b + 1e-3 and e_a <= BF16_TOL
+
+
 @pytest.mark.parametrize("n_clips,samples", [(7, 48000), (2, 16000), (3, 80000), (3, 160000), (1, 170000)])
 def test_bf16_posconv_kernel_matches_grouped_gemm(wavlm_sd, n_clips, samples):
     """The dedicated positional-conv kernel (input window staged once per block, kernels_posconv.hip)
