@@ -233,6 +233,14 @@ int sse_attention(const void* d_qkv, void* d_out, int B, int T, int H, int nh, i
 int sse_attention_f8(const uint8_t* d_qk, const uint8_t* d_qk_scale, const void* d_v, const uint32_t* d_vamax,
                      void* d_out, int B, int T, int H, int nh, void* stream);
 
+/* sse_attention_f8 with the output as MX-fp8 (test hook; round 6: with option f8_oproj = 1 the SSE_DTYPE_FP8
+ * Whisper path's attention writes this and its out-projection runs on the MX GEMM): d_out_q e4m3 [B*T][H], d_out_scale the E8M0 exponents of every 32-column block in the MX GEMM's
+ * A-operand layout for K = H (sse_mx_scale_bytes(B*T, H) bytes; the layout sse_mx_quantize role 0 writes).  Each
+ * block's exponent is the smallest E with max |o| <= 448 * 2^E over its fp32 outputs, each code RNE(o * 2^-E).
+ * H % 128 == 0.  Same reference line as sse_attention_f8. */
+int sse_attention_f8_mx(const uint8_t* d_qk, const uint8_t* d_qk_scale, const void* d_v, const uint32_t* d_vamax,
+                        uint8_t* d_out_q, uint8_t* d_out_scale, int B, int T, int H, int nh, void* stream);
+
 /* Every epilogue form of the path's GEMMs behind one test hook (guard-band and epilogue tests; no
  * reference counterpart).  C[M][N] = A[M][K] . B[N][K]^T with, by the non-null fields:
  *   bias[N]; act (0 none, 1 erf-GELU, 2 the bf16 path's GELU);
@@ -340,6 +348,9 @@ const char* sse_version(void);
  *   "attn_long"         Whisper bf16 / fp8 encoder attention: 0 = the 32x32 swapped-product kernel with two
  *                       32-query blocks per wave (production), 2 = the same with one (identical outputs),
  *                       1 = the 16x16 flash kernel (same bar, not bit-identical)
+ *   "fp8_attn_bf16"     1 = the fp8 Whisper path keeps the bf16 QKV output and the bf16 flash attention
+ *   "f8_oproj"          1 = the fp8 Whisper path's attention writes MX-fp8 and its out-projection runs on the MX
+ *                       GEMM (opt-in: Whisper-large-v2 then misses the fp8 bar, 0.083 vs 0.08 rel-L2)
  * sse_set_option returns the previous value (>= 0), or SSE_ERR_INVALID for an unknown name or a value outside
  * the switch's range (0..1; gemm_cfg 0..3, attn_short 0..2, attn_long 0..2, split_cumask 0..2) -- nothing is changed then. */
 int sse_set_option(const char* name, int value);

@@ -7,6 +7,7 @@ attention operands rounded the way a GPU path stores them, products accumulated 
 
   gemm mx8     qkv / fc1 / fc2: both operands MX-fp8 along K (blocks of 32, E8M0 scale, e4m3 RNE;
                oracle/mx.py's rule), out-projection and convs bf16 -- the SSE_DTYPE_FP8 path
+  oproj        bf16 (default) | mx8: the out-projection's operands MX-fp8 too (option f8_oproj = 1, round 6)
   stream bf16  residual stream and the qkv / context outputs rounded to bf16 where the path stores them
   attn         bf16     Q, K, V, P bf16 (the shipped attention)
                qk8      Q.K^T on MX-fp8 operands (blocks of 32 along the head dim), P.V bf16
@@ -120,7 +121,7 @@ GELU_FP8 = {   # tools/fit_gelu.py fits: (clamp, coefficients highest degree fir
 }
 
 
-def hidden_states(spec, p, mel, gemm="mx8", attn="bf16", stream="bf16", gelu_fc1="exact"):
+def hidden_states(spec, p, mel, gemm="mx8", attn="bf16", stream="bf16", gelu_fc1="exact", oproj="bf16"):
     eps, nh, hd = spec.ln_eps, spec.heads, spec.head_dim
     rnd = _bf if stream == "bf16" else (lambda t: t)
     cf = "bf16" if gemm != "fp32" else "fp32"
@@ -139,7 +140,7 @@ def hidden_states(spec, p, mel, gemm="mx8", attn="bf16", stream="bf16", gelu_fc1
         v = rnd(_lin(h, p[f"{s_}.v_proj.weight"], gemm) + p[f"{s_}.v_proj.bias"])
         qh, kh, vh = (t.reshape(T, nh, hd).transpose(0, 1) for t in (q, k, v))
         ctx = rnd(_attn(qh, kh, vh, attn).transpose(0, 1).reshape(T, nh * hd))
-        x = rnd(x + _lin(ctx, p[f"{s_}.out_proj.weight"], cf) + p[f"{s_}.out_proj.bias"])
+        x = rnd(x + _lin(ctx, p[f"{s_}.out_proj.weight"], oproj if gemm == "mx8" else cf) + p[f"{s_}.out_proj.bias"])
         h = _ln(x, p[f"{a}.final_layer_norm.weight"], p[f"{a}.final_layer_norm.bias"], eps)
         h = _lin(h, p[f"{a}.fc1.weight"], gemm) + p[f"{a}.fc1.bias"]
         h = _gelu(h) if gelu_fc1 == "exact" else _gelu_poly(h, *GELU_FP8[gelu_fc1])
@@ -154,6 +155,7 @@ def main() -> None:
     ap.add_argument("--attn", default="bf16,qk8,qk8pv8t,qk8pv8")
     ap.add_argument("--gemm", default="mx8")
     ap.add_argument("--gelu", default="exact", help="fc1 GELU: exact | deg5 | deg3 | deg2 (the fp8-out polynomials)")
+    ap.add_argument("--oproj", default="bf16", help="out-projection operands with --gemm mx8: bf16 | mx8")
     ap.add_argument("--threads", type=int, default=os.cpu_count())
     ap.add_argument("--out", default="")
     a = ap.parse_args()
@@ -168,12 +170,13 @@ def main() -> None:
     res = {}
     with torch.no_grad():
         for attn in a.attn.split(","):
-            hs = hidden_states(spec, p, mel, a.gemm, attn, gelu_fc1=a.gelu)
+            hs = hidden_states(spec, p, mel, a.gemm, attn, gelu_fc1=a.gelu, oproj=a.oproj)
             got = np.stack([hs[i].mean(0).numpy() for i in idx])
             rel = np.linalg.norm(got - ref, axis=-1) / np.linalg.norm(ref, axis=-1)
             cos = (got * ref).sum(-1) / (np.linalg.norm(got, axis=-1) * np.linalg.norm(ref, axis=-1))
-            res[f"{a.gemm}/{attn}/{a.gelu}"] = {"rel_l2_max": float(rel.max()), "cos_min": float(cos.min())}
-            print(a.gemm, attn, a.gelu, json.dumps(res[f"{a.gemm}/{attn}/{a.gelu}"]), flush=True)
+            key = f"{a.gemm}/{attn}/{a.gelu}/oproj-{a.oproj}"
+            res[key] = {"rel_l2_max": float(rel.max()), "cos_min": float(cos.min())}
+            print(key, json.dumps(res[key]), flush=True)
     if a.out:
         with open(a.out, "w") as f:
             json.dump(res, f, indent=1)

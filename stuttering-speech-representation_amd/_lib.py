@@ -34,7 +34,7 @@ EXPORTED = ("sse_weight_floats", "sse_model_create", "sse_model_destroy", "sse_o
             "sse_resample", "sse_augment", "sse_mx_scale_bytes", "sse_mx_scale_offset", "sse_mx_quantize",
             "sse_mx_quantize_host", "sse_gemm_mx", "sse_pitch_shift_workspace_bytes", "sse_pitch_shift",
             "sse_set_option", "sse_get_option", "sse_embed_ragged", "sse_gemm_lnfold", "sse_check_range",
-            "sse_attention", "sse_gemm_ex", "sse_attention_f8", "sse_layernorm_mx")
+            "sse_attention", "sse_gemm_ex", "sse_attention_f8", "sse_layernorm_mx", "sse_attention_f8_mx")
 
 
 class SSEError(RuntimeError):
@@ -168,6 +168,9 @@ def lib() -> ctypes.CDLL:
     if hasattr(L, "sse_attention_f8"):
         L.sse_attention_f8.argtypes = [vp, vp, vp, vp, vp, i32, i32, i32, i32, vp]
         L.sse_attention_f8.restype = i32
+    if hasattr(L, "sse_attention_f8_mx"):
+        L.sse_attention_f8_mx.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp]
+        L.sse_attention_f8_mx.restype = i32
     L.sse_gemm_lnfold.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, ctypes.c_float, vp, vp]
     L.sse_gemm_lnfold.restype = i32
     L.sse_whisper_embed.argtypes = [vp, vp, i32, i32, vp, i32, vp, vp, i32, vp, vp, sz, vp]

@@ -91,6 +91,10 @@ struct AttnArgs {
   const unsigned char* qks;
   const void* v16;
   const unsigned* vamax;
+  // fp8 attention, optional MX-fp8 output instead of bf16 `out` (round 6: the out-projection's A operand):
+  // e4m3 [B*T][H] and E8M0 scales in the MX GEMM's A layout for K = H (mx_a_scale_off)
+  unsigned char* out_q;
+  unsigned char* out_s;
 };
 int launch_attention_f8(const AttnArgs& a, int B, hipStream_t s);
 template <typename T>

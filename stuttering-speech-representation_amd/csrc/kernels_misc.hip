@@ -2480,6 +2480,37 @@ __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attention_f8_kernel(Attn
     const int qi = q0 + 32 * qb;
     if (qi < T) {
       const float inv = 1.0f / l;
+      if (a.out_q) {
+        // MX-fp8 output (the out-projection's A operand): block 2 h + db of the row = dims 32 db .. 32 db + 31 of
+        // this head, 16 in this lane (8 c + 4 hw + e, c = 0..3) and 16 in its partner (lane ^ 32).  amax over both
+        // halves, E8M0 exponent, e4m3 = RNE(x 2^-E) four values per dword; the partners trade dwords so that lane
+        // hw stores dims 16 hw .. 16 hw + 15 as one 16-B store (hw = 0: its dwords 0, 1 with the partner's after
+        // each; hw = 1: the partner's dwords 2, 3 before its own); lane hw = 0 writes the scale byte
+        unsigned char* orow = a.out_q + (row0 + qi) * H + h * AT_HD;
+        #pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          float am = 0.f;
+          #pragma unroll
+          for (int e = 0; e < 16; ++e) am = __builtin_elementwise_maximum(am, fabsf(o[qb][db][e] * inv));
+          const auto t32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(am), __float_as_uint(am), false, false);
+          am = __builtin_elementwise_maximum(__uint_as_float(t32[0]), __uint_as_float(t32[1]));
+          const int e8 = mx_scale_exp(am);
+          const float qs = inv * mx_inv_scale(e8);
+          int w[4];
+          #pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int x = __builtin_amdgcn_cvt_pk_fp8_f32(o[qb][db][4 * c] * qs, o[qb][db][4 * c + 1] * qs, 0, false);
+            w[c] = __builtin_amdgcn_cvt_pk_fp8_f32(o[qb][db][4 * c + 2] * qs, o[qb][db][4 * c + 3] * qs, x, true);
+          }
+          const auto r0 = __builtin_amdgcn_permlane32_swap((unsigned)w[0], (unsigned)w[2], false, false);
+          const auto r1 = __builtin_amdgcn_permlane32_swap((unsigned)w[1], (unsigned)w[3], false, false);
+          const uint4 v = hw == 0 ? make_uint4((unsigned)w[0], r0[1], (unsigned)w[1], r1[1])
+                                  : make_uint4(r0[0], (unsigned)w[2], r1[0], (unsigned)w[3]);
+          *(uint4*)(orow + 32 * db + 16 * hw) = v;
+          if (hw == 0) a.out_s[mx_a_scale_off(row0 + qi, (h * AT_HD + 32 * db) >> 5, H >> 7)] = (unsigned char)e8;
+        }
+        continue;
+      }
       bf16* orow = (bf16*)a.out + (row0 + qi) * H + h * AT_HD;
       #pragma unroll
       for (int db = 0; db < 2; ++db)
@@ -2495,6 +2526,7 @@ __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attention_f8_kernel(Attn
 
 int launch_attention_f8(const AttnArgs& a, int B, hipStream_t s) {
   if (a.H != a.nh * AT_HD || !a.q_log2 || a.tlen || !a.qk8 || !a.qks || !a.v16 || !a.vamax || a.T <= 0) return -3;
+  if (a.out_q ? (!a.out_s || a.H % 128) : !a.out) return -3;   // MX output: K-tiles of 128 columns
   if ((long long)a.T * 2 * a.H >= (1LL << 31)) return -3;   // 32-bit buffer offsets
   // (one query block per wave, 168 VGPRs at three blocks per CU, measured 1.4 % slower per step: not kept)
   hipLaunchKernelGGL(attention_f8_kernel<2>, dim3((a.T + 255) / 256, a.nh, B), dim3(256), 0, s, a);

@@ -35,9 +35,10 @@ static int g_opt[OPT_COUNT] = {0};
 static const char* const g_opt_name[OPT_COUNT] = {"gemm_cfg", "gemm_nonpersist", "gelu_exact", "conv0_valu",
                                                    "posconv_gemm", "no_lnfold", "gemm_mx_staged", "no_split",
                                                    "logmel_v1", "ln_x3_v1", "attn_x3_f32", "ln_rows_v1", "posconv_2cl",
-                                                   "attn_short", "attn_long", "fp8_attn_bf16", "split_cumask"};
+                                                   "attn_short", "attn_long", "fp8_attn_bf16", "split_cumask",
+                                                   "f8_oproj"};
 // the largest value each switch takes (0 .. max; anything else is SSE_ERR_INVALID, not a silent default)
-static const int g_opt_max[OPT_COUNT] = {3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 1, 2};
+static const int g_opt_max[OPT_COUNT] = {3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 1, 2, 1};
 int sse_opt(int id) { return __atomic_load_n(&g_opt[id], __ATOMIC_RELAXED); }
 
 // CU-masked streams (split_forward, OPT_SPLIT_CUMASK) and their CU counts; registered once, never removed
@@ -260,6 +261,7 @@ struct LayerW {
   size_t qkv_w, qkv_b, o_w, o_b, ln1_w, ln1_b, f1_w, f1_b, f2_w, f2_b, ln2_w, ln2_b;
   size_t g_const, g_w, g_b;   // WavLM gate
   size_t qkv_q, qkv_s, f1_q, f1_s, f2_q, f2_s;   // SSE_DTYPE_FP8: MX-fp8 copies (e4m3 + scales)
+  size_t o_q, o_s;                                // SSE_DTYPE_FP8: the out-projection's MX-fp8 copy (round 6)
   // folded LayerNorm (bf16 post-LN, common.h GemmArgs.apart): QKV folded with the previous layer's
   // final LayerNorm (layers >= 1), FFN1 with this layer's attention LayerNorm: weight W diag(ln_w)
   // (bf16), its column sums acol and bias b + W ln_b
@@ -546,6 +548,7 @@ int build_whisper(sse_model* m, Blob& bl, Arena& ar) {
       L.qkv_q = ar.put_mx(qkv, 3 * D, D, &L.qkv_s);
       L.f1_q = ar.put_mx(std::vector<float>(f1w, f1w + (size_t)F * D), F, D, &L.f1_s);
       L.f2_q = ar.put_mx(std::vector<float>(f2w, f2w + (size_t)D * F), D, F, &L.f2_s);
+      L.o_q = ar.put_mx(std::vector<float>(ow, ow + (size_t)D * D), D, D, &L.o_s);
     }
     L.o_w = X3 ? ar.put_x3(std::vector<float>(ow, ow + (size_t)D * D), D, 1, D)
                : ar.put_elem(std::vector<float>(ow, ow + (size_t)D * D), BF);
@@ -1387,6 +1390,13 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
   // fp8 attention (default on the MX path): Q | K e4m3 [M][2D] | V bf16 [M][D] | Q | K scales [M][2D / 32] in
   // the QKV space ([M][3D] bf16 = 6D bytes per row)
   const bool f8attn = mx && !sse_opt(OPT_FP8_ATTN_BF16);
+  // MX-fp8 out-projection (round 6, opt-in f8_oproj = 1): the attention writes its output as MX-fp8 (e4m3 +
+  // A-layout scales) into ctx's space and the out-projection runs on the MX GEMM with the residual.  Not the
+  // default: one more e4m3 rounding per layer takes Whisper-large-v2 (B = 128, 32 layers) from 0.066 to 0.083
+  // rel-L2 against the reference fixture, over the fp8 bar of 0.08 (tests/test_gpu_whisper.py)
+  const bool f8oproj = f8attn && D % 128 == 0 && sse_opt(OPT_F8_OPROJ);
+  unsigned char* cq = (unsigned char*)ctx;
+  unsigned char* cq_s = cq + (size_t)M * D;
   unsigned char* qk8 = (unsigned char*)qkv;
   bf16* v16 = (bf16*)(qk8 + (size_t)M * 2 * D);
   unsigned char* qks = qk8 + (size_t)M * 4 * D;
@@ -1454,17 +1464,23 @@ int whisper_forward(sse_model* m, const float* wave, int B, int L, const Sink& s
     a.scale = a.q_log2 ? 0.6931471805599453f : 1.0f;
     if (f8attn) {
       a.qkv = nullptr; a.qk8 = qk8; a.qks = qks; a.v16 = v16; a.vamax = vam;
-      RC(prof(m, s, "attn_f8", 4.0 * B * (double)Tq * Tq * D, (double)B * Tq * (2.0 * D * (1 + 1.0 / 32) + 4.0 * D),
+      if (f8oproj) { a.out = nullptr; a.out_q = cq; a.out_s = cq_s; }
+      RC(prof(m, s, "attn_f8", 4.0 * B * (double)Tq * Tq * D,
+              (double)B * Tq * (2.0 * D * (1 + 1.0 / 32) + 2.0 * D + (f8oproj ? D * (1 + 1.0 / 32) : 2.0 * D)),
               [&] { return launch_attention_f8(a, B, s); }));
     } else {
       RC(prof(m, s, "attn", 4.0 * B * (double)Tq * Tq * D, (double)B * Tq * 4.0 * D * sizeof(T),
               [&] { return launch_attention<T>(a, B, s); }));
     }
-    g = GemmArgs{};
-    g.A = ctx; g.B = m->ptr(Lw.o_w); g.M = M; g.N = D; g.K = D; g.rows_per_seg = M; g.lda = D;
-    g.bias = m->ptr<float>(Lw.o_b); set_resid(g); g.ldc = D; g.zero = zero;
-    if (f1fold) g.opart = p1;
-    RC(prof(m, s, "gemm:oproj", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    if (f8oproj) {
+      RC(mx_gemm("gemm_mx:oproj", cq, cq_s, Lw.o_q, Lw.o_s, Lw.o_b, D, D, true, nullptr, nullptr, ACT_NONE));
+    } else {
+      g = GemmArgs{};
+      g.A = ctx; g.B = m->ptr(Lw.o_w); g.M = M; g.N = D; g.K = D; g.rows_per_seg = M; g.lda = D;
+      g.bias = m->ptr<float>(Lw.o_b); set_resid(g); g.ldc = D; g.zero = zero;
+      if (f1fold) g.opart = p1;
+      RC(prof(m, s, "gemm:oproj", gflops(g), gbytes<T>(g), [&] { return launch_gemm<T>(g, AMODE_SEG, 1, s); }));
+    }
     if (mx) {
       RC(launch_layernorm_mx<R>(x, m->ptr<float>(Lw.ln2_w), m->ptr<float>(Lw.ln2_b), M, D, eps, xq, xq_s, s));
       RC(mx_gemm("gemm_mx:ffn1", xq, xq_s, Lw.f1_q, Lw.f1_s, Lw.f1_b, F, D, false, fq, fq_s, gelu_rounded_act<T>()));
@@ -2122,6 +2138,18 @@ int sse_attention_f8(const uint8_t* d_qk, const uint8_t* d_qk_scale, const void*
   AttnArgs a{};
   a.out = d_out; a.T = T; a.H = H; a.nh = nh; a.ldq = 2 * H; a.scale = 0.6931471805599453f; a.q_log2 = 1;
   a.qk8 = d_qk; a.qks = d_qk_scale; a.v16 = d_v; a.vamax = d_vamax;
+  const int rc = launch_attention_f8(a, B, (hipStream_t)stream);
+  return rc == -3 ? SSE_ERR_INVALID : (rc ? SSE_ERR_HIP : SSE_OK);
+}
+
+int sse_attention_f8_mx(const uint8_t* d_qk, const uint8_t* d_qk_scale, const void* d_v, const uint32_t* d_vamax,
+                        uint8_t* d_out_q, uint8_t* d_out_scale, int B, int T, int H, int nh, void* stream) {
+  if (!d_qk || !d_qk_scale || !d_v || !d_vamax || !d_out_q || !d_out_scale || B <= 0 || T <= 0 || nh <= 0 ||
+      H != nh * 64 || H % 128)
+    return SSE_ERR_INVALID;
+  AttnArgs a{};
+  a.T = T; a.H = H; a.nh = nh; a.ldq = 2 * H; a.scale = 0.6931471805599453f; a.q_log2 = 1;
+  a.qk8 = d_qk; a.qks = d_qk_scale; a.v16 = d_v; a.vamax = d_vamax; a.out_q = d_out_q; a.out_s = d_out_scale;
   const int rc = launch_attention_f8(a, B, (hipStream_t)stream);
   return rc == -3 ? SSE_ERR_INVALID : (rc ? SSE_ERR_HIP : SSE_OK);
 }

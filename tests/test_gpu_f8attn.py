@@ -182,6 +182,51 @@ def test_attention_f8_large_v2_shape():
     assert _rel(out, ref) <= 1.5 * _rel(_reference(deq, v16, B, T, H, nh, p8=True), ref) + 2e-3
 
 
+@pytest.mark.parametrize("T,nh,kind", [(1500, 20, "random"), (161, 4, "vscale"), (1, 4, "random"), (300, 2, "spike")])
+def test_attention_f8_mx_output(T, nh, kind):
+    """The MX-fp8 output form (sse_attention_f8_mx; with option f8_oproj = 1 the fp8 Whisper path's attention
+    writes it as the MX out-projection's A operand) against the bf16 output of the same kernel on the same operands: per 32-column
+    block the E8M0 exponent is that of the block's amax (oracle/mx.py scale_exp: the kernel takes it over fp32
+    values, the check over their bf16 roundings, so a block may sit one exponent apart at a binade edge -- at most
+    1 % of blocks), and each code is within e4m3's RNE step of the bf16 value (half an ulp: 2^-4 relative, 2^-10
+    of the scale in the subnormal range) plus the bf16 rounding.  Rows past B*T untouched."""
+    from oracle import mx
+    from ssr_amd import _lib
+    B = 2
+    H = 64 * nh
+    if H % 128:
+        pytest.skip("MX output needs H % 128 == 0")
+    q, k, v = _operands(B, T, H, kind, seed=T * 3 + nh)
+    qk8, qks, _ = _quantize_qk(q, k)
+    v16 = v.to(torch.bfloat16)
+    vam = _vamax(v16, B, T, H)
+    ref = _run(qk8, qks, v16, vam, B, T, H, nh).float()
+    R = B * T
+    oq = torch.full((R + 64, H), 0xA5, dtype=torch.uint8, device="cuda")
+    osc = torch.full((mx.scale_bytes(R, H),), 0xEE, dtype=torch.uint8, device="cuda")
+    rc = _lib.lib().sse_attention_f8_mx(qk8.data_ptr(), qks.data_ptr(), v16.data_ptr(), vam.data_ptr(), oq.data_ptr(),
+                                        osc.data_ptr(), B, T, H, nh, _stream())
+    _lib.check(rc, "sse_attention_f8_mx")
+    torch.cuda.synchronize()
+    assert bool((oq[R:] == 0xA5).all()), "store past the output"
+    codes = oq[:R].cpu().numpy()
+    eb = mx.exps_from_scales(osc.cpu().numpy(), R, H, 0)
+    r = ref.cpu().numpy().astype(np.float32)
+    want = mx.scale_exp(np.abs(r.reshape(R, H // 32, 32)).max(axis=2))
+    d = eb.astype(np.int32) - want.astype(np.int32)
+    assert np.abs(d).max() <= 1 and (d != 0).mean() <= 0.01, (np.abs(d).max(), (d != 0).mean())
+    deq = mx.dequantize(codes, eb)
+    step = np.ldexp(1.0, eb.astype(np.int64) - 127 - 10)[:, :, None]
+    bound = (np.abs(r) * (2.0 ** -4 + 2.0 ** -8)).reshape(R, H // 32, 32) + step
+    over = (np.abs(deq - r).reshape(R, H // 32, 32) - bound).max()
+    print(f"f8 attention MX output T={T} nh={nh} {kind}: exponent mismatches {(d != 0).mean():.2e}, "
+          f"rel-L2 vs bf16 {_rel(torch.from_numpy(deq).float(), torch.from_numpy(r)):.3e}")
+    assert over <= 0.0, over
+    with pytest.raises(Exception):   # H % 128 != 0 has no MX output form
+        _lib.check(_lib.lib().sse_attention_f8_mx(qk8.data_ptr(), qks.data_ptr(), v16.data_ptr(), vam.data_ptr(),
+                                                  oq.data_ptr(), osc.data_ptr(), B, T, 192, 3, _stream()), "x")
+
+
 def _gemm_mx(qa, sa, qb, sb, bias, M, N, K, **kw):
     from ssr_amd import _lib
     d = _lib.sse_gemm_desc()
