@@ -330,6 +330,8 @@ const char* sse_version(void);
  * reads the environment).  Process-wide; 0 is the production choice for every name:
  *   "gemm_cfg"          1 = no 256x256 tile, 2 = 256x128 3-stage ring, 3 = 2-stage 256x256 kernel
  *   "gemm_nonpersist"   1 = non-persistent 8-phase bf16 GEMM for every shape
+ *   "gemm_4phase"       1 = the persistent bf16 GEMM with four 16-MFMA phases per K-tile (rounds 1-5; the default
+ *                       since round 6 is two 32-MFMA phases, bit-identical)
  *   "gelu_exact"        1 = erf-GELU in the bf16 path's epilogues
  *   "conv0_valu"        1 = VALU conv0 + GroupNorm kernel instead of the matrix-core one
  *   "posconv_gemm"      1 = grouped GEMM for the bf16 positional conv

@@ -1166,7 +1166,13 @@ SSE_DEV void g8p_epilogue(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int m0, i
 // costs no epilogue instruction (runtime selects measured +5-6 % on conv1 / ffn1 when removed).
 // DBG (timing probes only): see g8p_epilogue; 2 = no epilogue at all (accumulators kept live); 4 = no epilogue and
 // no MFMA (the LDS fragment reads kept live); 5 = no epilogue and no main-loop LDS-DMA.
-template <int ACT, bool CT3 = false, bool F16 = false, int EP = 1, int DBG = 0, int FNT = 3>
+// PH2 (round 6, the default; option gemm_4phase = 1 keeps four): two phases per K-tile instead of four -- Q0 reads A0, B0, B1 and runs A0 B0 and
+// A0 B1 (32 MFMAs), Q1 reads A1 and runs A1 B1, A1 B0 -- so half the barriers per K-tile and 32-MFMA sections.  Issue
+// schedule (2-phase index j = 2t + h): Q0(t) -> A1(t+1), Q1(t) -> A0, B0, B1(t+2) (their slots' previous occupants
+// were read in Q0(t)); the prologue is j = -3 .. -1 (all of tile 0, then A0, B0, B1 of tile 1).  Every half is
+// issued two phases before its first read and the wait at the end of L(j) leaves ops(j) + ops(j - 1) in flight
+// (8 in steady state, as the 4-phase schedule).
+template <int ACT, bool CT3 = false, bool F16 = false, int EP = 1, int DBG = 0, int FNT = 3, bool PH2 = false>
 __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
   __shared__ __attribute__((aligned(16))) char smem[G8P_SMEM];   // operands | 2 epilogue slots: the ONLY shared object
   const int lane = threadIdx.x & 63;
@@ -1217,11 +1223,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
         b_voff[h][s] = (unsigned)((long long)row * K * 2 + ch * 16);
       }
   };
-  auto issue = [&](int k) {
-    if (k < -6) return;
-    int tl, half;
-    g8_target(k, tl, half);
-    if (tl >= nk) return;
+  auto issue_half = [&](int tl, int half) {
     char* dst = smem + (tl & 1) * G8_BUF + half * G8_HALF;
     const unsigned soff = (unsigned)tl * 128u;
     if (half < 2) {
@@ -1231,6 +1233,38 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, LPTR(dst + wave * 1024), 16, b_voff[half - 2][0], soff, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, LPTR(dst + (wave + 8) * 1024), 16, b_voff[half - 2][1], soff, 0,
                                                0);
+    }
+  };
+  auto issue = [&](int k) {
+    if (k < -6) return;
+    int tl, half;
+    g8_target(k, tl, half);
+    if (tl >= nk) return;
+    issue_half(tl, half);
+  };
+  // PH2 schedule (see the template comment): ops per wave issued at 2-phase j, the issue itself, the counted wait
+  auto ops2 = [&](int j) -> int {
+    if (j < -3) return 0;
+    const int t = j >> 1;
+    return (j & 1) == 0 ? (t + 1 < nk ? 2 : 0) : (t + 2 < nk ? 6 : 0);
+  };
+  auto issue2 = [&](int j) {
+    if (j < -3) return;
+    const int t = j >> 1;
+    if ((j & 1) == 0) {
+      if (t + 1 < nk) issue_half(t + 1, 1);
+    } else if (t + 2 < nk) {
+      issue_half(t + 2, 0);
+      issue_half(t + 2, 2);
+      issue_half(t + 2, 3);
+    }
+  };
+  auto count2 = [&](int j) { return ops2(j) + ops2(j - 1); };
+  auto prologue = [&]() {
+    if constexpr (PH2) {
+      for (int j = -3; j < 0; ++j) issue2(j);
+    } else {
+      for (int k = -6; k < 0; ++k) issue(k);
     }
   };
   // epilogue-parameter DMA of tile tl into slot: 1 KiB pieces -- the row partials (2 FNT pieces), the bias,
@@ -1337,7 +1371,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
   int slot = 0;
   ep_issue(tile, 0);
   setup(tile);
-  for (int k = -6; k < 0; ++k) issue(k);
+  prologue();
   int S = 0;   // store instructions issued after the current tile's prologue
   while (true) {
     const int m0 = (tile / n_tiles_n) * 256, n0 = (tile % n_tiles_n) * 256;
@@ -1350,7 +1384,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
           #pragma unroll
           for (int j = 0; j < 2; ++j) acc[a][c][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     // the epilogue-parameter DMA precedes the prologue: retired by the same counted waits
-    g8_vmcnt_dyn<false>(g8_count<false>(-1, nk) + S);
+    g8_vmcnt_dyn<false>((PH2 ? count2(-1) : g8_count<false>(-1, nk)) + S);
     g8_barrier();
     if (wm == 1) g8_barrier();   // group 1 runs one barrier behind
 
@@ -1391,10 +1425,49 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
       mma(acc[1][0], b0f);
       g8_barrier();
     };
-    run_tile(0, std::integral_constant<bool, false>{}, std::integral_constant<bool, true>{});
+    // PH2: the same K-tile in two phases of 32 MFMAs
+    auto run_tile2 = [&](int t, auto steady, auto first) {
+      constexpr bool ST = decltype(steady)::value;
+      constexpr bool FI = decltype(first)::value;
+      const char* buf = smem + (t & 1) * G8_BUF;
+      const int j = 2 * t;
+      auto issue_wait = [&](int jj) {
+        if constexpr (DBG != 5) issue2(jj);
+        if constexpr (FI) {
+          g8_vmcnt_dyn<false>(count2(jj) + S);
+        } else if constexpr (ST) {
+          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else {
+          g8_vmcnt_dyn<false>(count2(jj));
+        }
+      };
+      read_a(buf);
+      read_b(buf + 2 * G8_HALF, b0f);
+      read_b(buf + 3 * G8_HALF, b1f);
+      issue_wait(j);
+      g8_barrier();
+      mma(acc[0][0], b0f);
+      mma(acc[0][1], b1f);
+      g8_barrier();
+      read_a(buf + G8_HALF);
+      issue_wait(j + 1);
+      g8_barrier();
+      mma(acc[1][1], b1f);
+      mma(acc[1][0], b0f);
+      g8_barrier();
+    };
+    using F_ = std::integral_constant<bool, false>;
+    using T_ = std::integral_constant<bool, true>;
     int t = 1;
-    for (; t + 2 < nk; ++t) run_tile(t, std::integral_constant<bool, true>{}, std::integral_constant<bool, false>{});
-    for (; t < nk; ++t) run_tile(t, std::integral_constant<bool, false>{}, std::integral_constant<bool, false>{});
+    if constexpr (PH2) {
+      run_tile2(0, F_{}, T_{});
+      for (; t + 2 < nk; ++t) run_tile2(t, T_{}, F_{});
+      for (; t < nk; ++t) run_tile2(t, F_{}, F_{});
+    } else {
+      run_tile(0, F_{}, T_{});
+      for (; t + 2 < nk; ++t) run_tile(t, T_{}, F_{});
+      for (; t < nk; ++t) run_tile(t, F_{}, F_{});
+    }
     if (wm == 0) g8_barrier();   // balance group 1's extra barrier: every wave's LDS reads are done
 
     ++round;
@@ -1402,7 +1475,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
     if (next >= 0) {
       ep_issue(next, slot ^ 1);
       setup(next);
-      for (int k = -6; k < 0; ++k) issue(k);
+      prologue();
     }
     if constexpr (DBG == 2 || DBG == 4 || DBG == 5) {   // (DBG 6, 7: the library epilogue)
       #pragma unroll
@@ -2081,27 +2154,32 @@ int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
     const int ncu = sse_stream_cus(s, cus[dev]);   // a CU-masked stream's own CUs
     const int G = n_tiles < ncu ? n_tiles : ncu;
     const int ep = (a.bias ? 1 : 0) | (a.apart ? 2 : 0);
-    auto go = [&](auto act, auto ct3, auto f16) {
+    const bool ph2 = sse_opt(OPT_GEMM_4PHASE) == 0;   // two phases per K-tile (round 6 default)
+    auto go2 = [&](auto act, auto ct3, auto f16, auto p2) {
       constexpr int AC = decltype(act)::value;
-      constexpr bool C3 = decltype(ct3)::value, F = decltype(f16)::value;
+      constexpr bool C3 = decltype(ct3)::value, F = decltype(f16)::value, P2 = decltype(p2)::value;
       switch (ep) {
-        case 0: hipLaunchKernelGGL((gemm8p_kernel<AC, C3, F, 0>), dim3(G), dim3(512), 0, s, a, n_tiles); break;
-        case 1: hipLaunchKernelGGL((gemm8p_kernel<AC, C3, F, 1>), dim3(G), dim3(512), 0, s, a, n_tiles); break;
-        case 2: hipLaunchKernelGGL((gemm8p_kernel<AC, C3, F, 2>), dim3(G), dim3(512), 0, s, a, n_tiles); break;
+        case 0: hipLaunchKernelGGL((gemm8p_kernel<AC, C3, F, 0, 0, 3, P2>), dim3(G), dim3(512), 0, s, a, n_tiles); break;
+        case 1: hipLaunchKernelGGL((gemm8p_kernel<AC, C3, F, 1, 0, 3, P2>), dim3(G), dim3(512), 0, s, a, n_tiles); break;
+        case 2: hipLaunchKernelGGL((gemm8p_kernel<AC, C3, F, 2, 0, 3, P2>), dim3(G), dim3(512), 0, s, a, n_tiles); break;
         default:
           if constexpr (!F && !C3) {   // bf16 folded LayerNorm: the input's column-tile count
             if (a.apart_nt == 4) {
-              hipLaunchKernelGGL((gemm8p_kernel<AC, C3, F, 3, 0, 4>), dim3(G), dim3(512), 0, s, a, n_tiles);
+              hipLaunchKernelGGL((gemm8p_kernel<AC, C3, F, 3, 0, 4, P2>), dim3(G), dim3(512), 0, s, a, n_tiles);
               break;
             }
             if (a.apart_nt == 5) {
-              hipLaunchKernelGGL((gemm8p_kernel<AC, C3, F, 3, 0, 5>), dim3(G), dim3(512), 0, s, a, n_tiles);
+              hipLaunchKernelGGL((gemm8p_kernel<AC, C3, F, 3, 0, 5, P2>), dim3(G), dim3(512), 0, s, a, n_tiles);
               break;
             }
           }
-          hipLaunchKernelGGL((gemm8p_kernel<AC, C3, F, 3>), dim3(G), dim3(512), 0, s, a, n_tiles);
+          hipLaunchKernelGGL((gemm8p_kernel<AC, C3, F, 3, 0, 3, P2>), dim3(G), dim3(512), 0, s, a, n_tiles);
           break;
       }
+    };
+    auto go = [&](auto act, auto ct3, auto f16) {
+      if (ph2) go2(act, ct3, f16, std::true_type{});
+      else go2(act, ct3, f16, std::false_type{});
     };
     using F_ = std::false_type;
     using T_ = std::true_type;

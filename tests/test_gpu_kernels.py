@@ -156,9 +156,10 @@ def test_fast_gelu_pointwise_bf16_out():
 def test_gemm_persistent_agrees(M, N, K, epi):
     """The persistent 8-phase kernel (default for GEMMs without a residual: blocks walk several
     tiles, the next tile's prologue is issued before this tile's stores, which stay in flight)
-    against the non-persistent kernel (gemm_nonpersist=1) and the 2-stage kernel
-    (gemm_cfg=3): bit-identical.  Tile counts above the CU count, ragged M, K-tile counts
-    1, 2, 3, 4, 12 and every output combination."""
+    against its round-1..5 four-phase schedule (gemm_4phase=1; the default runs two 32-MFMA phases per
+    K-tile), the non-persistent kernel (gemm_nonpersist=1) and the 2-stage kernel (gemm_cfg=3):
+    bit-identical.  Tile counts above the CU count, ragged M, K-tile counts 1, 2, 3, 4, 12 and every
+    output combination."""
     from ssr_amd.model import gemm
     from ssr_amd import _lib
     import ctypes
@@ -180,7 +181,7 @@ def test_gemm_persistent_agrees(M, N, K, epi):
         return cf, ct
 
     outs = []
-    for name, v in (("gemm_cfg", 0), ("gemm_nonpersist", 1), ("gemm_cfg", 3)):
+    for name, v in (("gemm_cfg", 0), ("gemm_4phase", 1), ("gemm_nonpersist", 1), ("gemm_cfg", 3)):
         with _lib.option(name, v):
             outs.append(run())
             torch.cuda.synchronize()

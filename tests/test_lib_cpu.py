@@ -83,7 +83,7 @@ def test_options_are_explicit_only():
     from ssr_amd import _lib
     L = _lib.lib()
     for name in (b"gemm_cfg", b"gemm_nonpersist", b"gelu_exact", b"conv0_valu", b"posconv_gemm", b"no_lnfold",
-                 b"gemm_mx_staged", b"fp8_attn_bf16", b"f8_oproj"):
+                 b"gemm_mx_staged", b"fp8_attn_bf16", b"f8_oproj", b"gemm_4phase"):
         assert L.sse_get_option(name) == 0
         with _lib.option(name.decode(), 1):
             assert L.sse_get_option(name) == 1
