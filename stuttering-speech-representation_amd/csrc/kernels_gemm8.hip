@@ -111,6 +111,31 @@ SSE_DEV void g8_vmcnt_dyn(int n) {
 template <bool MX>
 SSE_DEV void g8_wait(int k, int nk) { g8_vmcnt_dyn<MX>(g8_count<MX>(k, nk)); }
 
+// Two-phase schedule (round 6 default; gemm8p_kernel's template comment): 2-phase index j = 2t + h, Q0(t) issues
+// A1(t+1), Q1(t) issues A0, B0, B1(t+2); the prologue is j = -3 .. -1.  ih(tile, half) issues one half-tile (2 ops).
+// (MX: Q1's A0 issue carries the K-tile's scale DMA, 7 ops)
+template <bool MX = false>
+SSE_DEV int g8_ops2(int j, int nk) {
+  if (j < -3) return 0;
+  const int t = j >> 1;
+  return (j & 1) == 0 ? (t + 1 < nk ? 2 : 0) : (t + 2 < nk ? (MX ? 7 : 6) : 0);
+}
+// ops the wait at the end of L(j) leaves in flight: what was issued at j and j - 1
+template <bool MX = false>
+SSE_DEV int g8_count2(int j, int nk) { return g8_ops2<MX>(j, nk) + g8_ops2<MX>(j - 1, nk); }
+template <typename IH>
+SSE_DEV void g8_issue2(int j, int nk, IH&& ih) {
+  if (j < -3) return;
+  const int t = j >> 1;
+  if ((j & 1) == 0) {
+    if (t + 1 < nk) ih(t + 1, 1);
+  } else if (t + 2 < nk) {
+    ih(t + 2, 0);
+    ih(t + 2, 2);
+    ih(t + 2, 3);
+  }
+}
+
 // epilogue memory ops; NT = non-temporal (streaming: C tiles and residual rows are touched once
 // and should not evict the A / B operand lines from L2)
 template <bool NT, typename V> SSE_DEV void g8_st(V* p, V v) {
@@ -169,7 +194,9 @@ SSE_DEV void g8_epilogue_direct(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], int
 // it and the fp8-out epilogue spilled 178 VGPRs); 3: qkv (bias, bf16 out); 4: the fp8 attention's Q / K (bias,
 // MX-fp8 out, row-major scales); 5: its V (bias, bf16 out, per-clip column amax).  Runtime selects in the
 // persistent bf16 kernel's epilogue measured +5-6 %.
-template <int DBG, bool TR, bool NT, bool MX = false, int MXE = 0>
+// PH2 (MX only; round 6 default, option gemm_4phase = 1 keeps four phases): two 32-MFMA phases per K-tile, the
+// schedule of gemm8p_kernel's template comment, the scale DMA issued with A0 in Q1 (7 ops; steady vmcnt(9) as before)
+template <int DBG, bool TR, bool NT, bool MX = false, int MXE = 0, bool PH2 = false>
 __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[MX ? G8_SMEM_MX : G8_SMEM];   // the ONLY shared object
   const int lane = threadIdx.x & 63;
@@ -231,11 +258,7 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
         b_voff[h][s] = (unsigned)((long long)row * K * ES + ch * 16);
       }
   }
-  auto issue = [&](int k) {
-    if (k < -6) return;
-    int tile, half;
-    g8_target(k, tile, half);
-    if (tile >= nk) return;
+  auto issue_half = [&](int tile, int half) {
     char* dst = smem + (tile & 1) * G8_BUF + half * G8_HALF;
     const unsigned soff = (unsigned)tile * 128u;
     if constexpr (MX) {
@@ -251,6 +274,13 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, LPTR(dst + (wave + 8) * 1024), 16, b_voff[half - 2][1], soff, 0,
                                                0);
     }
+  };
+  auto issue = [&](int k) {
+    if (k < -6) return;
+    int tile, half;
+    g8_target(k, tile, half);
+    if (tile >= nk) return;
+    issue_half(tile, half);
   };
 
   // fc2 (MXE 2): the bf16 residual rows of the tile go to LDS by DMA -- half 0 during the last K-tile into the
@@ -293,6 +323,32 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, LPTR(dst + wave * 1024), 16, b_voff[half - 2][0], soff, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, LPTR(dst + (wave + 8) * 1024), 16, b_voff[half - 2][1], soff, 0,
                                                0);
+    }
+  };
+
+  // PH2 steady issue (t + 2 < nk), branch-free as issue_steady: Q0 -> A1(t+1); Q1 -> scales, A0, B0, B1 (t+2)
+  auto issue_steady2 = [&](int t, auto h_c) {
+    constexpr int Hh = decltype(h_c)::value;
+    if constexpr (Hh == 0) {
+      char* dst = smem + ((t + 1) & 1) * G8_BUF + G8_HALF;
+      const unsigned soff = (unsigned)(t + 1) * 128u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, LPTR(dst + wave * 1024), 16, a_voff[1][0], soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, LPTR(dst + (wave + 8) * 1024), 16, a_voff[1][1], soff, 0, 0);
+    } else {
+      const int tile = t + 2;
+      char* dst = smem + (tile & 1) * G8_BUF;
+      const unsigned soff = (unsigned)tile * 128u;
+      if constexpr (MX)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(s_rsrc, LPTR(smem + G8_OPS + (tile & 3) * G8_SC + wave * 256), 4, s_voff,
+                                                 (unsigned)tile * 1024u, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, LPTR(dst + wave * 1024), 16, a_voff[0][0], soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, LPTR(dst + (wave + 8) * 1024), 16, a_voff[0][1], soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, LPTR(dst + 2 * G8_HALF + wave * 1024), 16, b_voff[0][0], soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, LPTR(dst + 2 * G8_HALF + (wave + 8) * 1024), 16, b_voff[0][1], soff,
+                                               0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, LPTR(dst + 3 * G8_HALF + wave * 1024), 16, b_voff[1][0], soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, LPTR(dst + 3 * G8_HALF + (wave + 8) * 1024), 16, b_voff[1][1], soff,
+                                               0, 0);
     }
   };
 
@@ -381,11 +437,57 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  // ---- prologue: phases -6..-1 stage A0(0) B0(0) B1(0) A1(0) A0(1) B0(1)
-  for (int k = -6; k < 0; ++k) issue(k);
-  g8_wait<MX>(-1, nk);
+  // ---- prologue: phases -6..-1 stage A0(0) B0(0) B1(0) A1(0) A0(1) B0(1) (PH2: j = -3..-1, tile 0 and A0 B0 B1 (1))
+  if constexpr (PH2) {
+    for (int j = -3; j < 0; ++j) g8_issue2(j, nk, issue_half);
+    g8_vmcnt_dyn<MX>(g8_count2<MX>(-1, nk));
+  } else {
+    for (int k = -6; k < 0; ++k) issue(k);
+    g8_wait<MX>(-1, nk);
+  }
   g8_barrier();
   if (wm == 1) g8_barrier();   // group 1 runs one barrier behind
+
+  // PH2: the K-tile in two phases of 32 MFMAs (same accumulation order per accumulator: bit-identical)
+  auto run_tile2 = [&](int t, auto mode_c) {
+    constexpr int MODE = decltype(mode_c)::value;
+    const char* buf = smem + (t & 1) * G8_BUF;
+    const int j = 2 * t;
+    const int xr = (RBP && MODE == 0 && t == nk - 1) ? 8 : 0;
+    if (xr) res_dma(0, nk & 1);
+    auto issue_wait = [&](auto h_c) {
+      constexpr int Hh = decltype(h_c)::value;
+      if constexpr (MODE == 1) {
+        if constexpr (DBG != 5) issue_steady2(t, h_c);
+        if constexpr (MX) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        g8_issue2(j + Hh, nk, issue_half);
+        g8_vmcnt_dyn<MX>(g8_count2<MX>(j + Hh, nk) + xr);
+      }
+    };
+    const std::integral_constant<int, 0> ni0;
+    const std::integral_constant<int, 1> ni1;
+    // Q0: (mi 0) reads A rows 0-127 and all B columns; A0 B0 then A0 B1
+    read_a(buf);
+    read_b(buf + 2 * G8_HALF, b0f, b0x);
+    read_b(buf + 3 * G8_HALF, b1f, b1x);
+    read_sa(t, 0);
+    read_sb(t);
+    issue_wait(std::integral_constant<int, 0>{});
+    g8_barrier();
+    mma(acc[0][0], b0f, b0x, ni0);
+    mma(acc[0][1], b1f, b1x, ni1);
+    g8_barrier();
+    // Q1: (mi 1) reads A rows 128-255; A1 B1 then A1 B0
+    read_a(buf + G8_HALF);
+    read_sa(t, 1);
+    issue_wait(std::integral_constant<int, 1>{});
+    g8_barrier();
+    mma(acc[1][1], b1f, b1x, ni1);
+    mma(acc[1][0], b0f, b0x, ni0);
+    g8_barrier();
+  };
 
   // steady K-tiles (t + 2 < nk): every phase issues a half and waits vmcnt(8) with no
   // scalar bookkeeping; the last two K-tiles take the counted tail path.
@@ -442,8 +544,13 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmArgs g) {
     g8_barrier();
   };
   int t = 0;
-  for (; t + 2 < nk; ++t) run_tile(t, std::integral_constant<int, 1>{});
-  for (; t < nk; ++t) run_tile(t, std::integral_constant<int, 0>{});
+  if constexpr (PH2) {
+    for (; t + 2 < nk; ++t) run_tile2(t, std::integral_constant<int, 1>{});
+    for (; t < nk; ++t) run_tile2(t, std::integral_constant<int, 0>{});
+  } else {
+    for (; t + 2 < nk; ++t) run_tile(t, std::integral_constant<int, 1>{});
+    for (; t < nk; ++t) run_tile(t, std::integral_constant<int, 0>{});
+  }
   if (wm == 0) g8_barrier();   // balance group 1's extra barrier: every wave's LDS reads are done
   if constexpr (RBP) {
     res_dma(1, (nk - 1) & 1);
@@ -1242,24 +1349,9 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(GemmArgs g, int n_tiles) {
     if (tl >= nk) return;
     issue_half(tl, half);
   };
-  // PH2 schedule (see the template comment): ops per wave issued at 2-phase j, the issue itself, the counted wait
-  auto ops2 = [&](int j) -> int {
-    if (j < -3) return 0;
-    const int t = j >> 1;
-    return (j & 1) == 0 ? (t + 1 < nk ? 2 : 0) : (t + 2 < nk ? 6 : 0);
-  };
-  auto issue2 = [&](int j) {
-    if (j < -3) return;
-    const int t = j >> 1;
-    if ((j & 1) == 0) {
-      if (t + 1 < nk) issue_half(t + 1, 1);
-    } else if (t + 2 < nk) {
-      issue_half(t + 2, 0);
-      issue_half(t + 2, 2);
-      issue_half(t + 2, 3);
-    }
-  };
-  auto count2 = [&](int j) { return ops2(j) + ops2(j - 1); };
+  // PH2 schedule (see the template comment)
+  auto issue2 = [&](int j) { g8_issue2(j, nk, issue_half); };
+  auto count2 = [&](int j) { return g8_count2(j, nk); };
   auto prologue = [&]() {
     if constexpr (PH2) {
       for (int j = -3; j < 0; ++j) issue2(j);
@@ -1674,7 +1766,8 @@ SSE_DEV void g8r_epilogue_rb(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], char* 
 // 37.3 with no epilogue; 7.8 of the 28.6 us were the residual loads, 2.6 the parameter wait.
 // DBG (timing probes only, tools/gemm8_probe.hip; the library launches DBG = 0): 2 = no epilogue (accumulators
 // kept live).
-template <bool LN, bool OPART, bool RB, bool F16 = false, int DBG = 0>
+// PH2: the two-phase K-tile schedule (gemm8p_kernel's template comment; option gemm_4phase = 2 selects it here)
+template <bool LN, bool OPART, bool RB, bool F16 = false, int DBG = 0, bool PH2 = false>
 __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
   // RB: operands | epilogue parameters (9 KiB, staged at kernel start) | row-chunk statistics (8 KiB)
   __shared__ __attribute__((aligned(16))) char smem[RB ? G8R_SMEM_RB : G8_OPS];   // the ONLY shared object
@@ -1716,11 +1809,7 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
         b_voff[h][s] = (unsigned)((long long)row * K * 2 + ch * 16);
       }
   }
-  auto issue = [&](int k) {
-    if (k < -6) return;
-    int tl, half;
-    g8_target(k, tl, half);
-    if (tl >= nk) return;
+  auto issue_half = [&](int tl, int half) {
     char* dst = smem + (tl & 1) * G8_BUF + half * G8_HALF;
     const unsigned soff = (unsigned)tl * 128u;
     if (half < 2) {
@@ -1731,6 +1820,13 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, LPTR(dst + (wave + 8) * 1024), 16, b_voff[half - 2][1], soff, 0,
                                                0);
     }
+  };
+  auto issue = [&](int k) {
+    if (k < -6) return;
+    int tl, half;
+    g8_target(k, tl, half);
+    if (tl >= nk) return;
+    issue_half(tl, half);
   };
   f32x4 acc[2][2][4][2];
   #pragma unroll
@@ -1820,10 +1916,42 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
       }
     }
   };
-  for (int k = -6; k < 0; ++k) issue(k);
-  g8_wait<false>(-1, nk);
+  if constexpr (PH2) {
+    for (int j = -3; j < 0; ++j) g8_issue2(j, nk, issue_half);
+    g8_vmcnt_dyn<false>(g8_count2(-1, nk));
+  } else {
+    for (int k = -6; k < 0; ++k) issue(k);
+    g8_wait<false>(-1, nk);
+  }
   g8_barrier();
   if (wm == 1) g8_barrier();   // group 1 runs one barrier behind
+  // PH2: the K-tile in two phases of 32 MFMAs (same accumulation order per accumulator: bit-identical)
+  auto run_tile2 = [&](int t, auto steady) {
+    constexpr bool ST = decltype(steady)::value;
+    const char* buf = smem + (t & 1) * G8_BUF;
+    const int j = 2 * t;
+    const int xr = (RB && !ST && t == nk - 1) ? 8 : 0;
+    if (xr) res_dma(0, nk & 1);
+    auto issue_wait = [&](int jj) {
+      g8_issue2(jj, nk, issue_half);
+      if constexpr (ST) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else g8_vmcnt_dyn<false>(g8_count2(jj, nk) + xr);
+    };
+    read_a(buf);
+    read_b(buf + 2 * G8_HALF, b0f);
+    read_b(buf + 3 * G8_HALF, b1f);
+    issue_wait(j);
+    g8_barrier();
+    mma(acc[0][0], b0f);
+    mma(acc[0][1], b1f);
+    g8_barrier();
+    read_a(buf + G8_HALF);
+    issue_wait(j + 1);
+    g8_barrier();
+    mma(acc[1][1], b1f);
+    mma(acc[1][0], b0f);
+    g8_barrier();
+  };
   auto run_tile = [&](int t, auto steady) {
     constexpr bool ST = decltype(steady)::value;
     const char* buf = smem + (t & 1) * G8_BUF;
@@ -1858,8 +1986,13 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
     g8_barrier();
   };
   int t = 0;
-  for (; t + 2 < nk; ++t) run_tile(t, std::integral_constant<bool, true>{});
-  for (; t < nk; ++t) run_tile(t, std::integral_constant<bool, false>{});
+  if constexpr (PH2) {
+    for (; t + 2 < nk; ++t) run_tile2(t, std::integral_constant<bool, true>{});
+    for (; t < nk; ++t) run_tile2(t, std::integral_constant<bool, false>{});
+  } else {
+    for (; t + 2 < nk; ++t) run_tile(t, std::integral_constant<bool, true>{});
+    for (; t < nk; ++t) run_tile(t, std::integral_constant<bool, false>{});
+  }
   if (wm == 0) g8_barrier();   // balance group 1's extra barrier: every wave's LDS reads are done
   if constexpr (RB) {
     if constexpr (DBG == 2) {
@@ -2077,6 +2210,25 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
   }
 }
 
+// the residual GEMM in the schedule the options select: four phases per K-tile unless gemm_4phase = 2 (two phases
+// measured level on oproj and 1.5 % slower on ffn2, profiles/r6_ab_gemm_2phase_all.txt)
+template <bool LN, bool OP, bool RB, bool F16 = false>
+void launch_g8r(dim3 grid, hipStream_t s, const GemmArgs& a) {
+  if (sse_opt(OPT_GEMM_4PHASE) != 2)
+    hipLaunchKernelGGL((gemm8r_kernel<LN, OP, RB, F16, 0, false>), grid, dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm8r_kernel<LN, OP, RB, F16, 0, true>), grid, dim3(512), 0, s, a);
+}
+
+// the MX GEMM in the schedule the options select (two phases per K-tile unless gemm_4phase = 1)
+template <bool TR, int MXE = 0>
+void launch_g8mx(dim3 grid, hipStream_t s, const GemmArgs& a) {
+  if (sse_opt(OPT_GEMM_4PHASE) == 1)
+    hipLaunchKernelGGL((gemm8_kernel<0, TR, false, true, MXE, false>), grid, dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm8_kernel<0, TR, false, true, MXE, true>), grid, dim3(512), 0, s, a);
+}
+
 }  // namespace
 
 int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
@@ -2097,7 +2249,7 @@ int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
     if (a.resid_t || a.rstats || a.rpart || a.opart || a.apart || a.resid_rows || a.alpha == 0.f) return -3;
     if (a.resid) {
       if (!a.Cf || a.Ct) return -3;
-      hipLaunchKernelGGL((gemm8r_kernel<false, false, false, true>), grid, dim3(512), 0, s, a);
+      launch_g8r<false, false, false, true>(grid, s, a);
       return hipGetLastError() == hipSuccess ? 0 : -2;
     }
     if (a.ct3 ? (a.act != ACT_GELU || a.Cf) : (a.act != ACT_NONE || !a.Cf || a.Ct)) return -3;
@@ -2109,11 +2261,11 @@ int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
     if (a.resid_t) {
       if (!a.Ct || a.Cf) return -3;
       if (a.rpart) {
-        if (a.opart) hipLaunchKernelGGL((gemm8r_kernel<true, true, true, true>), grid, dim3(512), 0, s, a);
-        else hipLaunchKernelGGL((gemm8r_kernel<true, false, true, true>), grid, dim3(512), 0, s, a);
+        if (a.opart) launch_g8r<true, true, true, true>(grid, s, a);
+        else launch_g8r<true, false, true, true>(grid, s, a);
       } else {
-        if (a.opart) hipLaunchKernelGGL((gemm8r_kernel<false, true, true, true>), grid, dim3(512), 0, s, a);
-        else hipLaunchKernelGGL((gemm8r_kernel<false, false, true, true>), grid, dim3(512), 0, s, a);
+        if (a.opart) launch_g8r<false, true, true, true>(grid, s, a);
+        else launch_g8r<false, false, true, true>(grid, s, a);
       }
       return hipGetLastError() == hipSuccess ? 0 : -2;
     }
@@ -2126,22 +2278,22 @@ int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
     // bf16 residual stream (folded post-LN path): bf16 out only
     if (!a.Ct || a.Cf || a.resid || a.resid_rows || a.rstats) return -3;
     if (a.rpart) {
-      if (a.opart) hipLaunchKernelGGL((gemm8r_kernel<true, true, true>), grid, dim3(512), 0, s, a);
-      else hipLaunchKernelGGL((gemm8r_kernel<true, false, true>), grid, dim3(512), 0, s, a);
+      if (a.opart) launch_g8r<true, true, true>(grid, s, a);
+      else launch_g8r<true, false, true>(grid, s, a);
     } else {
-      if (a.opart) hipLaunchKernelGGL((gemm8r_kernel<false, true, true>), grid, dim3(512), 0, s, a);
-      else hipLaunchKernelGGL((gemm8r_kernel<false, false, true>), grid, dim3(512), 0, s, a);
+      if (a.opart) launch_g8r<false, true, true>(grid, s, a);
+      else launch_g8r<false, false, true>(grid, s, a);
     }
   } else if (a.resid) {
     // residual GEMMs: fp32 out (Cf) required; the rstats form is the staged kernel's only
     if (!a.Cf || a.rstats || (a.opart && !a.rpart && a.rln_w)) {
       hipLaunchKernelGGL((gemm8_kernel<0, false, false>), grid, dim3(512), 0, s, a);
     } else if (a.rpart) {
-      if (a.opart) hipLaunchKernelGGL((gemm8r_kernel<true, true, false>), grid, dim3(512), 0, s, a);
-      else hipLaunchKernelGGL((gemm8r_kernel<true, false, false>), grid, dim3(512), 0, s, a);
+      if (a.opart) launch_g8r<true, true, false>(grid, s, a);
+      else launch_g8r<true, false, false>(grid, s, a);
     } else {
-      if (a.opart) hipLaunchKernelGGL((gemm8r_kernel<false, true, false>), grid, dim3(512), 0, s, a);
-      else hipLaunchKernelGGL((gemm8r_kernel<false, false, false>), grid, dim3(512), 0, s, a);
+      if (a.opart) launch_g8r<false, true, false>(grid, s, a);
+      else launch_g8r<false, false, false>(grid, s, a);
     }
   } else {
     // persistent: one block per CU (LDS-bound), at most one per tile
@@ -2154,7 +2306,7 @@ int launch_gemm8_bf16(const GemmArgs& a, hipStream_t s) {
     const int ncu = sse_stream_cus(s, cus[dev]);   // a CU-masked stream's own CUs
     const int G = n_tiles < ncu ? n_tiles : ncu;
     const int ep = (a.bias ? 1 : 0) | (a.apart ? 2 : 0);
-    const bool ph2 = sse_opt(OPT_GEMM_4PHASE) == 0;   // two phases per K-tile (round 6 default)
+    const bool ph2 = sse_opt(OPT_GEMM_4PHASE) != 1;   // two phases per K-tile (round 6 default)
     auto go2 = [&](auto act, auto ct3, auto f16, auto p2) {
       constexpr int AC = decltype(act)::value;
       constexpr bool C3 = decltype(ct3)::value, F = decltype(f16)::value, P2 = decltype(p2)::value;
@@ -2227,7 +2379,7 @@ int launch_gemm8_mx(const GemmArgs& a, hipStream_t s) {
     if (!plain || a.resid_t || a.act != ACT_NONE || !a.c_scale || !a.c_scale_rm || !a.vamax || !a.ct2 ||
         a.vamax_rows < 64 || a.n_split % 256 || a.n_split >= a.N || a.ldc != a.n_split || a.ldc2 < a.N - a.n_split)
       return -3;
-    hipLaunchKernelGGL((gemm8_kernel<0, true, false, true, 6>), grid, dim3(512), 0, s, a);
+    launch_g8mx<true, 6>(grid, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
   }
   if (a.c_scale_rm || a.vamax) {
@@ -2235,26 +2387,26 @@ int launch_gemm8_mx(const GemmArgs& a, hipStream_t s) {
         (a.vamax && a.vamax_rows < 64))
       return -3;
     if (a.c_scale_rm)
-      hipLaunchKernelGGL((gemm8_kernel<0, true, false, true, 4>), grid, dim3(512), 0, s, a);
+      launch_g8mx<true, 4>(grid, s, a);
     else
-      hipLaunchKernelGGL((gemm8_kernel<0, true, false, true, 5>), grid, dim3(512), 0, s, a);
+      launch_g8mx<true, 5>(grid, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
   }
   if (direct && !sse_opt(OPT_GEMM_MX_STAGED)) {
     if (a.resid_t) {   // (direct implies Ct, no Cf / fp8 out / LayerNorm)
       // fc2's compile-time epilogue (MXE 2) is bias + residual, no activation; any other bias / act combination
       // takes the staged epilogue, which reads both at run time
-      if (a.bias && a.act == ACT_NONE) hipLaunchKernelGGL((gemm8_kernel<0, true, false, true, 2>), grid, dim3(512), 0, s, a);
-      else hipLaunchKernelGGL((gemm8_kernel<0, false, false, true>), grid, dim3(512), 0, s, a);
+      if (a.bias && a.act == ACT_NONE) launch_g8mx<true, 2>(grid, s, a);
+      else launch_g8mx<false>(grid, s, a);
     }
     else if (plain && a.c_scale && a.act == ACT_GELU_FAST)   // fc1
-      hipLaunchKernelGGL((gemm8_kernel<0, true, false, true, 1>), grid, dim3(512), 0, s, a);
+      launch_g8mx<true, 1>(grid, s, a);
     else if (plain && !a.c_scale && a.act == ACT_NONE)      // qkv
-      hipLaunchKernelGGL((gemm8_kernel<0, true, false, true, 3>), grid, dim3(512), 0, s, a);
+      launch_g8mx<true, 3>(grid, s, a);
     else
-      hipLaunchKernelGGL((gemm8_kernel<0, true, false, true>), grid, dim3(512), 0, s, a);
+      launch_g8mx<true>(grid, s, a);
   } else {
-    hipLaunchKernelGGL((gemm8_kernel<0, false, false, true>), grid, dim3(512), 0, s, a);
+    launch_g8mx<false>(grid, s, a);
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
