@@ -331,8 +331,8 @@ const char* sse_version(void);
  *   "gemm_cfg"          1 = no 256x256 tile, 2 = 256x128 3-stage ring, 3 = 2-stage 256x256 kernel
  *   "gemm_nonpersist"   1 = non-persistent 8-phase bf16 GEMM for every shape
  *   "gemm_4phase"       8-wave GEMM K-tile schedule, bit-identical outputs: 0 = two 32-MFMA phases in the persistent
- *                       and MX GEMMs, four in the residual GEMM (round 6 default); 1 = four 16-MFMA phases everywhere
- *                       (rounds 1-5); 2 = two phases everywhere
+ *                       and MX GEMMs and the residual GEMM at N > 768, four there at N <= 768 (round 6 default);
+ *                       1 = four 16-MFMA phases everywhere (rounds 1-5); 2 = two phases everywhere
  *   "gelu_exact"        1 = erf-GELU in the bf16 path's epilogues
  *   "conv0_valu"        1 = VALU conv0 + GroupNorm kernel instead of the matrix-core one
  *   "posconv_gemm"      1 = grouped GEMM for the bf16 positional conv

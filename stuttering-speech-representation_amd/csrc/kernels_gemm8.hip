@@ -2210,11 +2210,13 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
   }
 }
 
-// the residual GEMM in the schedule the options select: four phases per K-tile unless gemm_4phase = 2 (two phases
-// measured level on oproj and 1.5 % slower on ffn2, profiles/r6_ab_gemm_2phase_all.txt)
+// the residual GEMM in the schedule the options select: by default two phases per K-tile for N > 768 (Whisper-large-v2
+// bf16 fc2 32.4 -> 31.5, WavLM-large fc2 7.22 -> 7.03 ms/step) and four at N <= 768 (WavLM-base: oproj level, fc2
+// 1.5 % slower with two; profiles/r6_ab_gemm_2phase_all.txt, r6_ab_gemm_2phase_residual.txt); gemm_4phase 1 / 2 force
 template <bool LN, bool OP, bool RB, bool F16 = false>
 void launch_g8r(dim3 grid, hipStream_t s, const GemmArgs& a) {
-  if (sse_opt(OPT_GEMM_4PHASE) != 2)
+  const int o = sse_opt(OPT_GEMM_4PHASE);
+  if (o == 1 || (o == 0 && a.N <= 768))
     hipLaunchKernelGGL((gemm8r_kernel<LN, OP, RB, F16, 0, false>), grid, dim3(512), 0, s, a);
   else
     hipLaunchKernelGGL((gemm8r_kernel<LN, OP, RB, F16, 0, true>), grid, dim3(512), 0, s, a);
