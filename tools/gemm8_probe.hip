@@ -312,18 +312,23 @@ __global__ void fill_bf16(bf16* p, long long n, unsigned seed, float scale) {
 
 typedef void (*kfn)(GemmArgs, int);
 
+static bool g_ph2 = true;   // round 6: the library's two-phase K-tile schedule (argument "4": the four-phase one)
+template <int ACT, int EP, bool P2>
+static kfn pick2(int dbg) {
+  switch (dbg) {
+    case 1: return gemm8p_kernel<ACT, false, false, EP, 1, 3, P2>;
+    case 2: return gemm8p_kernel<ACT, false, false, EP, 2, 3, P2>;
+    case 3: return gemm8p_kernel<ACT, false, false, EP, 3, 3, P2>;
+    case 4: return gemm8p_kernel<ACT, false, false, EP, 4, 3, P2>;
+    case 5: return gemm8p_kernel<ACT, false, false, EP, 5, 3, P2>;
+    case 6: return gemm8p_kernel<ACT, false, false, EP, 6, 3, P2>;
+    case 7: return gemm8p_kernel<ACT, false, false, EP, 7, 3, P2>;
+    default: return gemm8p_kernel<ACT, false, false, EP, 0, 3, P2>;
+  }
+}
 template <int ACT, int EP>
 static kfn pick(int dbg) {
-  switch (dbg) {
-    case 1: return gemm8p_kernel<ACT, false, false, EP, 1>;
-    case 2: return gemm8p_kernel<ACT, false, false, EP, 2>;
-    case 3: return gemm8p_kernel<ACT, false, false, EP, 3>;
-    case 4: return gemm8p_kernel<ACT, false, false, EP, 4>;
-    case 5: return gemm8p_kernel<ACT, false, false, EP, 5>;
-    case 6: return gemm8p_kernel<ACT, false, false, EP, 6>;
-    case 7: return gemm8p_kernel<ACT, false, false, EP, 7>;
-    default: return gemm8p_kernel<ACT, false, false, EP, 0>;
-  }
+  return g_ph2 ? pick2<ACT, EP, true>(dbg) : pick2<ACT, EP, false>(dbg);
 }
 
 typedef void (*kfr)(GemmArgs);
@@ -362,6 +367,8 @@ static int half_tiles(int argc, char** argv);
 
 int main(int argc, char** argv) {
   if (argc > 1 && argv[1][0] == 'h') return half_tiles(argc, argv);
+  if (argc > 1 && argv[1][0] == '4') g_ph2 = false;
+  printf("persistent GEMM schedule: %s phases per K-tile\n", g_ph2 ? "two" : "four");
   int cus = 256;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const Shape shapes[] = {
