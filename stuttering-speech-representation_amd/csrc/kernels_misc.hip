@@ -59,8 +59,10 @@ constexpr int NMOM = K0 + NG;            // 65 moments per clip
 // One block per (clip, frame chunk): a clip's frames in MOM_NCH chunks, each block's partial moments
 // written to mom[b][chunk]; gn_finalize sums the chunks in chunk order (deterministic, and every clip's
 // result independent of the batch).  One block per clip walked ~38 dependent load rounds per thread
-// (latency-bound, 72 us at B = 128 while the GPU was otherwise idle at the step's start).
-constexpr int MOM_NCH = 8;
+// (latency-bound, 72 us at B = 128 while the GPU was otherwise idle at the step's start); 8 chunks spent
+// most of their time in the 65 fp64 wave reductions per block (~5 frames per thread): 2 chunks (~19 frames per
+// thread) took the conv0 + GroupNorm role 0.633 -> 0.576 ms/step at B = 256 (round 6, profiles/r6_ab_conv0_moments.txt).
+constexpr int MOM_NCH = 2;
 
 __global__ __launch_bounds__(256) void conv0_moments_kernel(const float* __restrict__ x, int L,
                                                             const float* __restrict__ norm, int s0, int T0S,
