@@ -21,6 +21,10 @@
 //    buffer (tile & 1).  Every half is issued >= 5 phases before its first read and after the
 //    barrier that follows the last lgkmcnt of its previous occupant; a uniform vmcnt(8) at the
 //    end of each L-section (fewer in the tail) retires what the next phase reads.
+//  * Round 6 (the default for the persistent and MX kernels, and the residual kernel at N > 768; option
+//    gemm_4phase): the same K-tile in TWO phases of 32 MFMAs -- Q0 reads A0, B0, B1 (A0 B0, A0 B1), Q1 reads A1
+//    (A1 B1, A1 B0) -- half the barriers, bit-identical; issue schedule Q0(t) -> A1(t+1), Q1(t) -> A0, B0, B1(t+2)
+//    (g8_ops2 / g8_count2 / g8_issue2; DESIGN.md "Two phases per K-tile").
 //
 // MX = true: MX-fp8 operands (OCP e4m3 + E8M0 per 32 K-elements, v_mfma_scale_f32_16x16x128_f8f6f4,
 // 2x the bf16 MFMA rate).  A K-tile is still 128 B per row (128 elements), the LDS image and the
