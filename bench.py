@@ -172,8 +172,8 @@ def cpu_baseline(model_name: str, n: int, seconds: float):
 
 # rocprofv3 PMC traffic per kernel (tools/pmc_traffic.sh: FETCH_SIZE x2 + WRITE_SIZE per launch),
 # measured on the same workload; kernel symbols of each bench tag prefix
-TRAFFIC_FILE = {("wavlm-base", "bf16"): "profiles/r6_pmc_traffic_wavlm_base_bf16.json",
-                ("whisper-large-v2", "fp8"): "profiles/r6_pmc_traffic_whisper_large_v2_fp8.json"}
+TRAFFIC_FILE = {("wavlm-base", "bf16"): "profiles/r6_pmc_traffic_wavlm_base_bf16_final2.json",
+                ("whisper-large-v2", "fp8"): "profiles/r6_pmc_traffic_whisper_large_v2_fp8_final2.json"}
 TAG_SYMBOLS = {"gemm": ("gemm8_kernel<0, false, false, false>", "gemm8p_kernel", "gemm8r_kernel"),
                # (round 5: the compile-time epilogue forms gemm8_kernel<0, true, false, true, MXE>)
                "gemm_mx": ("gemm8_kernel<0, true, false, true", "gemm8_kernel<0, false, false, true"),
