@@ -9,6 +9,7 @@ attention operands rounded the way a GPU path stores them, products accumulated 
                oracle/mx.py's rule), out-projection and convs bf16 -- the SSE_DTYPE_FP8 path
   oproj        bf16 (default) | mx8: the out-projection's operands MX-fp8 too (option f8_oproj = 1, round 6)
   stream bf16  residual stream and the qkv / context outputs rounded to bf16 where the path stores them
+               (--stream res32: the residual stream kept fp32, the others bf16; fp32: nothing rounded)
   attn         bf16     Q, K, V, P bf16 (the shipped attention)
                qk8      Q.K^T on MX-fp8 operands (blocks of 32 along the head dim), P.V bf16
                qk8pv8t  + P e4m3 (unscaled, p <= 1) and V MX-fp8 along the KEY axis (blocks of 32 keys)
@@ -123,12 +124,13 @@ GELU_FP8 = {   # tools/fit_gelu.py fits: (clamp, coefficients highest degree fir
 
 def hidden_states(spec, p, mel, gemm="mx8", attn="bf16", stream="bf16", gelu_fc1="exact", oproj="bf16"):
     eps, nh, hd = spec.ln_eps, spec.heads, spec.head_dim
-    rnd = _bf if stream == "bf16" else (lambda t: t)
+    rnd = _bf if stream in ("bf16", "res32") else (lambda t: t)     # qkv / context outputs
+    rx = _bf if stream == "bf16" else (lambda t: t)                  # the residual stream (res32: fp32)
     cf = "bf16" if gemm != "fp32" else "fp32"
     x = mel.T
     x = _gelu(_conv(x, p["encoder.conv1.weight"], p["encoder.conv1.bias"], 1, cf))
     x = _gelu(_conv(x, p["encoder.conv2.weight"], p["encoder.conv2.bias"], 2, cf))
-    x = rnd(x + p["encoder.embed_positions.weight"][: x.shape[0]])
+    x = rx(x + p["encoder.embed_positions.weight"][: x.shape[0]])
     hs = [x]
     T = x.shape[0]
     for l in range(spec.layers):
@@ -140,11 +142,11 @@ def hidden_states(spec, p, mel, gemm="mx8", attn="bf16", stream="bf16", gelu_fc1
         v = rnd(_lin(h, p[f"{s_}.v_proj.weight"], gemm) + p[f"{s_}.v_proj.bias"])
         qh, kh, vh = (t.reshape(T, nh, hd).transpose(0, 1) for t in (q, k, v))
         ctx = rnd(_attn(qh, kh, vh, attn).transpose(0, 1).reshape(T, nh * hd))
-        x = rnd(x + _lin(ctx, p[f"{s_}.out_proj.weight"], oproj if gemm == "mx8" else cf) + p[f"{s_}.out_proj.bias"])
+        x = rx(x + _lin(ctx, p[f"{s_}.out_proj.weight"], oproj if gemm == "mx8" else cf) + p[f"{s_}.out_proj.bias"])
         h = _ln(x, p[f"{a}.final_layer_norm.weight"], p[f"{a}.final_layer_norm.bias"], eps)
         h = _lin(h, p[f"{a}.fc1.weight"], gemm) + p[f"{a}.fc1.bias"]
         h = _gelu(h) if gelu_fc1 == "exact" else _gelu_poly(h, *GELU_FP8[gelu_fc1])
-        x = rnd(x + _lin(h, p[f"{a}.fc2.weight"], gemm) + p[f"{a}.fc2.bias"])
+        x = rx(x + _lin(h, p[f"{a}.fc2.weight"], gemm) + p[f"{a}.fc2.bias"])
         hs.append(x)
     hs[-1] = _ln(x, p["encoder.layer_norm.weight"], p["encoder.layer_norm.bias"], eps)
     return hs
@@ -156,6 +158,7 @@ def main() -> None:
     ap.add_argument("--gemm", default="mx8")
     ap.add_argument("--gelu", default="exact", help="fc1 GELU: exact | deg5 | deg3 | deg2 (the fp8-out polynomials)")
     ap.add_argument("--oproj", default="bf16", help="out-projection operands with --gemm mx8: bf16 | mx8")
+    ap.add_argument("--stream", default="bf16", help="bf16 | res32 | fp32 (see the module docstring)")
     ap.add_argument("--threads", type=int, default=os.cpu_count())
     ap.add_argument("--out", default="")
     a = ap.parse_args()
@@ -170,11 +173,11 @@ def main() -> None:
     res = {}
     with torch.no_grad():
         for attn in a.attn.split(","):
-            hs = hidden_states(spec, p, mel, a.gemm, attn, gelu_fc1=a.gelu, oproj=a.oproj)
+            hs = hidden_states(spec, p, mel, a.gemm, attn, stream=a.stream, gelu_fc1=a.gelu, oproj=a.oproj)
             got = np.stack([hs[i].mean(0).numpy() for i in idx])
             rel = np.linalg.norm(got - ref, axis=-1) / np.linalg.norm(ref, axis=-1)
             cos = (got * ref).sum(-1) / (np.linalg.norm(got, axis=-1) * np.linalg.norm(ref, axis=-1))
-            key = f"{a.gemm}/{attn}/{a.gelu}/oproj-{a.oproj}"
+            key = f"{a.gemm}/{attn}/{a.gelu}/oproj-{a.oproj}/stream-{a.stream}"
             res[key] = {"rel_l2_max": float(rel.max()), "cos_min": float(cos.min())}
             print(key, json.dumps(res[key]), flush=True)
     if a.out:
