@@ -330,9 +330,8 @@ const char* sse_version(void);
  * reads the environment).  Process-wide; 0 is the production choice for every name:
  *   "gemm_cfg"          1 = no 256x256 tile, 2 = 256x128 3-stage ring, 3 = 2-stage 256x256 kernel
  *   "gemm_nonpersist"   1 = non-persistent 8-phase bf16 GEMM for every shape
- *   "gemm_4phase"       8-wave GEMM K-tile schedule, bit-identical outputs: 0 = two 32-MFMA phases in the persistent
- *                       and MX GEMMs and the residual GEMM at N > 768, four there at N <= 768 (round 6 default);
- *                       1 = four 16-MFMA phases everywhere (rounds 1-5); 2 = two phases everywhere
+ *   "gemm_4phase"       8-wave GEMM K-tile schedule, bit-identical outputs: 0 = two 32-MFMA phases per K-tile (round 6
+ *                       default), 1 = four 16-MFMA phases (rounds 1-5)
  *   "gelu_exact"        1 = erf-GELU in the bf16 path's epilogues
  *   "conv0_valu"        1 = VALU conv0 + GroupNorm kernel instead of the matrix-core one
  *   "posconv_gemm"      1 = grouped GEMM for the bf16 positional conv
@@ -355,8 +354,7 @@ const char* sse_version(void);
  *   "f8_oproj"          1 = the fp8 Whisper path's attention writes MX-fp8 and its out-projection runs on the MX
  *                       GEMM (opt-in: Whisper-large-v2 then misses the fp8 bar, 0.083 vs 0.08 rel-L2)
  * sse_set_option returns the previous value (>= 0), or SSE_ERR_INVALID for an unknown name or a value outside
- * the switch's range (0..1; gemm_cfg 0..3, attn_short 0..2, attn_long 0..2, split_cumask 0..2,
- * gemm_4phase 0..2) -- nothing is changed then. */
+ * the switch's range (0..1; gemm_cfg 0..3, attn_short 0..2, attn_long 0..2, split_cumask 0..2) -- nothing is changed then. */
 int sse_set_option(const char* name, int value);
 int sse_get_option(const char* name);
 

@@ -285,9 +285,8 @@ enum {
                         // 2 the same with one; 1 the 16x16 flash2 kernel
   OPT_FP8_ATTN_BF16,    // 1: the fp8 (MX) Whisper path keeps the bf16 QKV output and the bf16 flash attention
   OPT_SPLIT_CUMASK,     // two-stream split on CU-masked streams: 1 = CUs [0, n/2) | [n/2, n), 2 = even | odd CUs
-  OPT_GEMM_4PHASE,      // 8-wave GEMM K-tile schedule (bit-identical): 0 = two 32-MFMA phases in the persistent and
-                        // MX GEMMs and the residual GEMM at N > 768, four 16-MFMA phases in the residual GEMM at
-                        // N <= 768 (default); 1 = four phases everywhere (rounds 1-5); 2 = two phases everywhere
+  OPT_GEMM_4PHASE,      // 8-wave GEMM K-tile schedule (bit-identical): 0 = two 32-MFMA phases per K-tile (default since
+                        // round 6), 1 = four 16-MFMA phases (rounds 1-5)
   OPT_F8_OPROJ,         // 1: the fp8 (MX) Whisper path's out-projection on the MX GEMM (MX-fp8 attention output);
                         // opt-in: large-v2 at B = 128 then misses the 0.08 rel-L2 bar (0.083)
   OPT_COUNT

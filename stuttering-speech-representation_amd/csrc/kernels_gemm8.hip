@@ -21,8 +21,7 @@
 //    buffer (tile & 1).  Every half is issued >= 5 phases before its first read and after the
 //    barrier that follows the last lgkmcnt of its previous occupant; a uniform vmcnt(8) at the
 //    end of each L-section (fewer in the tail) retires what the next phase reads.
-//  * Round 6 (the default for the persistent and MX kernels, and the residual kernel at N > 768; option
-//    gemm_4phase): the same K-tile in TWO phases of 32 MFMAs -- Q0 reads A0, B0, B1 (A0 B0, A0 B1), Q1 reads A1
+//  * Round 6 (the default for all three 8-wave kernels; option gemm_4phase = 1 keeps four phases): the same K-tile in TWO phases of 32 MFMAs -- Q0 reads A0, B0, B1 (A0 B0, A0 B1), Q1 reads A1
 //    (A1 B1, A1 B0) -- half the barriers, bit-identical; issue schedule Q0(t) -> A1(t+1), Q1(t) -> A0, B0, B1(t+2)
 //    (g8_ops2 / g8_count2 / g8_issue2; DESIGN.md "Two phases per K-tile").
 //
@@ -1770,7 +1769,7 @@ SSE_DEV void g8r_epilogue_rb(const GemmArgs& g, f32x4 (&acc)[2][2][4][2], char* 
 // 37.3 with no epilogue; 7.8 of the 28.6 us were the residual loads, 2.6 the parameter wait.
 // DBG (timing probes only, tools/gemm8_probe.hip; the library launches DBG = 0): 2 = no epilogue (accumulators
 // kept live).
-// PH2: the two-phase K-tile schedule (gemm8p_kernel's template comment; option gemm_4phase = 2 selects it here)
+// PH2: the two-phase K-tile schedule (gemm8p_kernel's template comment; the default, option gemm_4phase = 1 keeps four)
 template <bool LN, bool OPART, bool RB, bool F16 = false, int DBG = 0, bool PH2 = false>
 __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
   // RB: operands | epilogue parameters (9 KiB, staged at kernel start) | row-chunk statistics (8 KiB)
@@ -2214,13 +2213,13 @@ __global__ __launch_bounds__(512) void gemm8r_kernel(GemmArgs g) {
   }
 }
 
-// the residual GEMM in the schedule the options select: by default two phases per K-tile for N > 768 (Whisper-large-v2
-// bf16 fc2 32.4 -> 31.5, WavLM-large fc2 7.22 -> 7.03 ms/step) and four at N <= 768 (WavLM-base: oproj level, fc2
-// 1.5 % slower with two; profiles/r6_ab_gemm_2phase_all.txt, r6_ab_gemm_2phase_residual.txt); gemm_4phase 1 / 2 force
+// the residual GEMM in the schedule the options select: two phases per K-tile unless gemm_4phase = 1 (Whisper-large-v2
+// bf16 fc2 32.4 -> 31.5, WavLM-large fc2 7.22 -> 7.03 ms/step; at WavLM-base's N = 768 one box measured fc2 1.5 %
+// slower, another 2.7 % faster and oproj 1.2 % faster: profiles/r6_ab_gemm_2phase_all.txt, r6_ab_gemm_2phase_residual.txt,
+// r6_ab_gemm_2phase_residual_n768.txt)
 template <bool LN, bool OP, bool RB, bool F16 = false>
 void launch_g8r(dim3 grid, hipStream_t s, const GemmArgs& a) {
-  const int o = sse_opt(OPT_GEMM_4PHASE);
-  if (o == 1 || (o == 0 && a.N <= 768))
+  if (sse_opt(OPT_GEMM_4PHASE) == 1)
     hipLaunchKernelGGL((gemm8r_kernel<LN, OP, RB, F16, 0, false>), grid, dim3(512), 0, s, a);
   else
     hipLaunchKernelGGL((gemm8r_kernel<LN, OP, RB, F16, 0, true>), grid, dim3(512), 0, s, a);

@@ -38,7 +38,7 @@ static const char* const g_opt_name[OPT_COUNT] = {"gemm_cfg", "gemm_nonpersist",
                                                    "attn_short", "attn_long", "fp8_attn_bf16", "split_cumask",
                                                    "gemm_4phase", "f8_oproj"};
 // the largest value each switch takes (0 .. max; anything else is SSE_ERR_INVALID, not a silent default)
-static const int g_opt_max[OPT_COUNT] = {3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 1, 2, 2, 1};
+static const int g_opt_max[OPT_COUNT] = {3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 1, 2, 1, 1};
 int sse_opt(int id) { return __atomic_load_n(&g_opt[id], __ATOMIC_RELAXED); }
 
 // CU-masked streams (split_forward, OPT_SPLIT_CUMASK) and their CU counts; registered once, never removed

@@ -20,7 +20,7 @@ for spec, dtype, B, L in ((C.WAVLM_BASE, "bf16", 7, 48000), (C.WAVLM_BASE, "fp16
     w = torch.from_numpy(synth.synth_clips(B, L, seed=B)).cuda()
     idx = spec.default_layer_indices()
     a = m.embed(w, idx)
-    for v in (1, 2):
+    for v in (1,):
         with _lib.option("gemm_4phase", v):
             b = m.embed(w, idx)
         same = bool(torch.equal(a, b))
