@@ -1,4 +1,4 @@
-# Round 6: residual GEMM in two phases (gemm_4phase = 2) vs the default on the other lines
+# Round 6: residual GEMM in two phases (default) vs four phases (gemm_4phase = 1) on the other lines
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -10,7 +10,7 @@ run() {   # tag, args
 }
 TAG=$1
 for r in 1 2; do
-  for o in 0 2; do
+  for o in 1 0; do
     run f8_o$o --model whisper-large-v2 --dtype fp8 --steps 5 --warmup 2 --opt gemm_4phase=$o || exit 1
     run wb_o$o --model whisper-large-v2 --steps 5 --warmup 2 --opt gemm_4phase=$o || exit 1
     run lg_o$o --model wavlm-large --steps 10 --opt gemm_4phase=$o || exit 1
